@@ -1,0 +1,265 @@
+/*
+ * fwsim.h -- C ABI of libfwsim.so, the MI355X-native batched fixed-wing stepper.
+ *
+ * One handle = one GPU = N independent aircraft ("envs"), state kept resident
+ * in HBM as structure-of-arrays (SoA, one lane per aircraft).  Every call is
+ * asynchronous on the given HIP stream (`void* stream` is a hipStream_t; NULL =
+ * the null stream).  All functions return 0 on success and a negative FW_E_*
+ * code on error; fw_last_error() returns the message of the last error on the
+ * calling thread.  No C++ exception crosses this boundary.
+ *
+ * Device pointers passed in are plain device addresses (e.g. a torch tensor's
+ * data_ptr() on the handle's device).  Element type of every floating-point
+ * buffer is the handle's precision: float (FW_F32) or double (FW_F64).
+ *
+ * Reference interfaces replaced (paths relative to the reference checkout):
+ *   fw_create       PyFly.__init__            magpie/libs/pyfly/pyfly/pyfly.py:1054-1249
+ *                   FixedWingAircraft.__init__ magpie/libs/fixed-wing-gym/gym_fixed_wing/fixed_wing.py:14-306
+ *   fw_seed         PyFly.seed / FixedWingAircraft.seed   pyfly.py:1251-1260, fixed_wing.py:324-332
+ *   fw_reset        PyFly.reset               pyfly.py:1262-1311
+ *                   FixedWingAircraft.reset   fixed_wing.py:414-481
+ *   fw_sim_step     PyFly.step                pyfly.py:1358-1420
+ *   fw_env_step     FixedWingAircraft.step    fixed_wing.py:483-628, plus the
+ *                   SubprocVecEnv worker's auto-reset + terminal_observation
+ *                   (stable_baselines3/common/vec_env/subproc_vec_env.py:25-31)
+ *                   and Monitor episode statistics (common/monitor.py:88-115)
+ *   fw_get_state /  PyFly.state[name].value reads / writes (pyfly.py:1422-1430)
+ *   fw_set_state
+ */
+#ifndef FWSIM_H
+#define FWSIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FWSIM_ABI_VERSION 1
+
+/* ---- error codes ---------------------------------------------------------- */
+#define FW_OK 0
+#define FW_E_INVALID (-1)   /* bad argument / config */
+#define FW_E_HIP (-2)       /* HIP runtime error */
+#define FW_E_UNSUPPORTED (-3)
+#define FW_E_NOMEM (-4)
+
+/* ---- precision -------------------------------------------------------------- */
+#define FW_F32 0
+#define FW_F64 1
+
+/* ---- ODE state vector (pyfly.py:1372-1389 ordering) -------------------------
+ * [e0 e1 e2 e3 | p q r | n e d | u v w | act0 act1 act2 | act0' act1' act2']
+ * act* are the *dynamics* actuators in config order (elevon_right, elevon_left,
+ * throttle for the X8).                                                        */
+#define FW_NY 19
+
+/* ---- variable slots with limits / constraints (pyfly.py:114-133, 312-328) --- */
+enum fw_var {
+  FW_V_ROLL = 0, FW_V_PITCH, FW_V_YAW,
+  FW_V_OMEGA_P, FW_V_OMEGA_Q, FW_V_OMEGA_R,
+  FW_V_POS_N, FW_V_POS_E, FW_V_POS_D,
+  FW_V_VEL_U, FW_V_VEL_V, FW_V_VEL_W,
+  FW_V_VA, FW_V_ALPHA, FW_V_BETA,
+  FW_V_ACT0, FW_V_ACT1, FW_V_ACT2,       /* dynamics actuators (value limits) */
+  FW_V_ELEVATOR, FW_V_AILERON, FW_V_THROTTLE, /* model-input actuator states */
+  FW_NVAR
+};
+
+/* termination codes: 0 = none, 1 + fw_var = ConstraintException on that variable,
+ * FW_TERM_STEPS / FW_TERM_SUCCESS = env terminations (fixed_wing.py:519-559)     */
+#define FW_TERM_NONE 0
+#define FW_TERM_VAR(v) (1 + (v))
+#define FW_TERM_STEPS 100
+#define FW_TERM_SUCCESS 101
+
+/* ---- aircraft parameters (x8_param.mat keys) ------------------------------ */
+enum fw_param {
+  FW_P_MASS = 0, FW_P_JX, FW_P_JY, FW_P_JZ, FW_P_JXZ,
+  FW_P_S_WING, FW_P_B, FW_P_C, FW_P_S_PROP, FW_P_C_PROP,
+  FW_P_K_MOTOR, FW_P_K_T_P, FW_P_K_OMEGA, FW_P_E, FW_P_M, FW_P_A0,
+  FW_P_C_L_0, FW_P_C_L_ALPHA, FW_P_C_L_Q, FW_P_C_L_DELTA_E,
+  FW_P_C_D_P, FW_P_C_D_Q, FW_P_C_D_BETA1, FW_P_C_D_BETA2, FW_P_C_D_DELTA_E,
+  FW_P_C_M_0, FW_P_C_M_ALPHA, FW_P_C_M_Q, FW_P_C_M_DELTA_E, FW_P_C_M_FP,
+  FW_P_C_Y_0, FW_P_C_Y_BETA, FW_P_C_Y_P, FW_P_C_Y_R, FW_P_C_Y_DELTA_A, FW_P_C_Y_DELTA_R,
+  FW_P_C_L0_ROLL, FW_P_C_L_BETA, FW_P_C_L_P, FW_P_C_L_R, FW_P_C_L_DELTA_A, FW_P_C_L_DELTA_R,
+  FW_P_C_N_0, FW_P_C_N_BETA, FW_P_C_N_P, FW_P_C_N_R, FW_P_C_N_DELTA_A, FW_P_C_N_DELTA_R,
+  FW_NPARAM
+};
+
+/* Variable limits.  "None" in the reference is +-INFINITY here. */
+typedef struct fw_limits {
+  double value_min, value_max;           /* clip */
+  double constraint_min, constraint_max; /* raise -> termination */
+  double init_min, init_max;             /* uniform reset sampling */
+  int32_t wrap;                          /* +-pi wrap (pyfly.py:130-131) */
+  int32_t pad_;
+} fw_limits;
+
+/* Actuator dynamics (ControlVariable, pyfly.py:264-310). */
+typedef struct fw_actuator {
+  int32_t order;    /* 1 or 2 */
+  int32_t pad_;
+  double tau;       /* order 1 */
+  double omega_0;   /* order 2 */
+  double zeta;      /* order 2 */
+  double dot_max;   /* +inf = None */
+} fw_actuator;
+
+/* Simulator configuration (pyfly_config.json + x8_param.mat after config_kw
+ * overrides).  Built by the host from the reference-format JSON files.        */
+typedef struct fw_sim_config {
+  double dt, rho, g;
+  double rtol, atol;                 /* solve_ivp defaults 1e-3 / 1e-6 */
+  double param[FW_NPARAM];
+  fw_limits lim[FW_NVAR];
+  fw_actuator act[3];                /* dynamics actuators, dynamics order */
+  int32_t elevon;                    /* 1: dynamics = (elevon_right, elevon_left, throttle) */
+  int32_t disabled_inputs;           /* bit0 elevator, bit1 aileron: "disabled" ControlVariables,
+                                        whose .value is 0 after reset (pyfly.py:359-363) */
+  int32_t wind_random;               /* 1: steady wind magnitude sampled in [mag_min, mag_max] */
+  int32_t pad0_;
+  double wind_mag_min, wind_mag_max;
+  double wind_init_min[3], wind_init_max[3]; /* per-component sampling when !wind_random */
+  int32_t turbulence;              /* Dryden on/off */
+  int32_t turb_len;                  /* chunk length L (turbulence_sim_length) */
+  double dryden_g0[6], dryden_g1[6]; /* FIR taps, channels (u v w p q r) */
+} fw_sim_config;
+
+/* ---- gym env configuration (fixed_wing_config.json) ------------------------ */
+#define FW_MAX_OBS 32
+#define FW_MAX_REW 8
+#define FW_MAX_WINDOW 16
+
+/* observation entry kinds (fixed_wing.py:1149-1234) */
+#define FW_OBS_STATE 0          /* var = fw_var (roll..beta, omega, pos, vel, act states) */
+#define FW_OBS_TARGET_ABS 1     /* var = target index 0..2 (roll, pitch, Va) */
+#define FW_OBS_TARGET_REL 2
+#define FW_OBS_ACTION_WINDOW 3  /* var = action index 0..2 */
+
+typedef struct fw_obs_entry {
+  int32_t kind, var, window, norm;
+  double mean, var_;
+} fw_obs_entry;
+
+/* reward factor kinds (fixed_wing.py:960-1077) */
+#define FW_REW_STATE_ERROR 0    /* var = target index */
+#define FW_REW_STATE_VALUE 1    /* var = fw_var */
+#define FW_REW_ACTION_DELTA 2
+#define FW_REW_ACTION_BOUND 3
+#define FW_REW_ACTION_VALUE 4
+
+#define FW_FUN_LINEAR 0
+#define FW_FUN_QUADRATIC 1
+#define FW_FUN_EXPONENTIAL 2
+
+typedef struct fw_rew_factor {
+  int32_t kind, var, window, fun;
+  int32_t shaping, pad_;
+  double scaling, max, sign;         /* max = +inf if absent */
+} fw_rew_factor;
+
+/* target classes (fixed_wing.py:1363-1471) */
+#define FW_TGT_CONSTANT 0
+#define FW_TGT_COMPENSATE 1
+
+typedef struct fw_env_config {
+  int32_t steps_max;
+  int32_t n_obs;
+  fw_obs_entry obs[FW_MAX_OBS];
+  int32_t scale_actions;              /* action.scale_space */
+  int32_t has_bounds;                 /* action.bounds_multiplier present */
+  double scale_low, scale_high, bounds_multiplier;
+  double act_low[3], act_high[3];     /* actuator state limits (action_scale_to_*) */
+  int32_t target_class[3];            /* roll, pitch, Va */
+  int32_t target_wrap[3];
+  double target_low[3], target_high[3];
+  double target_delta[3];             /* NaN = none */
+  double target_bound[3];             /* NaN = none */
+  int32_t streak_req;                 /* <= 128; 0 disables goal */
+  int32_t on_success;                 /* 0 none, 1 done */
+  double streak_frac;
+  int32_t n_rew;
+  int32_t step_fail_timesteps;        /* reward.step_fail == "timesteps" */
+  double step_fail_value;
+  double term_weight[3];              /* per function class (linear, quadratic, exponential) */
+  int32_t term_present[3];
+  int32_t pad_;
+  fw_rew_factor rew[FW_MAX_REW];
+} fw_env_config;
+
+/* explicit reset inputs: SoA [FW_NINIT][N]; NaN = sample like an omitted dict key */
+enum fw_init_field {
+  FW_I_ROLL = 0, FW_I_PITCH, FW_I_YAW, FW_I_P, FW_I_Q, FW_I_R,
+  FW_I_PN, FW_I_PE, FW_I_PD, FW_I_U, FW_I_V, FW_I_W,
+  FW_I_ACT0, FW_I_ACT0_DOT, FW_I_ACT1, FW_I_ACT1_DOT, FW_I_ACT2, FW_I_ACT2_DOT,
+  FW_I_WIND_N, FW_I_WIND_E, FW_I_WIND_D,
+  FW_NINIT
+};
+
+/* state blocks for fw_get_state / fw_set_state (all SoA, [rows][N]) */
+#define FW_BLK_ODE 0        /* FW_NY rows, T */
+#define FW_BLK_DERIVED 1    /* 8 rows, T: roll pitch yaw Va alpha beta elevator aileron */
+#define FW_BLK_TARGET 2     /* 3 rows, T */
+#define FW_BLK_WIND 3       /* 3 rows, T: steady wind n e d */
+#define FW_BLK_STEPS 4      /* 2 rows, int32: steps_count, steps_for_current_target */
+#define FW_BLK_COMMAND 5    /* 3 rows, T: last constrained commands (input order) */
+#define FW_NBLK 6
+
+typedef struct fw_handle fw_handle;
+
+int fw_abi_version(void);
+int fw_last_error(char* buf, size_t len);
+
+/* env may be NULL: a PyFly-only handle (fw_env_step then fails).  */
+int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs, int32_t precision,
+              int32_t device, fw_handle** out);
+int fw_destroy(fw_handle* h);
+int fw_num_envs(const fw_handle* h, int64_t* n);
+int fw_num_obs(const fw_handle* h, int32_t* n);
+
+/* Counter-based RNG key: env i of this handle draws from stream (seed, env_offset + i). */
+int fw_seed(fw_handle* h, uint64_t seed, int64_t env_offset);
+
+/* Turbulence noise injection (parity mode, the turbulence_noise argument of
+ * PyFly.reset): N(0,1) samples, SoA [4][len][N], consumed from index 0 at each
+ * reset.  NULL reverts to the on-device Philox generator. The buffer must stay
+ * alive while the handle uses it.                                            */
+int fw_set_noise(fw_handle* h, const void* noise_dev, int64_t len);
+
+/* Masked reset.  mask_dev: uint8[N] (NULL = all).  init_dev: [FW_NINIT][N] or
+ * NULL (all sampled).  target_dev: [3][N] or NULL.  obs_dev: [N][n_obs] or NULL. */
+int fw_reset(fw_handle* h, const uint8_t* mask_dev, const void* init_dev, const void* target_dev,
+             void* obs_dev, void* stream);
+
+/* PyFly.step for all envs.  commands_dev: [N][3] in actuation-input order
+ * (elevator, aileron, throttle).  Outputs (NULL = skip): commands_out_dev [N][3]
+ * constrained commands, success_dev uint8[N], term_dev int32[N] (FW_TERM_*),
+ * stats_dev int32[N] = nfev | (n_accepted << 16).                            */
+int fw_sim_step(fw_handle* h, const void* commands_dev, void* commands_out_dev, uint8_t* success_dev,
+                int32_t* term_dev, int32_t* stats_dev, void* stream);
+
+/* FixedWingAircraft.step for all envs (+ VecEnv auto-reset when auto_reset != 0).
+ * actions_dev [N][3]; obs_dev [N][n_obs]; reward_dev [N]; done_dev uint8[N];
+ * term_dev int32[N]; terminal_obs_dev [N][n_obs] (written for done envs only,
+ * may be NULL); episode_dev [N][2] = (return, length) written for done envs
+ * (may be NULL); stats_dev as in fw_sim_step (may be NULL).                  */
+int fw_env_step(fw_handle* h, const void* actions_dev, void* obs_dev, void* reward_dev, uint8_t* done_dev,
+                int32_t* term_dev, void* terminal_obs_dev, void* episode_dev, int32_t* stats_dev,
+                int32_t auto_reset, void* stream);
+
+/* Observation of the current state (FixedWingAircraft.get_observation). */
+int fw_observe(fw_handle* h, void* obs_dev, void* stream);
+
+int fw_get_state(fw_handle* h, int32_t block, void* dst_dev, void* stream);
+int fw_set_state(fw_handle* h, int32_t block, const void* src_dev, void* stream);
+
+/* Curriculum / config update between steps (FixedWingAircraft.set_curriculum_level
+ * recomputes ranges on the host and pushes a new env/sim config).            */
+int fw_update_config(fw_handle* h, const fw_sim_config* sim, const fw_env_config* env);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FWSIM_H */

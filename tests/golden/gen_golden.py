@@ -1,0 +1,520 @@
+"""Generate the golden fixtures that pin the oracle (test infrastructure only).
+
+Runs the *reference itself* (pyfly + gym_fixed_wing from /root/reference, pure
+Python, importable in the build container) on seeded inputs and stores inputs +
+outputs as small ``.npz`` files next to this script.  Only data leaves this
+script; no reference source is copied.  The GPU box never runs this file.
+
+The reference imports ``gym`` (0.18), which is not installed here, so this script
+installs a tiny offline stand-in module providing exactly what
+``fixed_wing.py`` touches: ``gym.Env``, ``gym.spaces.Box`` and
+``gym.utils.seeding.np_random`` (restated from gym 0.18's sha512 seeding scheme).
+All env fixtures pass explicit ``state``/``target`` dicts to ``reset`` so they
+do not depend on that seeding scheme.
+
+Usage:  python tests/golden/gen_golden.py   (takes ~2-4 minutes)
+
+Fixtures (all float64 unless noted):
+  pyfly_single_step.npz   teacher-forced single PyFly.step cases (turbulence off/on)
+  pyfly_traj.npz          free-running PyFly trajectories (PID + random commands)
+  dryden.npz              Dryden FIR coefficients + raw filter outputs
+  env_seq.npz             FixedWingAircraft reset/step sequences (obs, reward, done, term)
+  env_pid_set.npz         PID replay of a synthetic 40-scenario evaluation set
+"""
+import hashlib
+import math
+import os
+import struct
+import sys
+import types
+
+import numpy as np
+
+REF = "/root/reference/magpie/libs"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+# ---------------------------------------------------------------------------
+# offline gym stand-in (only what fixed_wing.py uses)
+# ---------------------------------------------------------------------------
+
+
+def _install_gym_stub():
+    gym = types.ModuleType("gym")
+    spaces = types.ModuleType("gym.spaces")
+    utils = types.ModuleType("gym.utils")
+    seeding = types.ModuleType("gym.utils.seeding")
+
+    class Env:
+        metadata = {}
+
+    class Box:
+        def __init__(self, low, high, shape=None, dtype=np.float32):
+            self.dtype = np.dtype(dtype)
+            self.low = np.asarray(low, dtype=self.dtype)
+            self.high = np.asarray(high, dtype=self.dtype)
+            self.shape = self.low.shape
+
+    def _bigint_from_bytes(b):
+        pad = 4 - len(b) % 4
+        b = b + b"\0" * pad
+        vals = struct.unpack("{}I".format(len(b) // 4), b)
+        return sum(v << (32 * i) for i, v in enumerate(vals))
+
+    def _int_list_from_bigint(x):
+        if x == 0:
+            return [0]
+        out = []
+        while x > 0:
+            x, m = divmod(x, 2 ** 32)
+            out.append(m)
+        return out
+
+    def np_random(seed=None):
+        if seed is None:
+            seed = _bigint_from_bytes(os.urandom(8))
+        seed = seed % 2 ** 64
+        h = _bigint_from_bytes(hashlib.sha512(str(seed).encode("utf8")).digest()[:8])
+        rng = np.random.RandomState()
+        rng.seed(_int_list_from_bigint(h))
+        return rng, seed
+
+    class GoalEnv(Env):
+        pass
+
+    gym.Env = Env
+    gym.GoalEnv = GoalEnv
+    spaces.Box = Box
+    gym.spaces = spaces
+    seeding.np_random = np_random
+    utils.seeding = seeding
+    gym.utils = utils
+    for name, mod in [("gym", gym), ("gym.spaces", spaces), ("gym.utils", utils),
+                      ("gym.utils.seeding", seeding)]:
+        sys.modules[name] = mod
+
+
+_install_gym_stub()
+sys.path.insert(0, os.path.join(REF, "pyfly"))
+sys.path.insert(0, os.path.join(REF, "fixed-wing-gym"))
+import scipy.integrate  # noqa: E402
+import pyfly.pyfly as pf  # noqa: E402
+from pyfly.dryden import DrydenGustModel  # noqa: E402
+from gym_fixed_wing.fixed_wing import FixedWingAircraft  # noqa: E402
+
+PYFLY_CFG = os.path.join(REF, "pyfly/pyfly/pyfly_config.json")
+PYFLY_PARAM = os.path.join(REF, "pyfly/pyfly/x8_param.mat")
+GYM_CFG = os.path.join(REF, "fixed-wing-gym/gym_fixed_wing/fixed_wing_config.json")
+
+# ---------------------------------------------------------------------------
+# instrumentation: solver statistics per PyFly.step
+# ---------------------------------------------------------------------------
+_orig_solve_ivp = scipy.integrate.solve_ivp
+_last = {}
+
+
+def _solve_ivp_probe(*a, **k):
+    _last.clear()
+    sol = _orig_solve_ivp(*a, **k)
+    _last["nfev"] = sol.nfev
+    _last["naccept"] = len(sol.t) - 1
+    return sol
+
+
+scipy.integrate.solve_ivp = _solve_ivp_probe
+
+
+def _count_rhs(sim):
+    counter = {"n": 0}
+    inner = sim._dynamics
+
+    def wrapped(t, y, control_sp=None):
+        counter["n"] += 1
+        return inner(t, y, control_sp)
+
+    sim._dynamics = wrapped
+    return counter
+
+
+ODE_NAMES = ["omega_p", "omega_q", "omega_r", "position_n", "position_e", "position_d",
+             "velocity_u", "velocity_v", "velocity_w"]
+
+
+def ode_vector(sim):
+    y = list(sim.state["attitude"].value)
+    y += [sim.state[n].value for n in ODE_NAMES]
+    y += sim.actuation.get_values()
+    return np.array(y, dtype=np.float64)
+
+
+def derived(sim):
+    return np.array([sim.state[n].value for n in ["roll", "pitch", "yaw", "Va", "alpha", "beta",
+                                                   "elevator", "aileron"]], dtype=np.float64)
+
+
+def hist_last(sim):
+    """history[-1] of the env-observed states (what FixedWingAircraft.get_observation reads)."""
+    return np.array([sim.state[n].history[-1] for n in
+                     ["roll", "pitch", "yaw", "Va", "alpha", "beta", "omega_p", "omega_q", "omega_r"]],
+                    dtype=np.float64)
+
+
+def turb_at(sim, k):
+    if not sim.wind.turbulence:
+        return np.zeros(6)
+    return np.concatenate([sim.wind.dryden.vel_lin[:, k], sim.wind.dryden.vel_ang[:, k]])
+
+
+def random_state(rng, omega_deg=60.0, dots=True):
+    """A full explicit initial-state dict in the gym init ranges."""
+    d2r = np.radians
+    st = {
+        "roll": rng.uniform(d2r(-110), d2r(110)),
+        "pitch": rng.uniform(d2r(-45), d2r(45)),
+        "yaw": rng.uniform(d2r(-180), d2r(180)),
+        "omega_p": rng.uniform(d2r(-omega_deg), d2r(omega_deg)),
+        "omega_q": rng.uniform(d2r(-omega_deg), d2r(omega_deg)),
+        "omega_r": rng.uniform(d2r(-omega_deg), d2r(omega_deg)),
+        "position_n": rng.uniform(-100, 100),
+        "position_e": rng.uniform(-100, 100),
+        "position_d": rng.uniform(-100, -20),
+        "velocity_u": rng.uniform(10, 23),
+        "velocity_v": rng.uniform(-5, 5),
+        "velocity_w": rng.uniform(-5, 5),
+    }
+    if dots:
+        st["elevon_right"] = (rng.uniform(d2r(-30), d2r(35)), rng.uniform(-3.4907, 3.4907))
+        st["elevon_left"] = (rng.uniform(d2r(-30), d2r(35)), rng.uniform(-3.4907, 3.4907))
+        st["throttle"] = (rng.uniform(0, 1), 0.0)
+    else:
+        st["elevon_right"] = 0.0
+        st["elevon_left"] = 0.0
+        st["throttle"] = 0.0
+    return st
+
+
+def random_wind(rng, mag=8.0):
+    m = rng.uniform(-mag, mag)
+    wn = rng.uniform(-abs(m), abs(m))
+    we_max = math.sqrt(max(m * m - wn * wn, 0.0))
+    we = rng.uniform(-we_max, we_max)
+    wd = math.sqrt(max(m * m - wn * wn - we * we, 0.0))
+    return [wn, we, wd]
+
+
+# ---------------------------------------------------------------------------
+# A. teacher-forced single steps
+# ---------------------------------------------------------------------------
+
+
+def gen_single_step():
+    rows = {k: [] for k in ["turb_on", "y0", "wind", "k", "turb", "noise_km1", "noise_k", "cmd_in",
+                            "cmd_out", "y1", "success", "term", "nfev", "naccept", "derived1",
+                            "hist1", "omega_limit_deg", "va_limit"]}
+    rng = np.random.RandomState(12345)
+    L = 300
+    n_cases = 800
+    for i in range(n_cases):
+        turb_on = i % 2 == 1
+        omega_lim = 180.0 if i % 4 < 2 else 720.0
+        kw = {"turbulence": turb_on, "turbulence_sim_length": L,
+              "variables": {}}
+        sim = pf.PyFly(PYFLY_CFG, PYFLY_PARAM, config_kw={"turbulence": turb_on,
+                                                          "turbulence_sim_length": L})
+        for n in ["omega_p", "omega_q", "omega_r"]:
+            sim.state[n].constraint_min = np.radians(-omega_lim)
+            sim.state[n].constraint_max = np.radians(omega_lim)
+        sim.seed(1000 + i)
+        # some cases start near the omega constraint to exercise termination
+        st = random_state(rng, omega_deg=(175.0 if i % 16 == 3 else 60.0))
+        wind = random_wind(rng) if i % 3 else [0.0, 0.0, 0.0]
+        st["wind"] = wind
+        noise = rng.standard_normal((4, L)) if turb_on else None
+        sim.reset(state=st, turbulence_noise=noise)
+        if i % 16 == 3:  # tight omega constraint: exercises mid-integration termination
+            lim = max(abs(st[n]) for n in ["omega_p", "omega_q", "omega_r"]) + np.radians(0.5)
+            for n in ["omega_p", "omega_q", "omega_r"]:
+                sim.state[n].constraint_min, sim.state[n].constraint_max = -lim, lim
+            omega_lim = np.degrees(lim)
+        if i % 16 == 7:  # tight airspeed constraint (gym config has Va <= 70)
+            sim.state["Va"].constraint_max = sim.state["Va"].value + 0.002
+        k = int(rng.randint(1, L - 1)) if turb_on else 0
+        sim.cur_sim_step = k
+        cnt = _count_rhs(sim)
+        # commands: elevator, aileron, throttle (gym input ordering), slightly beyond limits sometimes
+        cmd = [rng.uniform(np.radians(-40), np.radians(45)), rng.uniform(np.radians(-40), np.radians(40)),
+               rng.uniform(-0.2, 1.2)]
+        y0 = ode_vector(sim)
+        turb = turb_at(sim, k)
+        cmd_in = list(cmd)
+        ok, info = sim.step(cmd)
+        rows["turb_on"].append(turb_on)
+        rows["y0"].append(y0)
+        rows["wind"].append(np.array(wind, dtype=np.float64))
+        rows["k"].append(k)
+        rows["turb"].append(turb)
+        if turb_on:
+            rows["noise_km1"].append(noise[:, k - 1])
+            rows["noise_k"].append(noise[:, k])
+        else:
+            rows["noise_km1"].append(np.zeros(4))
+            rows["noise_k"].append(np.zeros(4))
+        rows["cmd_in"].append(np.array(cmd_in))
+        rows["cmd_out"].append(np.array(cmd, dtype=np.float64))
+        rows["y1"].append(ode_vector(sim))
+        rows["success"].append(ok)
+        rows["term"].append(info.get("termination", ""))
+        rows["nfev"].append(cnt["n"])
+        rows["naccept"].append(_last.get("naccept", -1) if ok else -1)
+        rows["derived1"].append(derived(sim))
+        rows["hist1"].append(hist_last(sim))
+        rows["omega_limit_deg"].append(omega_lim)
+        vc = sim.state["Va"].constraint_max
+        rows["va_limit"].append(np.inf if vc is None else vc)
+    out = {k: np.array(v) for k, v in rows.items()}
+    np.savez_compressed(os.path.join(OUT, "pyfly_single_step.npz"), **out)
+    print("single steps: %d cases, %d failures, nfev mean %.1f" % (
+        n_cases, int((~out["success"]).sum()), out["nfev"].mean()))
+
+
+# ---------------------------------------------------------------------------
+# B. free-running trajectories
+# ---------------------------------------------------------------------------
+
+
+def pid_action(pid, sim):
+    phi = sim.state["roll"].value
+    theta = sim.state["pitch"].value
+    va = sim.state["Va"].value
+    om = [sim.state["omega_p"].value, sim.state["omega_q"].value]
+    e_v, e_phi, e_th = va - pid["va"], phi - pid["phi"], theta - pid["theta"]
+    pid["iv"] += pid["dt"] * e_v
+    pid["ir"] += pid["dt"] * e_phi
+    pid["ip"] += pid["dt"] * e_th
+    dt_ = 0 - 0.5 * e_v - 0.1 * pid["iv"]
+    da = -1 * e_phi - 0 * pid["ir"] - 0.5 * om[0]
+    de = 0 - (-4) * e_th - (-0.75) * pid["ip"] - (-0.1) * om[1]
+    return [float(np.clip(de, np.radians(-30), np.radians(35))),
+            float(np.clip(da, np.radians(-30), np.radians(30))),
+            float(np.clip(dt_, 0, 1))]
+
+
+def run_traj(turb_on, controller, seed, n_steps=1000, L=300, omega_lim_deg=None):
+    rng = np.random.RandomState(seed)
+    sim = pf.PyFly(PYFLY_CFG, PYFLY_PARAM, config_kw={"turbulence": turb_on,
+                                                      "turbulence_sim_length": L})
+    if omega_lim_deg is not None:
+        for n in ["omega_p", "omega_q", "omega_r"]:
+            sim.state[n].constraint_min = np.radians(-omega_lim_deg)
+            sim.state[n].constraint_max = np.radians(omega_lim_deg)
+    sim.seed(seed)
+    st = random_state(rng, omega_deg=60.0 if omega_lim_deg is None else 0.5 * omega_lim_deg, dots=False)
+    st["roll"], st["pitch"] = -0.5, 0.15
+    wind = random_wind(rng) if turb_on else [0.0, 0.0, 0.0]
+    st["wind"] = wind
+    n_chunks = (n_steps + L - 1) // L + 1
+    noise = rng.standard_normal((4, L * n_chunks)) if turb_on else np.zeros((4, L * n_chunks))
+    sim.reset(state=st, turbulence_noise=noise if turb_on else None)
+    cnt = _count_rhs(sim)
+    pid = {"dt": sim.dt, "va": 22.0, "phi": 0.2, "theta": 0.0, "iv": 0.0, "ir": 0.0, "ip": 0.0}
+    y = [ode_vector(sim)]
+    der = [derived(sim)]
+    cmds, nfev, succ, term = [], [], [], ""
+    for s in range(n_steps):
+        if controller == "pid":
+            cmd = pid_action(pid, sim)
+        else:
+            cmd = [rng.uniform(np.radians(-30), np.radians(35)), rng.uniform(np.radians(-32.5), np.radians(32.5)),
+                   rng.uniform(0, 1)]
+        cmds.append(list(cmd))
+        cnt["n"] = 0
+        ok, info = sim.step(cmd)
+        nfev.append(cnt["n"])
+        succ.append(ok)
+        y.append(ode_vector(sim))
+        der.append(derived(sim))
+        if not ok:
+            term = info["termination"]
+            break
+    return dict(y=np.array(y), derived=np.array(der), cmd=np.array(cmds), nfev=np.array(nfev),
+                success=np.array(succ), term=np.array(term), wind=np.array(wind), noise=noise,
+                L=np.array(L), turb_on=np.array(turb_on),
+                omega_lim_deg=np.array(180.0 if omega_lim_deg is None else omega_lim_deg))
+
+
+def gen_traj():
+    out = {}
+    for name, turb_on, ctrl, seed, olim in [("pid_off", False, "pid", 0, None), ("pid_on", True, "pid", 0, None),
+                                            ("rand_off", False, "rand", 1, None),
+                                            ("rand_on", True, "rand", 2, None),
+                                            ("rand_fail", True, "rand", 3, 45.0)]:
+        tr = run_traj(turb_on, ctrl, seed, omega_lim_deg=olim)
+        for k, v in tr.items():
+            out[name + "__" + k] = v
+        print("traj %s: %d steps, term=%r, nfev mean %.1f" % (name, len(tr["nfev"]), str(tr["term"]),
+                                                             tr["nfev"].mean()))
+    np.savez_compressed(os.path.join(OUT, "pyfly_traj.npz"), **out)
+
+
+# ---------------------------------------------------------------------------
+# C. Dryden
+# ---------------------------------------------------------------------------
+
+
+def gen_dryden():
+    out = {}
+    rng = np.random.RandomState(7)
+    for L, inten in [(300, "light"), (300, "moderate"), (300, "severe"), (2000, "light"),
+                     (2000, "severe")]:
+        if True:
+            # exactly how pyfly.Wind wires it (pyfly.py:781-783): positional (sim_length, dt, b)
+            dm = DrydenGustModel(L, 0.01, 2.1, intensity=inten)
+            noise = rng.standard_normal((4, 2 * L))
+            dm.reset(noise)
+            dm.simulate(L)
+            dm.simulate(L)
+            keep = np.r_[0:200, L - 20:L + 200]  # both chunk starts, FIR interior
+            out["L%d_%s__noise" % (L, inten)] = noise[:, keep]
+            out["L%d_%s__idx" % (L, inten)] = keep
+            out["L%d_%s__vel_lin" % (L, inten)] = dm.vel_lin[:, keep]
+            out["L%d_%s__vel_ang" % (L, inten)] = dm.vel_ang[:, keep]
+    np.savez_compressed(os.path.join(OUT, "dryden.npz"), **out)
+    print("dryden done")
+
+
+# ---------------------------------------------------------------------------
+# D. gym env sequences
+# ---------------------------------------------------------------------------
+
+ENV_STATE_KEYS = ["roll", "pitch", "yaw", "omega_p", "omega_q", "omega_r", "position_n", "position_e",
+                  "position_d", "velocity_u", "velocity_v", "velocity_w"]
+
+
+def make_env(turb_on, steps_max=2000, config_kw=None):
+    ckw = {"steps_max": steps_max}
+    if config_kw:
+        ckw.update(config_kw)
+    env = FixedWingAircraft(GYM_CFG, config_kw=ckw,
+                            sim_config_kw={"turbulence": turb_on, "turbulence_intensity": "light"})
+    env.seed(0)
+    return env
+
+
+def env_episode(env, rng, turb_on, n_steps, act_scale=1.2, omega_deg=60.0, policy="rand"):
+    st = random_state(rng, omega_deg=omega_deg, dots=False)
+    st["wind"] = random_wind(rng) if turb_on else [0.0, 0.0, 0.0]
+    d2r = np.radians
+    target = {"roll": rng.uniform(d2r(-60), d2r(60)), "pitch": rng.uniform(d2r(-25), d2r(25)),
+              "Va": rng.uniform(15, 28)}
+    L = env.simulator.wind.turbulence_sim_length
+    noise = rng.standard_normal((4, L)) if turb_on else None
+    obs0 = env.reset(state=dict(st), target=dict(target), turbulence_noise=noise)
+    init = np.array([st[k] for k in ENV_STATE_KEYS] + [0.0, 0.0, 0.0] + list(st["wind"]))
+    obs, rew, done, term, acts, tgt = [obs0], [], [], [], [], [
+        np.array([env.target["roll"], env.target["pitch"], env.target["Va"]])]
+    pid = {"dt": 0.01, "va": target["Va"], "phi": target["roll"], "theta": target["pitch"],
+           "iv": 0.0, "ir": 0.0, "ip": 0.0}
+    for s in range(n_steps):
+        if policy == "rand":
+            a = rng.uniform(-act_scale, act_scale, size=3).astype(np.float32)
+        else:
+            a = np.array(pid_action(pid, env.simulator), dtype=np.float64)
+        o, r, d, info = env.step(a)
+        acts.append(np.asarray(a, dtype=np.float64))
+        obs.append(o)
+        rew.append(r)
+        done.append(d)
+        term.append(info.get("termination", ""))
+        tgt.append(np.array([env.target["roll"], env.target["pitch"], env.target["Va"]]))
+        if policy != "rand":
+            pid["phi"], pid["theta"], pid["va"] = info["target"]["roll"], info["target"]["pitch"], info["target"]["Va"]
+        if d:
+            break
+    return dict(init=init, target0=np.array([target["roll"], target["pitch"], target["Va"]]),
+                noise=noise if noise is not None else np.zeros((4, 1)), obs=np.array(obs),
+                act=np.array(acts), rew=np.array(rew), done=np.array(done), term=np.array(term),
+                target=np.array(tgt))
+
+
+def gen_env_seq():
+    out = {}
+    rng = np.random.RandomState(99)
+    cases = [
+        # name, turb, steps_max, n_steps, omega_deg, policy, config_kw
+        ("rand_off", False, 2000, 300, 60.0, "rand", None),
+        ("rand_on", False, 2000, 300, 60.0, "rand", None),
+        ("rand_turb", True, 2000, 300, 60.0, "rand", None),
+        ("short_max", False, 120, 200, 60.0, "rand", None),
+        ("fail_omega", False, 2000, 300, 700.0, "rand", None),
+        ("fail_va", False, 2000, 600, 60.0, "rand", {"simulator": {"states": {5: {"constraint_max": 17.5}}}}),
+        ("pid_goal", False, 2000, 400, 20.0, "pid", {"action": {"scale_space": False}}),
+        ("pid_goal_done", False, 1500, 1500, 20.0, "pid",
+         {"action": {"scale_space": False},
+          "target": {"on_success": "done", "success_streak_fraction": 1, "success_streak_req": 100}}),
+        ("pid_turb", True, 2000, 500, 20.0, "pid", {"action": {"scale_space": False}}),
+    ]
+    for name, turb, smax, n, omd, pol, ckw in cases:
+        env = make_env(turb, smax, ckw)
+        ep = env_episode(env, rng, turb, n, omega_deg=omd, policy=pol)
+        for k, v in ep.items():
+            out[name + "__" + k] = v
+        out[name + "__steps_max"] = np.array(smax)
+        out[name + "__turb_on"] = np.array(turb)
+        out[name + "__scale_space"] = np.array(ckw is None)
+        print("env %s: %d steps, last term=%r, rew sum %.3f" % (name, len(ep["rew"]), ep["term"][-1],
+                                                               ep["rew"].sum()))
+    np.savez_compressed(os.path.join(OUT, "env_seq.npz"), **out)
+
+
+def gen_pid_set(n_scen=40):
+    """PID replay on a synthetic evaluation set built like evaluate_controller.py:90-108."""
+    rng = np.random.RandomState(2021)
+    d2r = np.radians
+    ckw = {"steps_max": 1500, "action": {"scale_space": False},
+           "target": {"on_success": "done", "success_streak_fraction": 1, "success_streak_req": 100,
+                      "states": {0: {"bound": 5}, 1: {"bound": 5}, 2: {"bound": 2}}}}
+    env = make_env(False, 1500, ckw)
+    lengths, rewards, inits, targets, terms = [], [], [], [], []
+    for i in range(n_scen):
+        st = {"roll": rng.uniform(d2r(-60), d2r(60)), "pitch": rng.uniform(d2r(-25), d2r(25)),
+              "yaw": 0.0, "omega_p": 0.0, "omega_q": 0.0, "omega_r": 0.0,
+              "position_n": 0.0, "position_e": 0.0, "position_d": -50.0,
+              "velocity_u": rng.uniform(15, 23), "velocity_v": 0.0, "velocity_w": 0.0,
+              "elevon_right": 0.0, "elevon_left": 0.0, "throttle": 0.0, "wind": [0.0, 0.0, 0.0]}
+        tgt = {"roll": rng.uniform(d2r(-60), d2r(60)), "pitch": rng.uniform(d2r(-25), d2r(25)),
+               "Va": rng.uniform(15, 28)}
+        env.reset(state=dict(st), target=dict(tgt))
+        pid = {"dt": 0.01, "va": tgt["Va"], "phi": tgt["roll"], "theta": tgt["pitch"], "iv": 0.0,
+               "ir": 0.0, "ip": 0.0}
+        rs = []
+        while True:
+            a = np.array(pid_action(pid, env.simulator))
+            o, r, d, info = env.step(a)
+            rs.append(r)
+            pid["phi"], pid["theta"], pid["va"] = info["target"]["roll"], info["target"]["pitch"], info["target"]["Va"]
+            if d:
+                break
+        lengths.append(len(rs))
+        rr = np.zeros(1500)
+        rr[:len(rs)] = rs
+        rewards.append(rr)
+        inits.append([st[k] for k in ENV_STATE_KEYS])
+        targets.append([tgt["roll"], tgt["pitch"], tgt["Va"]])
+        terms.append(info.get("termination", ""))
+    np.savez_compressed(os.path.join(OUT, "env_pid_set.npz"), length=np.array(lengths),
+                        reward=np.array(rewards), init=np.array(inits), target=np.array(targets),
+                        term=np.array(terms))
+    print("pid set: lengths", lengths)
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["single", "traj", "dryden", "env", "pidset"]
+    if "single" in which:
+        gen_single_step()
+    if "traj" in which:
+        gen_traj()
+    if "dryden" in which:
+        gen_dryden()
+    if "env" in which:
+        gen_env_seq()
+    if "pidset" in which:
+        gen_pid_set()

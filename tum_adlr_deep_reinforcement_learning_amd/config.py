@@ -1,0 +1,722 @@
+"""Configuration: reference-format JSON/dicts -> the POD structs of include/fwsim.h.
+
+Mirrors how the reference builds its simulator and task from config files:
+  * PyFly.__init__              magpie/libs/pyfly/pyfly/pyfly.py:1054-1249
+    (config_kw dict recursion :1067-1073, Variable radians conversion :60-64,
+     ControlVariable coefficients :296-304, Actuation.finalize limits :584-623,
+     inertia "gammas" :1086-1116)
+  * FixedWingAircraft.__init__  magpie/libs/fixed-wing-gym/gym_fixed_wing/fixed_wing.py:14-306
+    (config_kw recursion into dicts *and lists by index* :34-40, forced
+     actuation inputs / turbulence_sim_length :54-62, observation/action
+     spaces :91-276)
+  * set_curriculum_level        fixed_wing.py:334-412
+  * DrydenGustModel             magpie/libs/pyfly/pyfly/dryden.py:51-146, as wired
+    (positionally) by Wind in pyfly.py:781-783
+
+Anything the device path does not implement raises NotImplementedError here, so
+an unsupported config fails loudly at construction instead of silently
+diverging from the reference.
+"""
+import copy
+import ctypes
+import json
+import math
+import os
+
+import numpy as np
+
+from . import defaults
+
+FLOAT32_MAX = float(np.finfo(np.float32).max)
+INF = float("inf")
+
+# ---------------------------------------------------------------------------
+# ctypes mirrors of include/fwsim.h
+# ---------------------------------------------------------------------------
+FW_NY = 19
+(FW_V_ROLL, FW_V_PITCH, FW_V_YAW, FW_V_OMEGA_P, FW_V_OMEGA_Q, FW_V_OMEGA_R, FW_V_POS_N, FW_V_POS_E, FW_V_POS_D,
+ FW_V_VEL_U, FW_V_VEL_V, FW_V_VEL_W, FW_V_VA, FW_V_ALPHA, FW_V_BETA, FW_V_ACT0, FW_V_ACT1, FW_V_ACT2,
+ FW_V_ELEVATOR, FW_V_AILERON, FW_V_THROTTLE, FW_NVAR) = range(22)
+
+PARAM_NAMES = [
+    "mass", "Jx", "Jy", "Jz", "Jxz", "S_wing", "b", "c", "S_prop", "C_prop",
+    "k_motor", "k_T_P", "k_Omega", "e", "M", "a_0",
+    "C_L_0", "C_L_alpha", "C_L_q", "C_L_delta_e",
+    "C_D_p", "C_D_q", "C_D_beta1", "C_D_beta2", "C_D_delta_e",
+    "C_m_0", "C_m_alpha", "C_m_q", "C_m_delta_e", "C_m_fp",
+    "C_Y_0", "C_Y_beta", "C_Y_p", "C_Y_r", "C_Y_delta_a", "C_Y_delta_r",
+    "C_l_0", "C_l_beta", "C_l_p", "C_l_r", "C_l_delta_a", "C_l_delta_r",
+    "C_n_0", "C_n_beta", "C_n_p", "C_n_r", "C_n_delta_a", "C_n_delta_r",
+]
+FW_NPARAM = len(PARAM_NAMES)
+
+FW_TERM_NONE, FW_TERM_STEPS, FW_TERM_SUCCESS = 0, 100, 101
+
+FW_OBS_STATE, FW_OBS_TARGET_ABS, FW_OBS_TARGET_REL, FW_OBS_ACTION_WINDOW = range(4)
+FW_REW_STATE_ERROR, FW_REW_STATE_VALUE, FW_REW_ACTION_DELTA, FW_REW_ACTION_BOUND, FW_REW_ACTION_VALUE = range(5)
+FW_FUN = {"linear": 0, "quadratic": 1, "exponential": 2}
+FW_TGT = {"constant": 0, "compensate": 1}
+FW_MAX_OBS, FW_MAX_REW, FW_MAX_WINDOW = 32, 8, 16
+
+(FW_I_ROLL, FW_I_PITCH, FW_I_YAW, FW_I_P, FW_I_Q, FW_I_R, FW_I_PN, FW_I_PE, FW_I_PD, FW_I_U, FW_I_V, FW_I_W,
+ FW_I_ACT0, FW_I_ACT0_DOT, FW_I_ACT1, FW_I_ACT1_DOT, FW_I_ACT2, FW_I_ACT2_DOT, FW_I_WIND_N, FW_I_WIND_E,
+ FW_I_WIND_D, FW_NINIT) = range(22)
+
+FW_BLK_ODE, FW_BLK_DERIVED, FW_BLK_TARGET, FW_BLK_WIND, FW_BLK_STEPS, FW_BLK_COMMAND = range(6)
+
+# name of every variable slot (termination strings match the reference's
+# ConstraintException.variable, pyfly.py:11-16)
+VAR_NAMES = ["roll", "pitch", "yaw", "omega_p", "omega_q", "omega_r", "position_n", "position_e", "position_d",
+             "velocity_u", "velocity_v", "velocity_w", "Va", "alpha", "beta", None, None, None,
+             "elevator", "aileron", "throttle"]
+
+STATE_VAR_IDS = {n: i for i, n in enumerate(VAR_NAMES) if n is not None}
+
+
+class FwLimits(ctypes.Structure):
+    _fields_ = [("value_min", ctypes.c_double), ("value_max", ctypes.c_double),
+                ("constraint_min", ctypes.c_double), ("constraint_max", ctypes.c_double),
+                ("init_min", ctypes.c_double), ("init_max", ctypes.c_double),
+                ("wrap", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+
+
+class FwActuator(ctypes.Structure):
+    _fields_ = [("order", ctypes.c_int32), ("pad_", ctypes.c_int32), ("tau", ctypes.c_double),
+                ("omega_0", ctypes.c_double), ("zeta", ctypes.c_double), ("dot_max", ctypes.c_double)]
+
+
+class FwSimConfig(ctypes.Structure):
+    _fields_ = [("dt", ctypes.c_double), ("rho", ctypes.c_double), ("g", ctypes.c_double),
+                ("rtol", ctypes.c_double), ("atol", ctypes.c_double),
+                ("param", ctypes.c_double * FW_NPARAM),
+                ("lim", FwLimits * FW_NVAR),
+                ("act", FwActuator * 3),
+                ("elevon", ctypes.c_int32), ("disabled_inputs", ctypes.c_int32),
+                ("wind_random", ctypes.c_int32), ("pad0_", ctypes.c_int32),
+                ("wind_mag_min", ctypes.c_double), ("wind_mag_max", ctypes.c_double),
+                ("wind_init_min", ctypes.c_double * 3), ("wind_init_max", ctypes.c_double * 3),
+                ("turbulence", ctypes.c_int32), ("turb_len", ctypes.c_int32),
+                ("dryden_g0", ctypes.c_double * 6), ("dryden_g1", ctypes.c_double * 6)]
+
+
+class FwObsEntry(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("var", ctypes.c_int32), ("window", ctypes.c_int32),
+                ("norm", ctypes.c_int32), ("mean", ctypes.c_double), ("var_", ctypes.c_double)]
+
+
+class FwRewFactor(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("var", ctypes.c_int32), ("window", ctypes.c_int32),
+                ("fun", ctypes.c_int32), ("shaping", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("scaling", ctypes.c_double), ("max", ctypes.c_double), ("sign", ctypes.c_double)]
+
+
+class FwEnvConfig(ctypes.Structure):
+    _fields_ = [("steps_max", ctypes.c_int32), ("n_obs", ctypes.c_int32),
+                ("obs", FwObsEntry * FW_MAX_OBS),
+                ("scale_actions", ctypes.c_int32), ("has_bounds", ctypes.c_int32),
+                ("scale_low", ctypes.c_double), ("scale_high", ctypes.c_double),
+                ("bounds_multiplier", ctypes.c_double),
+                ("act_low", ctypes.c_double * 3), ("act_high", ctypes.c_double * 3),
+                ("target_class", ctypes.c_int32 * 3), ("target_wrap", ctypes.c_int32 * 3),
+                ("target_low", ctypes.c_double * 3), ("target_high", ctypes.c_double * 3),
+                ("target_delta", ctypes.c_double * 3), ("target_bound", ctypes.c_double * 3),
+                ("streak_req", ctypes.c_int32), ("on_success", ctypes.c_int32),
+                ("streak_frac", ctypes.c_double),
+                ("n_rew", ctypes.c_int32), ("step_fail_timesteps", ctypes.c_int32),
+                ("step_fail_value", ctypes.c_double),
+                ("term_weight", ctypes.c_double * 3), ("term_present", ctypes.c_int32 * 3),
+                ("pad_", ctypes.c_int32),
+                ("rew", FwRewFactor * FW_MAX_REW)]
+
+
+# ---------------------------------------------------------------------------
+# config_kw recursion semantics
+# ---------------------------------------------------------------------------
+def _set_attrs_pyfly(parent, kws):
+    """PyFly.__init__.set_config_attrs (pyfly.py:1067-1073): recurse into dicts only."""
+    for attr, val in kws.items():
+        if isinstance(val, dict):
+            _set_attrs_pyfly(parent[attr], val)
+        else:
+            parent[attr] = val
+
+
+def _set_attrs_env(parent, kws):
+    """FixedWingAircraft.__init__.set_config_attrs (fixed_wing.py:34-40): dicts and lists by index."""
+    for attr, val in kws.items():
+        if isinstance(val, dict) or isinstance(parent[attr], list):
+            _set_attrs_env(parent[attr], val)
+        else:
+            parent[attr] = val
+
+
+def _load_json(path):
+    with open(path) as f:
+        return json.load(f)
+
+
+def load_params(parameter_path=None):
+    """Aircraft parameters (x8_param.mat / .json keys)."""
+    if parameter_path is None:
+        return dict(defaults.X8_PARAMS)
+    ext = os.path.splitext(parameter_path)[1]
+    if ext == ".json":
+        p = _load_json(parameter_path)
+    elif ext == ".mat":
+        import scipy.io  # noqa: WPS433 (host-side config only)
+        p = {k: v for k, v in scipy.io.loadmat(parameter_path, squeeze_me=True).items() if not k.startswith("__")}
+    else:
+        raise Exception("Unsupported parameter file extension.")
+    out = {}
+    for k in PARAM_NAMES:
+        out[k] = float(np.asarray(p[k]).reshape(-1)[0]) if np.ndim(p[k]) else float(p[k])
+    return out
+
+
+def load_pyfly_config(config_path=None, config_kw=None):
+    cfg = defaults.default_pyfly_config() if config_path is None else _load_json(config_path)
+    if config_kw is not None:
+        _set_attrs_pyfly(cfg, copy.deepcopy(config_kw))
+    return cfg
+
+
+def load_env_config(config_path=None, config_kw=None):
+    cfg = defaults.default_env_config() if config_path is None else _load_json(config_path)
+    if config_kw is not None:
+        _set_attrs_env(cfg, copy.deepcopy(config_kw))
+    return cfg
+
+
+# ---------------------------------------------------------------------------
+# Variables (Variable / ControlVariable __init__ semantics)
+# ---------------------------------------------------------------------------
+class VarSpec:
+    """Host-side mirror of a reference ``Variable``/``ControlVariable`` (limits only)."""
+
+    RAD_ATTRS = ("value_min", "value_max", "init_min", "init_max", "constraint_min", "constraint_max")
+
+    def __init__(self, name, value_min=None, value_max=None, init_min=None, init_max=None, constraint_min=None,
+                 constraint_max=None, convert_to_radians=False, wrap=False, order=None, tau=None, omega_0=None,
+                 zeta=None, dot_max=None, disabled=False, **_unused):
+        self.name = name
+        self.value_min, self.value_max = value_min, value_max
+        self.init_min = init_min if init_min is not None else value_min
+        self.init_max = init_max if init_max is not None else value_max
+        self.constraint_min, self.constraint_max = constraint_min, constraint_max
+        if convert_to_radians:  # pyfly.py:60-64 (only the Variable attributes)
+            for a in self.RAD_ATTRS:
+                v = getattr(self, a)
+                if v is not None:
+                    setattr(self, a, float(np.radians(v)))
+        self.wrap = bool(wrap)
+        self.order, self.tau, self.omega_0, self.zeta, self.dot_max = order, tau, omega_0, zeta, dot_max
+        self.disabled = bool(disabled)
+
+    def limits(self):
+        L = FwLimits()
+        f = (lambda v, d: d if v is None else float(v))
+        L.value_min, L.value_max = f(self.value_min, -INF), f(self.value_max, INF)
+        L.constraint_min, L.constraint_max = f(self.constraint_min, -INF), f(self.constraint_max, INF)
+        L.init_min, L.init_max = f(self.init_min, float("nan")), f(self.init_max, float("nan"))
+        L.wrap = int(self.wrap)
+        return L
+
+
+# ---------------------------------------------------------------------------
+# Dryden FIR taps (dryden.py:51-146 + scipy lsim FOH, scipy/signal/_ltisys.py)
+# ---------------------------------------------------------------------------
+def dryden_filters(dt_d, b, h=100.0, V_a=25.0, intensity=None):
+    """Transfer functions (num, den) of the six shaping filters (dryden.py:51-146)."""
+    m2f = 3.281
+    f2m = 1 / m2f
+    kn = 0.5144
+    W20 = {None: 15, "light": 15, "moderate": 30, "severe": 45}
+    if intensity not in W20:
+        raise Exception("Unsupported intensity type")
+    W_20 = W20[intensity] * kn
+    h, b, V_a, W_20 = h * m2f, b * m2f, V_a * m2f, W_20 * m2f
+    sigma_w = 0.1 * W_20
+    sigma_u = sigma_w / (0.177 + 0.000823 * h) ** 0.4
+    sigma_v = sigma_u
+    L_u = h / (0.177 + 0.000823 * h) ** 1.2
+    L_v, L_w = L_u, h
+    K_u = sigma_u * math.sqrt((2 * L_u) / (math.pi * V_a))
+    K_v = sigma_v * math.sqrt(L_v / (math.pi * V_a))
+    K_w = sigma_w * math.sqrt(L_w / (math.pi * V_a))
+    T_u = L_u / V_a
+    T_v1, T_v2 = math.sqrt(3.0) * L_v / V_a, L_v / V_a
+    T_w1, T_w2 = math.sqrt(3.0) * L_w / V_a, L_w / V_a
+    K_p = sigma_w * math.sqrt(0.8 / V_a) * ((math.pi / (4 * b)) ** (1 / 6)) / (L_w ** (1 / 3))
+    K_q = 1 / V_a
+    K_r = K_q
+    T_p = 4 * b / (math.pi * V_a)
+    T_q = T_p
+    T_r = 3 * b / (math.pi * V_a)
+    return {
+        "H_u": ([f2m * K_u], [T_u, 1]),
+        "H_v": ([f2m * K_v * T_v1, f2m * K_v], [T_v2 ** 2, 2 * T_v2, 1]),
+        "H_w": ([f2m * K_w * T_w1, f2m * K_w], [T_w2 ** 2, 2 * T_w2, 1]),
+        "H_p": ([K_p], [T_p, 1]),
+        "H_q": ([-K_w * K_q * T_w1, -K_w * K_q, 0], [T_q * T_w2 ** 2, T_w2 ** 2 + 2 * T_q * T_w2, T_q + 2 * T_w2, 1]),
+        "H_r": ([K_v * K_r * T_v1, K_v * K_r, 0], [T_r * T_v2 ** 2, T_v2 ** 2 + 2 * T_r * T_v2, T_r + 2 * T_v2, 1]),
+    }
+
+
+def _tf2ss(num, den):
+    """Controllable canonical realisation of a strictly proper SISO num/den."""
+    den = np.atleast_1d(np.asarray(den, dtype=np.float64))
+    num = np.atleast_1d(np.asarray(num, dtype=np.float64))
+    num = num / den[0]
+    den = den / den[0]
+    n = len(den) - 1
+    num = np.concatenate([np.zeros(n + 1 - len(num)), num])
+    if abs(num[0]) > 0:
+        raise NotImplementedError("Dryden filter with direct feed-through")
+    A = np.zeros((n, n))
+    A[0, :] = -den[1:]
+    if n > 1:
+        A[1:, :-1] = np.eye(n - 1)
+    B = np.zeros((n, 1))
+    B[0, 0] = 1.0
+    C = num[1:].reshape(1, n)
+    return A, B, C
+
+
+def dryden_fir(turb_len, dt, wingspan, intensity):
+    """FIR taps g0 (u[k-1]) and g1 (u[k]) of the six Dryden outputs for the reference's wiring.
+
+    Wind passes (sim_length, dt, b) positionally into DrydenGustModel(dt, b, h)
+    (pyfly.py:781-783 vs dryden.py:52), so the filter's noise spacing is
+    ``turb_len`` s, its "wingspan" ``dt`` and its altitude the real wingspan.
+    lsim (first-order hold) then steps L*L/(L-1) seconds per sample, where the
+    state transition e^{A*dT} vanishes and each output is exactly
+    g0*u[k-1] + g1*u[k] (and 0 at the first sample of every chunk).
+    """
+    from scipy.linalg import expm  # host-side config only
+
+    filt = dryden_filters(turb_len, dt, wingspan, 25.0, intensity)
+    L = int(turb_len)
+    dT = (L * float(turb_len)) / (L - 1) if L > 1 else float(turb_len)
+    g0, g1 = np.zeros(6), np.zeros(6)
+    for i, name in enumerate(["H_u", "H_v", "H_w", "H_p", "H_q", "H_r"]):
+        A, B, C = _tf2ss(*filt[name])
+        n = A.shape[0]
+        M = np.zeros((n + 2, n + 2))
+        M[:n, :n] = A * dT
+        M[:n, n:n + 1] = B * dT
+        M[n, n + 1] = 1.0
+        E = expm(M)
+        Ad = E[:n, :n]
+        Bd1 = E[:n, n + 1:n + 2]
+        Bd0 = E[:n, n:n + 1] - Bd1
+        if np.max(np.abs(Ad)) > 1e-30:
+            raise NotImplementedError("Dryden chunk length %d too short for the FIR reduction "
+                                      "(|Ad|=%g); the stateful filter bank is not implemented" % (L, np.abs(Ad).max()))
+        g0[i] = float((C @ Bd0)[0, 0])
+        g1[i] = float((C @ Bd1)[0, 0])
+    return g0, g1
+
+
+# ---------------------------------------------------------------------------
+# Simulator config
+# ---------------------------------------------------------------------------
+class SimSpec:
+    """Everything the host needs about a PyFly configuration."""
+
+    def __init__(self, cfg, params):
+        self.cfg = cfg
+        self.params = params
+        self.vars = {}
+        for v in cfg["variables"]:
+            self.vars[v["name"]] = VarSpec(**v)
+        for n in ["elevator", "aileron", "rudder", "throttle"]:  # pyfly.py:1217-1221
+            if n not in self.vars:
+                self.vars[n] = VarSpec(name=n, disabled=True)
+        missing = set(["alpha", "beta", "roll", "pitch", "yaw", "omega_p", "omega_q", "omega_r", "position_n",
+                       "position_e", "position_d", "velocity_u", "velocity_v", "velocity_w", "Va", "elevator",
+                       "aileron", "rudder", "throttle"]) - set(self.vars)
+        if missing:
+            raise Exception("Missing required variable(s) in config file: {}".format(",".join(missing)))
+        self.dynamics = list(cfg["actuation"]["dynamics"])
+        self.inputs = list(cfg["actuation"]["inputs"])
+        self.elevon = "elevon_left" in self.dynamics or "elevon_right" in self.dynamics
+        if self.elevon:
+            if self.dynamics != ["elevon_right", "elevon_left", "throttle"]:
+                raise NotImplementedError("elevon dynamics must be ordered [elevon_right, elevon_left, throttle]")
+            er, el = self.vars["elevon_right"], self.vars["elevon_left"]
+            # Actuation.finalize pyfly.py:599-623
+            self.vars["elevator"].value_min = (er.value_min + el.value_min) / 2
+            self.vars["elevator"].value_max = (er.value_max + el.value_max) / 2
+            self.vars["aileron"].value_min = (-er.value_max + el.value_min) / 2
+            self.vars["aileron"].value_max = (-er.value_min + el.value_max) / 2
+        elif self.dynamics != ["elevator", "aileron", "throttle"]:
+            raise NotImplementedError("actuation.dynamics must be elevons+throttle or [elevator, aileron, throttle]")
+        if self.inputs != ["elevator", "aileron", "throttle"]:
+            raise NotImplementedError("actuation.inputs must be [elevator, aileron, throttle]")
+        for n in self.dynamics:
+            o = self.vars[n].order
+            if o not in (1, 2):
+                raise ValueError("actuator %s must have order 1 or 2" % n)
+        if any(k in cfg for k in ("recorder",)):
+            raise NotImplementedError("recorder")
+
+    # attitude constraints during integration would re-check the previous saved
+    # attitude only (pyfly.py:1865-1869) -- a no-op; value limits on roll/pitch/yaw are honoured at save.
+
+    def struct(self):
+        c = FwSimConfig()
+        cfg = self.cfg
+        c.dt, c.rho, c.g = float(cfg["dt"]), float(cfg["rho"]), float(cfg["g"])
+        c.rtol, c.atol = 1e-3, 1e-6
+        for i, n in enumerate(PARAM_NAMES):
+            c.param[i] = float(self.params[n])
+        slot = {}
+        for n in ["roll", "pitch", "yaw", "omega_p", "omega_q", "omega_r", "position_n", "position_e", "position_d",
+                  "velocity_u", "velocity_v", "velocity_w", "Va", "alpha", "beta", "elevator", "aileron", "throttle"]:
+            slot[n] = STATE_VAR_IDS[n]
+        for n, i in slot.items():
+            c.lim[i] = self.vars[n].limits()
+        for j, n in enumerate(self.dynamics):
+            v = self.vars[n]
+            c.lim[FW_V_ACT0 + j] = v.limits()
+            a = c.act[j]
+            a.order = int(v.order)
+            a.tau = float(v.tau) if v.tau is not None else 0.0
+            a.omega_0 = float(v.omega_0) if v.omega_0 is not None else 0.0
+            a.zeta = float(v.zeta) if v.zeta is not None else 0.0
+            a.dot_max = float(v.dot_max) if v.dot_max is not None else INF
+        c.elevon = int(self.elevon)
+        c.disabled_inputs = (1 if self.vars["elevator"].disabled else 0) | (2 if self.vars["aileron"].disabled else 0)
+        mmin, mmax = cfg.get("wind_magnitude_min"), cfg.get("wind_magnitude_max")
+        c.wind_random = int(not (mmin is None and mmax is None))
+        c.wind_mag_min = float(mmin) if mmin is not None else 0.0
+        c.wind_mag_max = float(mmax) if mmax is not None else 0.0
+        for i, n in enumerate(["wind_n", "wind_e", "wind_d"]):
+            v = self.vars.get(n)
+            c.wind_init_min[i] = float(v.init_min) if v is not None and v.init_min is not None else 0.0
+            c.wind_init_max[i] = float(v.init_max) if v is not None and v.init_max is not None else 0.0
+        c.turbulence = int(bool(cfg["turbulence"]))
+        c.turb_len = int(cfg.get("turbulence_sim_length", 300))
+        if c.turbulence:
+            g0, g1 = dryden_fir(c.turb_len, c.dt, float(self.params["b"]), cfg["turbulence_intensity"])
+            for i in range(6):
+                c.dryden_g0[i], c.dryden_g1[i] = g0[i], g1[i]
+        return c
+
+
+def build_sim(config_path=None, parameter_path=None, config_kw=None):
+    return SimSpec(load_pyfly_config(config_path, config_kw), load_params(parameter_path))
+
+
+# ---------------------------------------------------------------------------
+# Env config
+# ---------------------------------------------------------------------------
+TARGET_INDEX = {"roll": 0, "pitch": 1, "Va": 2}
+ACTION_INDEX = {"elevator": 0, "aileron": 1, "throttle": 2}
+
+
+class EnvSpec:
+    """Host-side mirror of FixedWingAircraft's configuration (fixed_wing.py:14-306)."""
+
+    def __init__(self, config_path=None, config_kw=None, sim_config_path=None, sim_parameter_path=None,
+                 sim_config_kw=None, curriculum_level=1):
+        self.cfg = load_env_config(config_path, config_kw)
+        cfg = self.cfg
+        skw = copy.deepcopy(sim_config_kw) if sim_config_kw else {}
+        skw.update({"actuation": {"inputs": [a["name"] for a in cfg["action"]["states"]]}})
+        skw["turbulence_sim_length"] = cfg["steps_max"]  # fixed_wing.py:62
+        self.sim = build_sim(sim_config_path, sim_parameter_path, skw)
+        self.steps_max = int(cfg["steps_max"])
+        obs_cfg = cfg["observation"]
+        if obs_cfg.get("length", 1) != 1:
+            raise NotImplementedError("observation.length > 1")
+        if obs_cfg.get("normalize", False) and any(o.get("mean") is None for o in obs_cfg["states"]):
+            raise NotImplementedError("observation normalisation without explicit mean/var")
+        noise = obs_cfg.get("noise")
+        if noise is not None and (noise.get("var", 0) != 0 or noise.get("mean", 0) != 0):
+            raise NotImplementedError("observation noise")
+        if cfg.get("integration_window", 0):
+            raise NotImplementedError("integration_window")
+        if cfg["reward"].get("form", "absolute") != "absolute":
+            raise NotImplementedError("reward.form other than 'absolute'")
+        if cfg["reward"].get("randomize_scaling", False):
+            raise NotImplementedError("reward.randomize_scaling")
+        if cfg["target"].get("resample_every", 0):
+            raise NotImplementedError("target.resample_every")
+        if cfg["target"].get("on_success", "none") not in ("none", "done"):
+            raise NotImplementedError("target.on_success=%r" % cfg["target"].get("on_success"))
+        sim_keys = set(cfg.get("simulator", {}).keys()) - {"states"}
+        if sim_keys:
+            raise NotImplementedError("simulator parameter randomisation (%s)" % sorted(sim_keys))
+        self.scale_actions = bool(cfg["action"].get("scale_space", False))
+        self.set_curriculum_level(curriculum_level)
+        self._build_spaces()
+
+    # fixed_wing.py:334-412
+    def set_curriculum_level(self, level):
+        assert 0 <= level <= 1
+        self.curriculum_level = level
+        cfg = self.cfg
+        for state in cfg.get("simulator", {}).get("states", []):
+            state = copy.copy(state)
+            name = state.pop("name")
+            rad = state.pop("convert_to_radians", False)
+            var = self.sim.vars[name]
+            for prop, val in state.items():
+                if val is not None:
+                    if "constraint" not in prop and any(m in prop for m in ["min", "max"]):
+                        midpoint = (state[prop[:-3] + "max"] + state[prop[:-3] + "min"]) / 2
+                        val = midpoint - level * (midpoint - val)
+                    if rad:
+                        val = float(np.radians(val))
+                setattr(var, prop, val)
+        self.target_props = {}
+        for st in cfg["target"]["states"]:
+            props = {}
+            for k, v in st.items():
+                if k == "name":
+                    continue
+                if k not in ["bound", "class"] and v is not None and not isinstance(v, bool):
+                    if k == "low":
+                        midpoint = (st["high"] + v) / 2
+                    elif k == "high":
+                        midpoint = (v + st["low"]) / 2
+                    else:
+                        midpoint = 0
+                    v = midpoint - level * (midpoint - v)
+                props[k] = v
+            self.target_props[st["name"]] = props
+
+    def _state_bound(self, name, which):
+        v = self.sim.vars[name]
+        if which == "high":
+            if v.value_max is not None:
+                return v.value_max
+            if v.constraint_max is not None:
+                return v.constraint_max
+            return FLOAT32_MAX
+        if v.value_min is not None:
+            return v.value_min
+        if v.constraint_min is not None:
+            return v.constraint_min
+        return -FLOAT32_MAX
+
+    def _build_spaces(self):
+        cfg = self.cfg
+        lo, hi = [], []
+        for o in cfg["observation"]["states"]:
+            h = o.get("high")
+            if h is None:
+                h = self._state_bound(o["name"], "high")
+            elif o.get("convert_to_radians", False):
+                h = float(np.radians(h))
+            low = o.get("low")
+            if low is None:
+                low = self._state_bound(o["name"], "low")
+            elif o.get("convert_to_radians", False):
+                low = float(np.radians(low))
+            if o["type"] == "target" and o.get("value") == "relative":
+                if h != FLOAT32_MAX and low != -FLOAT32_MAX:
+                    hi.append(h - low)
+                    lo.append(low - h)
+                else:
+                    hi.append(FLOAT32_MAX)
+                    lo.append(-FLOAT32_MAX)
+            else:
+                hi.append(h)
+                lo.append(low)
+        self.obs_low = np.array(lo, dtype=np.float32)
+        self.obs_high = np.array(hi, dtype=np.float32)
+        alo, ahi, slo, shi = [], [], [], []
+        for a in cfg["action"]["states"]:
+            s_hi = self._state_bound(a["name"], "high")
+            s_lo = self._state_bound(a["name"], "low")
+            sp_hi, sp_lo = a.get("high"), a.get("low")
+            ahi.append(FLOAT32_MAX if sp_hi == "max" else (s_hi if sp_hi is None else sp_hi))
+            alo.append(-FLOAT32_MAX if sp_lo == "max" else (s_lo if sp_lo is None else sp_lo))
+            shi.append(s_hi)
+            slo.append(s_lo)
+        self.action_space_low = np.array(alo, dtype=np.float32)
+        self.action_space_high = np.array(ahi, dtype=np.float32)
+        self.action_scale_to_low = np.array(slo, dtype=np.float64)
+        self.action_scale_to_high = np.array(shi, dtype=np.float64)
+
+    @property
+    def n_obs(self):
+        return len(self.cfg["observation"]["states"])
+
+    def obs_names(self):
+        out = []
+        for o in self.cfg["observation"]["states"]:
+            out.append(o["name"] + ("_target" if o["type"] == "target" else "") +
+                       ("_delta" if o["type"] == "action" else ""))
+        return out
+
+    def struct(self):
+        cfg = self.cfg
+        e = FwEnvConfig()
+        e.steps_max = self.steps_max
+        states = cfg["observation"]["states"]
+        if len(states) > FW_MAX_OBS:
+            raise NotImplementedError("more than %d observation entries" % FW_MAX_OBS)
+        e.n_obs = len(states)
+        norm_all = bool(cfg["observation"].get("normalize", False))
+        for i, o in enumerate(states):
+            E = e.obs[i]
+            t = o["type"]
+            if t == "state":
+                if o["name"] not in STATE_VAR_IDS:
+                    raise NotImplementedError("observation of state %r" % o["name"])
+                E.kind, E.var = FW_OBS_STATE, STATE_VAR_IDS[o["name"]]
+            elif t == "target":
+                val = o.get("value")
+                if val == "absolute":
+                    E.kind = FW_OBS_TARGET_ABS
+                elif val == "relative":
+                    E.kind = FW_OBS_TARGET_REL
+                else:
+                    raise NotImplementedError("target observation value %r" % val)
+                E.var = TARGET_INDEX[o["name"]]
+            elif t == "action":
+                E.kind, E.var = FW_OBS_ACTION_WINDOW, ACTION_INDEX[o["name"]]
+                E.window = int(o.get("window_size", 1))
+                if E.window > FW_MAX_WINDOW:
+                    raise NotImplementedError("action window > %d" % FW_MAX_WINDOW)
+            else:
+                raise Exception("Unexpected observation variable type: {}".format(t))
+            E.norm = int(norm_all and o.get("norm", True))
+            E.mean = float(o.get("mean", 0.0) or 0.0)
+            E.var_ = float(o.get("var", 1.0) or 1.0)
+        a = cfg["action"]
+        e.scale_actions = int(self.scale_actions)
+        e.scale_low = float(a.get("scale_low", -1) if a.get("scale_low") is not None else -1)
+        e.scale_high = float(a.get("scale_high", 1) if a.get("scale_high") is not None else 1)
+        bm = a.get("bounds_multiplier")
+        e.has_bounds = int(bm is not None)
+        e.bounds_multiplier = float(bm) if bm is not None else 0.0
+        for i in range(3):
+            e.act_low[i] = float(self.action_scale_to_low[i])
+            e.act_high[i] = float(self.action_scale_to_high[i])
+        tnames = [s["name"] for s in cfg["target"]["states"]]
+        if tnames != ["roll", "pitch", "Va"]:
+            raise NotImplementedError("targets must be [roll, pitch, Va]")
+        for i, name in enumerate(tnames):
+            p = self.target_props[name]
+            cls = p.get("class", "constant")
+            if cls not in FW_TGT:
+                raise NotImplementedError("target class %r" % cls)
+            if cls == "compensate" and name != "Va":
+                raise NotImplementedError("compensate target for %s" % name)
+            e.target_class[i] = FW_TGT[cls]
+            e.target_wrap[i] = int(self.sim.vars[name].wrap)
+            rad = p.get("convert_to_radians", False)
+            cv = (lambda x: float(np.radians(x)) if rad else float(x))
+            e.target_low[i] = cv(p["low"])
+            e.target_high[i] = cv(p["high"])
+            e.target_delta[i] = cv(p["delta"]) if p.get("delta") is not None else float("nan")
+            e.target_bound[i] = cv(p["bound"]) if p.get("bound") is not None else float("nan")
+        t = cfg["target"]
+        e.streak_req = int(t["success_streak_req"])
+        if e.streak_req > 128:
+            raise NotImplementedError("success_streak_req > 128")
+        e.streak_frac = float(t["success_streak_fraction"])
+        e.on_success = 1 if t.get("on_success", "none") == "done" else 0
+        r = cfg["reward"]
+        fails = r.get("step_fail", 0)
+        e.step_fail_timesteps = int(fails == "timesteps")
+        e.step_fail_value = 0.0 if fails == "timesteps" else float(fails)
+        for term in r["terms"]:
+            fc = term["function_class"]
+            if fc not in FW_FUN:
+                raise ValueError("Unexpected function class {}".format(fc))
+            e.term_present[FW_FUN[fc]] = 1
+            e.term_weight[FW_FUN[fc]] = float(term["weight"])
+        if len(r["factors"]) > FW_MAX_REW:
+            raise NotImplementedError("more than %d reward factors" % FW_MAX_REW)
+        e.n_rew = len(r["factors"])
+        for i, f in enumerate(r["factors"]):
+            F = e.rew[i]
+            cls, typ = f["class"], f["type"]
+            if cls == "action":
+                if typ == "value":
+                    F.kind = FW_REW_ACTION_VALUE
+                elif typ == "delta":
+                    F.kind = FW_REW_ACTION_DELTA
+                    F.window = int(f["window_size"])
+                    if F.window > FW_MAX_WINDOW:
+                        raise NotImplementedError("reward window > %d" % FW_MAX_WINDOW)
+                elif typ == "bound":
+                    F.kind = FW_REW_ACTION_BOUND
+                    if bm is None:
+                        raise NotImplementedError("action bound reward without bounds_multiplier")
+                else:
+                    raise ValueError("Unexpected type {} for reward class action".format(typ))
+            elif cls == "state":
+                if typ == "error":
+                    F.kind, F.var = FW_REW_STATE_ERROR, TARGET_INDEX[f["name"]]
+                elif typ == "value":
+                    F.kind, F.var = FW_REW_STATE_VALUE, STATE_VAR_IDS[f["name"]]
+                else:
+                    raise NotImplementedError("state reward type %r" % typ)
+            else:
+                raise NotImplementedError("reward class %r" % cls)
+            fc = f["function_class"]
+            if fc not in FW_FUN:
+                raise ValueError("Unexpected function class {} for {}".format(fc, f["name"]))
+            F.fun = FW_FUN[fc]
+            if not e.term_present[F.fun]:
+                raise KeyError(fc)
+            F.shaping = int(bool(f.get("shaping", False)))
+            F.scaling = float(f["scaling"])
+            F.max = float(f["max"]) if f.get("max") is not None else INF
+            F.sign = float(f.get("sign", -1))
+        return e
+
+    def target_sampling(self):
+        """(low, high, delta) per target in radians where configured (sample_target, fixed_wing.py:654-746)."""
+        out = []
+        for name in ["roll", "pitch", "Va"]:
+            p = self.target_props[name]
+            rad = p.get("convert_to_radians", False)
+            cv = (lambda x: float(np.radians(x)) if rad else float(x))
+            out.append((cv(p["low"]), cv(p["high"]), cv(p["delta"]) if p.get("delta") is not None else None))
+        return out
+
+
+def init_array(states, n, spec=None):
+    """Pack explicit reset dicts (reference ``reset(state=...)`` keys) into [FW_NINIT][n] with NaN = sample."""
+    arr = np.full((FW_NINIT, n), np.nan, dtype=np.float64)
+    if states is None:
+        return arr
+    if isinstance(states, dict):
+        states = [states] * n
+    keys = {"roll": FW_I_ROLL, "pitch": FW_I_PITCH, "yaw": FW_I_YAW, "omega_p": FW_I_P, "omega_q": FW_I_Q,
+            "omega_r": FW_I_R, "position_n": FW_I_PN, "position_e": FW_I_PE, "position_d": FW_I_PD,
+            "velocity_u": FW_I_U, "velocity_v": FW_I_V, "velocity_w": FW_I_W,
+            "wind_n": FW_I_WIND_N, "wind_e": FW_I_WIND_E, "wind_d": FW_I_WIND_D}
+    dyn = spec.dynamics if spec is not None else ["elevon_right", "elevon_left", "throttle"]
+    for i, st in enumerate(states):
+        if st is None:
+            continue
+        for k, v in st.items():
+            if k in keys:
+                arr[keys[k], i] = v
+            elif k == "wind":
+                if v is None or isinstance(v, (int, float)):
+                    if v is not None:
+                        raise NotImplementedError("scalar wind magnitude in reset state")
+                    continue
+                arr[FW_I_WIND_N:FW_I_WIND_D + 1, i] = v
+            elif k in dyn:
+                j = dyn.index(k)
+                if isinstance(v, (tuple, list, np.ndarray)):
+                    arr[FW_I_ACT0 + 2 * j, i] = v[0]
+                    arr[FW_I_ACT0 + 2 * j + 1, i] = v[1]
+                else:
+                    arr[FW_I_ACT0 + 2 * j, i] = v
+                    arr[FW_I_ACT0 + 2 * j + 1, i] = 0.0
+            elif k in ("Va", "alpha", "beta", "attitude", "elevator", "aileron", "rudder") or "energy" in k:
+                continue  # ignored by PyFly.reset (pyfly.py:1273-1282)
+            else:
+                raise KeyError("unknown reset state key %r" % k)
+    return arr
