@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""Throughput benchmark: env-steps/s of the fused fixed-wing env step on MI355X.
+
+One "step" = one FixedWingAircraft.step (PyFly.step with scipy-RK45 step
+control + env epilogue + masked auto-reset) for every aircraft of the batch,
+i.e. one launch of k_env_step over N = --envs aircraft per GPU.  Actions are
+uniform random in [-1, 1]^3, pre-generated on the device (a pool of 16 batches
+cycled), so the timed region contains only the hot path.
+
+Workload (BASELINE.json configs[2]): 65536 parallel aircraft per GPU,
+attitude-tracking task (fixed_wing_config.json defaults), fp32, turbulence off.
+Multi-GPU: one process per GPU (torchrun), each rank owns its own 65536 envs
+(weak scaling, disjoint Philox streams), no collective on the data path.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from tum_adlr_deep_reinforcement_learning_amd import config as C  # noqa: E402
+from tum_adlr_deep_reinforcement_learning_amd.engine import Engine  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md: 8.0 TB/s spec)
+
+
+def algorithmic_bytes_per_env_step(spec, esz=4):
+    """HBM bytes one aircraft moves per env step in k_env_step (steady state, no reset).
+
+    reads : ODE state 19, elevator/aileron 2, steady wind 3, targets 3, action 3,
+            previous actions ring (act_window*3), ep_return 1            -> T
+            steps word, episode word, goal history 4 words               -> u32
+    writes: ODE state 19, derived 8, targets 3, ring slot 3, ep_return 1,
+            observation n_obs, reward 1                                  -> T
+            steps word, goal history 4 words, term code                  -> u32
+            done flag                                                    -> u8
+    """
+    act_window = 1
+    for o in spec.cfg["observation"]["states"]:
+        if o["type"] == "action" and spec.scale_actions:
+            act_window = max(act_window, int(o.get("window_size", 1)) - 1)
+    for f in spec.cfg["reward"]["factors"]:
+        if f["class"] == "action" and f["type"] == "delta":
+            act_window = max(act_window, int(f["window_size"]) - 1)
+    rd = (19 + 2 + 3 + 3 + 3 + act_window * 3 + 1) * esz + (1 + 1 + 4) * 4
+    wr = (19 + 8 + 3 + 3 + 1 + spec.n_obs + 1) * esz + (1 + 4 + 1) * 4 + 1
+    return rd, wr
+
+
+def cpu_baseline(seconds=12.0):
+    """The CPU oracle (oracle/fw_oracle.c, fp64 C port of the reference step) on one host core."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import oracle as O
+    spec = C.EnvSpec(sim_config_kw={"turbulence": False})
+    sc, ec = spec.sim.struct(), spec.struct()
+    rng = np.random.RandomState(0)
+    n_env = 64
+    envs = []
+    for j in range(n_env):
+        e = O.OracleEnv(sc, ec, spec.n_obs)
+        init = np.zeros(C.FW_NINIT)
+        init[C.FW_I_ROLL], init[C.FW_I_PITCH] = rng.uniform(-1.9, 1.9), rng.uniform(-0.78, 0.78)
+        init[C.FW_I_U] = rng.uniform(10, 23)
+        init[C.FW_I_PD] = -50.0
+        e.reset(init, np.array([rng.uniform(-1, 1), rng.uniform(-0.4, 0.4), rng.uniform(15, 28)]))
+        envs.append((e, init))
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for e, init in envs:
+            _, _, done, _, _ = e.step(rng.uniform(-1, 1, 3))
+            steps += 1
+            if done:
+                e.reset(init, np.array([0.1, 0.0, 20.0]))
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": "%d env steps (64 envs x U(-1,1) actions, default task, turbulence off) of the fp64 C oracle "
+                      "on 1 host core in %.1f s" % (steps, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--envs", type=int, default=65536, help="aircraft per GPU")
+    ap.add_argument("--precision", default="float32", choices=["float32", "float64"])
+    ap.add_argument("--turbulence", action="store_true", help="light Dryden turbulence + random steady wind")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    # pyfly_config.json defaults: random steady wind |w| <= 8 m/s; Dryden only with --turbulence
+    spec = C.EnvSpec(sim_config_kw={"turbulence": bool(args.turbulence), "turbulence_intensity": "light"})
+    n = args.envs
+    eng = Engine(spec.sim, spec, n, device=dev, precision=args.precision)
+    eng.seed(1234, env_offset=rank * n)
+    eng.reset()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1 + rank)
+    pool = torch.rand(16, n, 3, generator=gen, device=dev, dtype=eng.dtype) * 2 - 1
+    stream = torch.cuda.current_stream(dev)
+
+    for s in range(args.warmup):
+        eng.env_step(pool[s % 16], stats=False)
+    torch.cuda.synchronize(dev)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        ev[s][0].record(stream)
+        eng.env_step(pool[s % 16], stats=False)
+        ev[s][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    el = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = float(el[0]), float(el[1])
+
+    total_steps = n * world * args.steps
+    value = total_steps / elapsed
+    esz = 4 if args.precision == "float32" else 8
+    rd, wr = algorithmic_bytes_per_env_step(spec, esz)
+    achieved = (rd + wr) * n / (kern_ms * 1e-3) / 1e9  # GB/s per GPU, dominant kernel
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_env_step.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                pm = json.load(f)
+            if pm.get("envs") == n and pm.get("precision") == args.precision:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(args.cpu_seconds)
+        out = {
+            "metric": "env-steps/sec at 64k parallel aircraft, 1/2/4/8 MI355X; % HBM roofline",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" if args.precision == "float32" else "f64",
+            "data": "synthetic (seeded Philox initial states, U(-1,1) actions pre-generated on device)",
+            "config": {"workload": "FixedWingAircraft.step x %d aircraft per GPU (attitude task, fixed_wing_config "
+                                   "defaults, %s, RK45 rtol=1e-3 atol=1e-6, auto-reset)"
+                                   % (n, "light Dryden + steady wind" if args.turbulence else
+                                      "steady wind, turbulence off"),
+                       "envs_per_gpu": n, "global_envs": n * world, "kernel": "k_env_step",
+                       "parallelism": "env-dp%d" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes_per_env_step": rd + wr, "kernel_ms": kern_ms},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

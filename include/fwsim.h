@@ -203,7 +203,7 @@ enum fw_init_field {
 #define FW_BLK_DERIVED 1    /* 8 rows, T: roll pitch yaw Va alpha beta elevator aileron */
 #define FW_BLK_TARGET 2     /* 3 rows, T */
 #define FW_BLK_WIND 3       /* 3 rows, T: steady wind n e d */
-#define FW_BLK_STEPS 4      /* 2 rows, int32: steps_count, steps_for_current_target */
+#define FW_BLK_STEPS 4      /* 1 row, uint32: steps_count | steps_for_current_target << 16 */
 #define FW_BLK_COMMAND 5    /* 3 rows, T: last constrained commands (input order) */
 #define FW_NBLK 6
 

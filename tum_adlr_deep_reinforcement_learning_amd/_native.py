@@ -1,0 +1,115 @@
+"""Build and load libfwsim.so -- the gfx950 kernels behind the C ABI of include/fwsim.h.
+
+The library is built in-tree (``tum_adlr_deep_reinforcement_learning_amd/lib/libfwsim.so``)
+with hipcc for ``--offload-arch=gfx950``.  There is no CPU fallback: if the
+library is missing the product path raises.
+"""
+import ctypes
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB_DIR = os.path.join(PKG, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libfwsim.so")
+HEADER = os.path.join(ROOT, "include", "fwsim.h")
+SOURCES = [os.path.join(CSRC, "fw_kernels.hip"), os.path.join(CSRC, "fw_device.hpp"), HEADER]
+ARCH = os.environ.get("FWSIM_ARCH", "gfx950")
+
+_lib = None
+
+
+class FwError(RuntimeError):
+    pass
+
+
+def _hipcc():
+    return os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def needs_build():
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    return any(os.path.getmtime(s) > t for s in SOURCES if os.path.exists(s))
+
+
+EXTRA_FLAGS = ["-fno-slp-vectorize"]  # packed-f32 pairing costs register moves here
+
+
+def build(force=False, verbose=False, out=None, extra=None):
+    """Compile csrc/fw_kernels.hip into lib/libfwsim.so (seconds; cross-compiles without a GPU)."""
+    out = out or LIB_PATH
+    if out == LIB_PATH and not force and not needs_build():
+        return LIB_PATH
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = out + ".tmp"
+    flags = EXTRA_FLAGS if extra is None else extra
+    cmd = [_hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared"] + flags + ["-o", tmp,
+           os.path.join(CSRC, "fw_kernels.hip")]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(tmp, out)
+    return out
+
+
+_c = ctypes
+_vp = _c.c_void_p
+_i32 = _c.c_int32
+_i64 = _c.c_int64
+
+# name -> (restype, argtypes); must match include/fwsim.h
+SIGNATURES = {
+    "fw_abi_version": (_c.c_int, []),
+    "fw_last_error": (_c.c_int, [_c.c_char_p, _c.c_size_t]),
+    "fw_create": (_c.c_int, [_vp, _vp, _i64, _i32, _i32, _c.POINTER(_vp)]),
+    "fw_destroy": (_c.c_int, [_vp]),
+    "fw_num_envs": (_c.c_int, [_vp, _c.POINTER(_i64)]),
+    "fw_num_obs": (_c.c_int, [_vp, _c.POINTER(_i32)]),
+    "fw_seed": (_c.c_int, [_vp, _c.c_uint64, _i64]),
+    "fw_set_noise": (_c.c_int, [_vp, _vp, _i64]),
+    "fw_reset": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "fw_sim_step": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "fw_env_step": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
+    "fw_observe": (_c.c_int, [_vp, _vp, _vp]),
+    "fw_get_state": (_c.c_int, [_vp, _i32, _vp, _vp]),
+    "fw_set_state": (_c.c_int, [_vp, _i32, _vp, _vp]),
+    "fw_update_config": (_c.c_int, [_vp, _vp, _vp]),
+}
+
+
+def load(path=None):
+    """Load libfwsim.so (building it first only if the sources are newer and hipcc exists).
+
+    ``FWSIM_LIB`` may point at an alternative build (A/B experiments)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or os.environ.get("FWSIM_LIB") or LIB_PATH
+    if path == LIB_PATH and needs_build() and os.path.exists(_hipcc()):
+        build()
+    if not os.path.exists(path):
+        raise FwError("libfwsim.so not found at %s -- run __graft_entry__.build() (no CPU fallback exists)" % path)
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if lib.fw_abi_version() != 1:
+        raise FwError("libfwsim ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def last_error():
+    buf = ctypes.create_string_buffer(1024)
+    load().fw_last_error(buf, len(buf))
+    return buf.value.decode(errors="replace")
+
+
+def check(rc, what=""):
+    if rc != 0:
+        raise FwError("%s failed (%d): %s" % (what, rc, last_error()))
+    return rc

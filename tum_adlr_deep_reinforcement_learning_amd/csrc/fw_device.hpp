@@ -1,0 +1,878 @@
+// fw_device.hpp -- per-aircraft physics + env epilogue for the fused CDNA4 kernels.
+//
+// One lane owns one aircraft for a whole env step: the 19-element ODE state,
+// the Dormand-Prince stage accumulators and the error estimate all live in
+// VGPRs; nothing but the SoA state row is read or written per step.  Every
+// function is __host__ __device__ so tests/native can also exercise this exact
+// code on the CPU against the independent oracle (oracle/fw_oracle.c).
+//
+// Reference behaviour replicated (paths relative to the reference checkout):
+//   PyFly._dynamics / _forces / _f_*   magpie/libs/pyfly/pyfly/pyfly.py:1450-1747
+//   Variable/ControlVariable conditions pyfly.py:114-133, 312-328
+//   PyFly.step save + post-step        pyfly.py:1358-1420, 1852-1881
+//   scipy 1.15.3 RK45 step control     integrate/_ivp/rk.py:111-173, common.py:68-134
+//   FixedWingAircraft.step epilogue    magpie/libs/fixed-wing-gym/gym_fixed_wing/fixed_wing.py:483-628
+//
+// Code-size rule (measured, profiles/): with one wave per SIMD the kernel is
+// instruction-fetch bound as soon as its hot loop outgrows the instruction
+// cache, so the integrator below contains exactly ONE inlined RHS, driven by a
+// wave-uniform stage loop (initial-step probe, six stages, accept/reject).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/fwsim.h"
+
+#define FW_HD __host__ __device__ __forceinline__
+
+namespace fw {
+
+constexpr int NY = FW_NY;
+constexpr double PI_D = 3.141592653589793;
+
+template <typename T>
+struct Lim {
+  T vmin, vmax, cmin, cmax;
+};
+
+// Device-resident configuration (one copy per handle, read with scalar loads:
+// every address is wave-uniform).  Precomputed products keep the RHS short.
+template <typename T>
+struct DevCfg {
+  // ---- simulator ----
+  double t_bound;            // dt
+  T dt, rtol, atol;
+  T half_rho, S, b, c, mass, inv_mass, mg, inv_Jy;
+  T gam[9];
+  T M, a0, pi_e_ar;
+  T CL0, CLa, CLq, CLde, CDp, CDq, CDb1, CDb2, CDde, Cm0, Cma, Cmq, Cmde, Cmfp;
+  T CY0, CYb, CYp, CYr, CYda, CYdr, Cl0, Clb, Clp, Clr, Clda, Cldr, Cn0, Cnb, Cnp, Cnr, Cnda, Cndr;
+  T kmotor, prop_k, kTP, kOmega;
+  T rho, Sprop, Cprop;
+  T ac[3][6];                // actuator coefs c00 c01 c02 c10 c11 c12 (ControlVariable.coefs)
+  T dot_max[3];
+  Lim<T> lim[FW_NVAR];
+  T init_min[FW_NVAR], init_max[FW_NVAR];
+  uint32_t cmask, clipmask, wrapmask;  // per fw_var: has constraint / has clip / wraps
+  uint32_t dotmask;                    // per actuator: dot_max finite
+  int elevon, disabled_inputs, turbulence, turb_len, wind_random;
+  int trig_alpha, trig_beta;           // alpha/beta limited -> use trig of the clipped angle
+  int euler_exact;                     // roll/pitch/yaw limited -> Euler-angle rotation post step
+  T wind_mag_min, wind_mag_max, wind_init_min[3], wind_init_max[3];
+  T g0[6], g1[6], noise_scale;
+  // ---- env ----
+  int has_env;
+  int steps_max, n_obs, scale_actions, has_bounds, streak_req, on_success, n_rew;
+  int step_fail_timesteps;
+  int act_window;                      // ring length of raw actions kept (max window - 1, >= 1)
+  int cmd_window;                      // ring length of commands kept (0 if unused)
+  T scale_low, scale_high, bmax, bmin;
+  T act_low[3], act_high[3];
+  int target_class[3], target_wrap[3];
+  T target_low[3], target_high[3], target_delta[3], target_bound[3];
+  int has_delta[3], has_bound[3];
+  T streak_frac;
+  T step_fail_value;
+  T term_weight[3];
+  int term_present[3];
+  fw_obs_entry obs[FW_MAX_OBS];
+  fw_rew_factor rew[FW_MAX_REW];
+};
+
+// Re-materialise the (wave-uniform) config pointer so the scalar loads of the
+// ~90 aircraft constants are issued where they are used instead of being
+// hoisted out of the RK loop and pinned in SGPRs (which spills them into VGPR
+// lanes).  s_load from the scalar cache costs nothing next to the VALU work.
+template <typename T>
+FW_HD const DevCfg<T>& relaunder(const DevCfg<T>& c) {
+  return c;
+}
+
+// ---------------------------------------------------------------------------
+// arithmetic helpers.  fp64 = IEEE-exact (the parity build); fp32 = the
+// hardware single-instruction forms (v_rcp_f32 / v_sqrt_f32 / v_exp_f32 /
+// v_log_f32, ~1 ulp) instead of the multi-instruction correctly-rounded
+// sequences: an fp32 trajectory differs from fp64 at the 1e-7 level anyway.
+// ---------------------------------------------------------------------------
+FW_HD double fdiv(double a, double b) { return a / b; }
+FW_HD double frcp(double a) { return 1.0 / a; }
+FW_HD double fsqrt(double a) { return sqrt(a); }
+FW_HD double fexp(double a) { return exp(a); }
+FW_HD double fpow(double a, double p) { return pow(a, p); }
+FW_HD float frcp(float a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rcpf(a);
+#else
+  return 1.0f / a;
+#endif
+}
+FW_HD float fdiv(float a, float b) { return a * frcp(b); }
+FW_HD float fsqrt(float a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_sqrtf(a);
+#else
+  return sqrtf(a);
+#endif
+}
+FW_HD float fexp(float a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_exp2f(a * 1.4426950408889634f);
+#else
+  return expf(a);
+#endif
+}
+FW_HD float fpow(float a, float p) {  // a > 0
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_exp2f(p * __builtin_amdgcn_logf(a));
+#else
+  return powf(a, p);
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+FW_HD bool any_lane(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __any(p);
+#else
+  return p;
+#endif
+}
+
+template <typename T>
+FW_HD T sgn(T x) {
+  return (T)((x > T(0)) - (x < T(0)));
+}
+
+template <typename T>
+FW_HD T clipv(T x, T lo, T hi) {  // np.clip semantics (NaN propagates)
+  x = x < lo ? lo : x;
+  x = x > hi ? hi : x;
+  return x;
+}
+
+// Variable.apply_conditions (pyfly.py:114-133).  Records the first violation.
+template <typename T>
+FW_HD T cond(const DevCfg<T>& c, int v, T x, int& term) {
+  const uint32_t bit = 1u << v;
+  if (c.cmask & bit) {
+    if (!term && (x < c.lim[v].cmin || x > c.lim[v].cmax)) term = FW_TERM_VAR(v);
+  }
+  if (c.clipmask & bit) x = clipv(x, c.lim[v].vmin, c.lim[v].vmax);
+  if (c.wrapmask & bit) {
+    const T pi = T(PI_D);
+    if (fabs(x) > pi) x = sgn(x) * (fmod(fabs(x), pi) - pi);
+  }
+  return x;
+}
+
+// Philox4x32-10 counter-based RNG (Salmon et al., SC'11).
+FW_HD void philox(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t out[4]) {
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c0 = hi1 ^ c1 ^ k0;
+    c1 = lo1;
+    c2 = hi0 ^ c3 ^ k1;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  out[0] = c0;
+  out[1] = c1;
+  out[2] = c2;
+  out[3] = c3;
+}
+
+// uniform in (0, 1]: 32 random bits
+template <typename T>
+FW_HD T u01(uint32_t x) {
+  return (T)((double)x * 2.3283064365386963e-10 + 1.1641532182693481e-10);
+}
+
+// 4 standard normals from one Philox block (Box-Muller)
+template <typename T>
+FW_HD void normal4(const uint32_t r[4], T z[4]) {
+  const double two_pi = 6.283185307179586;
+  for (int k = 0; k < 2; k++) {
+    double u1 = (double)r[2 * k] * 2.3283064365386963e-10 + 1.1641532182693481e-10;
+    double u2 = (double)r[2 * k + 1] * 2.3283064365386963e-10;
+    T rad = (T)sqrt(-2.0 * log(u1));
+    T ang = (T)(two_pi * u2);
+    z[2 * k] = rad * cos(ang);
+    z[2 * k + 1] = rad * sin(ang);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// per-step context held constant across RK stages
+// ---------------------------------------------------------------------------
+template <typename T>
+struct StepCtx {
+  T sp[3];      // constrained dynamics set-points
+  T wind[3];    // steady wind (vehicle frame)
+  T tl[3];      // turbulence, linear (body)  -- ZOH over the step (pyfly.py:1502, 1839)
+  T ta[3];      // turbulence, angular
+  T elev0, ail0;  // stored elevator/aileron .value used by the t == 0 evaluation
+};
+
+// wind_b = R(q)·w + turb (quaternion branch of _rot_b_v, pyfly.py:1780-1800; 1843)
+template <typename T>
+FW_HD void airspeed_vec(const T* q, const T* w, const T* tl, const T* v, T va[3]) {
+  const T e0 = q[0], e1 = q[1], e2 = q[2], e3 = q[3];
+  const T R00 = T(-1) + T(2) * (e0 * e0 + e1 * e1), R01 = T(2) * (e1 * e2 + e3 * e0), R02 = T(2) * (e1 * e3 - e2 * e0);
+  const T R10 = T(2) * (e1 * e2 - e3 * e0), R11 = T(-1) + T(2) * (e0 * e0 + e2 * e2), R12 = T(2) * (e2 * e3 + e1 * e0);
+  const T R20 = T(2) * (e1 * e3 + e2 * e0), R21 = T(2) * (e2 * e3 - e1 * e0), R22 = T(-1) + T(2) * (e0 * e0 + e3 * e3);
+  va[0] = v[0] - (R00 * w[0] + R01 * w[1] + R02 * w[2] + tl[0]);
+  va[1] = v[1] - (R10 * w[0] + R11 * w[1] + R12 * w[2] + tl[1]);
+  va[2] = v[2] - (R20 * w[0] + R21 * w[1] + R22 * w[2] + tl[2]);
+}
+
+// Euler branch of _rot_b_v (pyfly.py:1757-1777) -- used post step when the Euler
+// angles may have been clipped (otherwise R(q_normalised) is the same matrix).
+template <typename T>
+FW_HD void airspeed_vec_euler(T phi, T th, T psi, const T* w, const T* tl, const T* v, T va[3]) {
+  const T cph = cos(phi), sph = sin(phi), cth = cos(th), sth = sin(th), cps = cos(psi), sps = sin(psi);
+  const T R00 = cth * cps, R01 = cth * sps, R02 = -sth;
+  const T R10 = sph * sth * cps - cph * sps, R11 = sph * sth * sps + cph * cps, R12 = sph * cth;
+  const T R20 = cph * sth * cps + sph * sps, R21 = cph * sth * sps - sph * cps, R22 = cph * cth;
+  va[0] = v[0] - (R00 * w[0] + R01 * w[1] + R02 * w[2] + tl[0]);
+  va[1] = v[1] - (R10 * w[0] + R11 * w[1] + R12 * w[2] + tl[1]);
+  va[2] = v[2] - (R20 * w[0] + R21 * w[1] + R22 * w[2] + tl[2]);
+}
+
+// ---------------------------------------------------------------------------
+// RHS: PyFly._dynamics (pyfly.py:1450-1482).  first == (t == 0): the stored,
+// already-conditioned state is used as is; otherwise the stage vector is
+// conditioned first (_set_states_from_ode_solution(save=False)), which can
+// terminate the step.  Returns the first violated condition (0 = none).
+// ---------------------------------------------------------------------------
+template <typename T>
+FW_HD int rhs(const DevCfg<T>& c0, const StepCtx<T>& X, bool first, const T* y, T* dy) {
+  const DevCfg<T>& c = relaunder(c0);
+  int term = 0;
+  T om[3] = {y[4], y[5], y[6]};
+  T vel[3] = {y[10], y[11], y[12]};
+  T av[3] = {y[13], y[14], y[15]};
+  T ad[3] = {y[16], y[17], y[18]};
+  T elev = X.elev0, ail = X.ail0;
+  if (!first) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) om[i] = cond(c, FW_V_OMEGA_P + i, om[i], term);
+#pragma unroll
+    for (int i = 0; i < 3; i++) (void)cond(c, FW_V_POS_N + i, y[7 + i], term);
+#pragma unroll
+    for (int i = 0; i < 3; i++) vel[i] = cond(c, FW_V_VEL_U + i, vel[i], term);
+#pragma unroll
+    for (int j = 0; j < 3; j++) {  // Actuation.set_states (pyfly.py:479-492)
+      av[j] = cond(c, FW_V_ACT0 + j, av[j], term);
+      if (c.dotmask & (1u << j)) ad[j] = clipv(ad[j], -c.dot_max[j], c.dot_max[j]);
+    }
+    if (c.elevon) {
+      ail = (-av[0] + av[1]) * T(0.5);
+      elev = (av[0] + av[1]) * T(0.5);
+      ail = cond(c, FW_V_AILERON, ail, term);
+      elev = cond(c, FW_V_ELEVATOR, elev, term);
+    } else {
+      elev = av[0];
+      ail = av[1];
+    }
+  }
+  const T thr = av[2];
+  const T e0 = y[0], e1 = y[1], e2 = y[2], e3 = y[3];  // raw attitude (pyfly.py:1464)
+
+  // ---- _forces (pyfly.py:1484-1643) ----
+  T p = om[0], q = om[1], r = om[2];
+  if (c.turbulence) {
+    p -= X.ta[0];
+    q -= X.ta[1];
+    r -= X.ta[2];
+  }
+  T va[3];
+  airspeed_vec(y, X.wind, X.tl, vel, va);
+  const T Va_raw = fsqrt(va[0] * va[0] + va[1] * va[1] + va[2] * va[2]);
+  T alpha = atan2(va[2], va[0]);
+  const T sb_raw = fdiv(va[1], Va_raw);
+  T beta = asin(sb_raw);
+  const T Va = cond(c, FW_V_VA, Va_raw, term);
+  alpha = cond(c, FW_V_ALPHA, alpha, term);
+  beta = cond(c, FW_V_BETA, beta, term);
+
+  T sa, ca, sb, cb;
+  if (c.trig_alpha) {
+    sa = sin(alpha);
+    ca = cos(alpha);
+  } else {  // sin/cos of atan2(z, x) without the transcendental
+    const T rxz2 = va[0] * va[0] + va[2] * va[2];
+    const T irxz = frcp(fsqrt(rxz2));
+    sa = rxz2 > T(0) ? va[2] * irxz : T(0);
+    ca = rxz2 > T(0) ? va[0] * irxz : T(1);
+  }
+  if (c.trig_beta) {
+    sb = sin(beta);
+    cb = cos(beta);
+  } else {  // beta = asin(s): sin = s, cos = sqrt(1 - s^2)
+    sb = sb_raw;
+    cb = fsqrt(fmax(T(1) - sb_raw * sb_raw, T(0)));
+  }
+
+  const T pre = c.half_rho * (Va * Va) * c.S;
+  const T fg0 = c.mg * (T(2) * (e1 * e3 - e2 * e0));
+  const T fg1 = c.mg * (T(2) * (e2 * e3 + e1 * e0));
+  const T fg2 = c.mg * (e3 * e3 + e0 * e0 - e1 * e1 - e2 * e2);
+  const T ex1 = fexp(-c.M * (alpha - c.a0));
+  const T ex2 = fexp(c.M * (alpha + c.a0));
+  // stall blend; an overflowed exponential means sigma == 1 to working precision
+  T sigma = fdiv(T(1) + ex1 + ex2, (T(1) + ex1) * (T(1) + ex2));
+  const T huge = sizeof(T) == 4 ? T(3.0e38f) : T(1e300);
+  if (ex1 > huge || ex2 > huge) sigma = T(1);
+  const T sgna = sgn(alpha);
+  const T CLlin = c.CL0 + c.CLa * alpha;
+  const T CL = (T(1) - sigma) * CLlin + sigma * (T(2) * sgna * sa * sa * ca);
+  const T inv2Va = frcp(T(2) * Va);
+  const T flift = pre * (CL + c.CLq * c.c * inv2Va * q + c.CLde * elev);
+  const T CD = c.CDp + fdiv((T(1) - sigma) * (CLlin * CLlin), c.pi_e_ar) + sigma * (T(2) * sgna * (sa * sa * sa));
+  const T CDb = c.CDb1 * beta + c.CDb2 * beta * beta;
+  const T fdrag = pre * (CD + CDb + c.CDq * c.c * inv2Va * q + c.CDde * elev * elev);
+  const T Cm = (T(1) - sigma) * (c.Cm0 + c.Cma * alpha) + sigma * (c.Cmfp * sgna * sa * sa);
+  const T mm = pre * c.c * (Cm + c.Cmq * c.b * inv2Va * q + c.Cmde * elev);
+  const T bp = c.b * inv2Va * p, br = c.b * inv2Va * r;
+  const T fy = pre * (c.CY0 + c.CYb * beta + c.CYp * bp + c.CYr * br + c.CYda * ail);
+  const T ll = pre * c.b * (c.Cl0 + c.Clb * beta + c.Clp * bp + c.Clr * br + c.Clda * ail);
+  const T nn = pre * c.b * (c.Cn0 + c.Cnb * beta + c.Cnp * bp + c.Cnr * br + c.Cnda * ail);
+  // f_aero = R_euler(0, alpha, beta) . [-D, Y, -L]
+  const T fa0 = ca * cb * (-fdrag) + ca * sb * fy - sa * (-flift);
+  const T fa1 = -sb * (-fdrag) + cb * fy;
+  const T fa2 = sa * cb * (-fdrag) + sa * sb * fy + ca * (-flift);
+  const T Vd = Va + thr * (c.kmotor - Va);
+  const T fprop = c.prop_k * Vd * (Vd - Va);
+  const T kt = c.kOmega * thr;
+  const T tprop = -c.kTP * kt * kt;
+  const T f0 = fprop + fg0 + fa0, f1 = fg1 + fa1, f2 = fg2 + fa2;
+  const T t0 = ll + tprop, t1 = mm, t2 = nn;
+
+  const T P0 = om[0], Q0 = om[1], R0 = om[2];
+  // _f_attitude_dot (pyfly.py:1645-1657)
+  dy[0] = T(0.5) * (-P0 * e1 - Q0 * e2 - R0 * e3);
+  dy[1] = T(0.5) * (P0 * e0 + R0 * e2 - Q0 * e3);
+  dy[2] = T(0.5) * (Q0 * e0 - R0 * e1 + P0 * e3);
+  dy[3] = T(0.5) * (R0 * e0 + Q0 * e1 - P0 * e2);
+  // _f_omega_dot (pyfly.py:1659-1683)
+  dy[4] = c.gam[1] * P0 * Q0 - c.gam[2] * Q0 * R0 + c.gam[3] * t0 + c.gam[4] * t2;
+  dy[5] = c.gam[5] * P0 * R0 - c.gam[6] * (P0 * P0 - R0 * R0) + t1 * c.inv_Jy;
+  dy[6] = c.gam[7] * P0 * Q0 - c.gam[1] * Q0 * R0 + c.gam[4] * t0 + c.gam[8] * t2;
+  // _f_p_dot (pyfly.py:1706-1737)
+  dy[7] = (e1 * e1 + e0 * e0 - e2 * e2 - e3 * e3) * vel[0] + T(2) * (e1 * e2 - e3 * e0) * vel[1] +
+          T(2) * (e1 * e3 + e2 * e0) * vel[2];
+  dy[8] = T(2) * (e1 * e2 + e3 * e0) * vel[0] + (e2 * e2 + e0 * e0 - e1 * e1 - e3 * e3) * vel[1] +
+          T(2) * (e2 * e3 - e1 * e0) * vel[2];
+  dy[9] = T(2) * (e1 * e3 - e2 * e0) * vel[0] + T(2) * (e2 * e3 + e1 * e0) * vel[1] +
+          (e3 * e3 + e0 * e0 - e1 * e1 - e2 * e2) * vel[2];
+  // _f_v_dot (pyfly.py:1685-1704)
+  dy[10] = R0 * vel[1] - Q0 * vel[2] + f0 * c.inv_mass;
+  dy[11] = P0 * vel[2] - R0 * vel[0] + f1 * c.inv_mass;
+  dy[12] = Q0 * vel[0] - P0 * vel[1] + f2 * c.inv_mass;
+  // Actuation.rhs (pyfly.py:519-543)
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    dy[13 + j] = av[j] * c.ac[j][0] + X.sp[j] * c.ac[j][2] + ad[j] * c.ac[j][1];
+    dy[16 + j] = av[j] * c.ac[j][3] + X.sp[j] * c.ac[j][5] + ad[j] * c.ac[j][4];
+  }
+  return term;
+}
+
+// ---------------------------------------------------------------------------
+// scipy RK45 (Dormand-Prince 5(4), FSAL) integrating y from 0 to dt with the
+// solve_ivp default controller; t/h bookkeeping in fp64 for both precisions so
+// the step-size sequence follows scipy's.
+//
+// Each lane runs its own phase machine around ONE rhs() evaluation per loop
+// iteration:  phase 0  f0 = f(0, y0)                       (RungeKutta.__init__)
+//             phase 1  probe f(h0, y0 + h0 f0)             (select_initial_step)
+//             phase 2..7  stage s = phase - 1 of an attempt, s = 6 is f(t_new, y_new)
+// Stage vectors are folded into running sums as soon as they are produced
+// (P_s = sum_j A[s][j] K_j for the stages to come, YB = sum_j B_j K_j,
+// ER = sum_j E_j K_j); per element the sums run j = 0, 1, ... as scipy's
+// np.dot(K[:s].T, a[:s]) (rk.py:58-64).
+// ---------------------------------------------------------------------------
+
+// Each wave walks ONE uniform sequence of RHS evaluations -- f0, the initial
+// step probe, then stages 1..6 of trial steps -- around a single inlined rhs()
+// call; lanes whose integration has finished (or terminated) sit masked.  The
+// stage index is wave-uniform, so every Butcher coefficient is a scalar
+// literal and each stage's fold is straight-line code.  Stage vectors are
+// folded into running sums as soon as they are produced (P_s = sum_j A[s][j]
+// K_j for the stages to come, YB = sum_j B_j K_j, ER = sum_j E_j K_j); per
+// element the sums run j = 0, 1, ... as scipy's np.dot(K[:s].T, a[:s])
+// (rk.py:58-64).
+template <typename T>
+FW_HD int rk45(const DevCfg<T>& c, const StepCtx<T>& X, T* y_io, T* __restrict__ sy, T* __restrict__ sf, int stride,
+               int& nfev, int& nacc) {
+  constexpr double A10 = 1.0 / 5;
+  constexpr double A20 = 3.0 / 40, A21 = 9.0 / 40;
+  constexpr double A30 = 44.0 / 45, A31 = -56.0 / 15, A32 = 32.0 / 9;
+  constexpr double A40 = 19372.0 / 6561, A41 = -25360.0 / 2187, A42 = 64448.0 / 6561, A43 = -212.0 / 729;
+  constexpr double A50 = 9017.0 / 3168, A51 = -355.0 / 33, A52 = 46732.0 / 5247, A53 = 49.0 / 176,
+                   A54 = -5103.0 / 18656;
+  constexpr double B0 = 35.0 / 384, B2 = 500.0 / 1113, B3 = 125.0 / 192, B4 = -2187.0 / 6784, B5 = 11.0 / 84;
+  constexpr double E0 = -71.0 / 57600, E2 = 71.0 / 16695, E3 = -71.0 / 1920, E4 = 17253.0 / 339200,
+                   E5 = -22.0 / 525, E6 = 1.0 / 40;
+  const T rtol = c.rtol, atol = c.atol;
+  const double t_bound = c.t_bound;
+  const T inv_sqrt_n = T(0.22941573387056177);  // 1 / sqrt(19)
+
+  // y and f (the accepted state and its derivative) live in LDS slots of this
+  // lane (element i at s[i * stride]); only the stage accumulators stay in VGPRs.
+#define Y(i) sy[(i) * stride]
+#define F(i) sf[(i) * stride]
+  T P3[NY], P4[NY], P5[NY], YB[NY], ER[NY], ys[NY], K[NY];
+#pragma unroll
+  for (int i = 0; i < NY; i++) {
+    ys[i] = y_io[i];
+    Y(i) = y_io[i];
+  }
+  double t = 0.0, h_abs = 0.0, h0 = 0.0, t_new = 0.0, min_step = 0.0;
+  T ht = T(0), d1 = T(0);
+  bool rejected = false, active = true;
+  int result = 0;
+  nfev = 0;
+  nacc = 0;
+
+  // stage: 0 = f0, 1 = probe, 2..7 = RK stage s = stage - 1 (s = 6: f(t_new, y_new))
+  for (int stage = 0;;) {
+    if (!any_lane(active)) break;
+    if (active) {
+      nfev++;
+      const int term = rhs(c, X, stage == 0, ys, K);
+      if (term) {
+        result = term;
+        active = false;
+      }
+    }
+    bool begin_step = false, begin_attempt = false;
+    if (stage == 0) {  // ---- f0; select_initial_step (common.py:68-110)
+      if (active) {
+        T d0s = T(0), d1s = T(0);
+#pragma unroll
+        for (int i = 0; i < NY; i++) {
+          F(i) = K[i];
+          const T isc = frcp(atol + fabs(Y(i)) * rtol);
+          const T a = Y(i) * isc, b = K[i] * isc;
+          d0s += a * a;
+          d1s += b * b;
+        }
+        const T d0 = fsqrt(d0s) * inv_sqrt_n;
+        d1 = fsqrt(d1s) * inv_sqrt_n;
+        h0 = (d0 < T(1e-5) || d1 < T(1e-5)) ? 1e-6 : 0.01 * (double)d0 / (double)d1;
+        if (h0 > t_bound) h0 = t_bound;
+        const T h0t = (T)h0;
+#pragma unroll
+        for (int i = 0; i < NY; i++) ys[i] = Y(i) + h0t * F(i);
+      }
+      stage = 1;
+    } else if (stage == 1) {  // ---- probe; select_initial_step (common.py:111-134)
+      if (active) {
+        T d2s = T(0);
+#pragma unroll
+        for (int i = 0; i < NY; i++) {
+          const T a = (K[i] - F(i)) * frcp(atol + fabs(Y(i)) * rtol);
+          d2s += a * a;
+        }
+        const double d2 = (double)(fsqrt(d2s) * inv_sqrt_n) / h0;
+        double h1;
+        if ((double)d1 <= 1e-15 && d2 <= 1e-15) h1 = fmax(1e-6, h0 * 1e-3);
+        else h1 = pow(0.01 / fmax((double)d1, d2), 1.0 / 5.0);
+        h_abs = fmin(fmin(100 * h0, h1), t_bound);
+        begin_step = true;
+      }
+      stage = 2;
+    } else if (stage == 2) {  // K = K1
+      if (active) {
+#pragma unroll
+        for (int i = 0; i < NY; i++) {
+          ys[i] = Y(i) + (F(i) * T(A20) + K[i] * T(A21)) * ht;
+          P3[i] = F(i) * T(A30) + K[i] * T(A31);
+          P4[i] = F(i) * T(A40) + K[i] * T(A41);
+          P5[i] = F(i) * T(A50) + K[i] * T(A51);
+          YB[i] = F(i) * T(B0);
+          ER[i] = F(i) * T(E0);
+        }
+      }
+      stage = 3;
+    } else if (stage == 3) {  // K = K2
+      if (active) {
+#pragma unroll
+        for (int i = 0; i < NY; i++) {
+          P3[i] += K[i] * T(A32);
+          P4[i] += K[i] * T(A42);
+          P5[i] += K[i] * T(A52);
+          YB[i] += K[i] * T(B2);
+          ER[i] += K[i] * T(E2);
+          ys[i] = Y(i) + P3[i] * ht;
+        }
+      }
+      stage = 4;
+    } else if (stage == 4) {  // K = K3
+      if (active) {
+#pragma unroll
+        for (int i = 0; i < NY; i++) {
+          P4[i] += K[i] * T(A43);
+          P5[i] += K[i] * T(A53);
+          YB[i] += K[i] * T(B3);
+          ER[i] += K[i] * T(E3);
+          ys[i] = Y(i) + P4[i] * ht;
+        }
+      }
+      stage = 5;
+    } else if (stage == 5) {  // K = K4
+      if (active) {
+#pragma unroll
+        for (int i = 0; i < NY; i++) {
+          P5[i] += K[i] * T(A54);
+          YB[i] += K[i] * T(B4);
+          ER[i] += K[i] * T(E4);
+          ys[i] = Y(i) + P5[i] * ht;
+        }
+      }
+      stage = 6;
+    } else if (stage == 6) {  // K = K5; ys <- y_new
+      if (active) {
+#pragma unroll
+        for (int i = 0; i < NY; i++) {
+          YB[i] += K[i] * T(B5);
+          ER[i] += K[i] * T(E5);
+          ys[i] = Y(i) + ht * YB[i];
+        }
+      }
+      stage = 7;
+    } else {  // K = f(t_new, y_new): error norm + step control (rk.py:138-173)
+      if (active) {
+        T es = T(0);
+#pragma unroll
+        for (int i = 0; i < NY; i++) {
+          const T e = (ER[i] + K[i] * T(E6)) * ht;
+          const T q = e * frcp(atol + fmax(fabs(Y(i)), fabs(ys[i])) * rtol);
+          es += q * q;
+        }
+        const T en = fsqrt(es) * inv_sqrt_n;
+        if (en < T(1)) {
+          double factor = (en == T(0)) ? 10.0 : fmin(10.0, 0.9 * (double)fpow(en, T(-0.2)));
+          if (rejected) factor = fmin(1.0, factor);
+          h_abs *= factor;
+          t = t_new;
+#pragma unroll
+          for (int i = 0; i < NY; i++) {
+            Y(i) = ys[i];
+            F(i) = K[i];
+          }
+          nacc++;
+          if (t - t_bound >= 0.0) active = false;  // OdeSolver.step: finished (base.py:203-204)
+          else begin_step = true;
+        } else {
+          h_abs *= fmax(0.2, 0.9 * (double)fpow(en, T(-0.2)));
+          rejected = true;
+          if (h_abs < min_step) {  // TOO_SMALL_STEP: solver failure
+            result = -1;
+            active = false;
+          } else {
+            begin_attempt = true;
+          }
+        }
+      }
+      stage = 2;
+    }
+    if (begin_step) {  // RungeKutta._step_impl entry (rk.py:111-124)
+      min_step = 10.0 * fabs(nextafter(t, 1e300) - t);
+      if (h_abs < min_step) h_abs = min_step;
+      rejected = false;
+      begin_attempt = true;
+    }
+    if (begin_attempt) {  // one trial step (rk.py:126-137); stage 1 input
+      double h = h_abs;
+      t_new = t + h;
+      if (t_new - t_bound > 0) t_new = t_bound;
+      h = t_new - t;
+      h_abs = fabs(h);
+      ht = (T)h;
+#pragma unroll
+      for (int i = 0; i < NY; i++) ys[i] = Y(i) + (F(i) * T(A10)) * ht;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NY; i++) y_io[i] = Y(i);
+#undef Y
+#undef F
+  return result;
+}
+
+// ---------------------------------------------------------------------------
+// Actuation.set_and_constrain_commands (pyfly.py:545-582).  cmd in/out in input
+// order (elevator, aileron, throttle); sp = dynamics set-points.
+// ---------------------------------------------------------------------------
+template <typename T>
+FW_HD int constrain_commands(const DevCfg<T>& c, T* cmd, T* sp) {
+  int term = 0;
+  if (c.elevon) {
+    T er = T(-1) * cmd[1] + cmd[0], el = cmd[1] + cmd[0];
+    er = cond(c, FW_V_ACT0, er, term);
+    el = cond(c, FW_V_ACT1, el, term);
+    const T thr = cond(c, FW_V_ACT2, cmd[2], term);
+    sp[0] = er;
+    sp[1] = el;
+    sp[2] = thr;
+    T ail = (-er + el) / T(2), elev = (er + el) / T(2);
+    elev = cond(c, FW_V_ELEVATOR, elev, term);
+    ail = cond(c, FW_V_AILERON, ail, term);
+    cmd[0] = elev;
+    cmd[1] = ail;
+    cmd[2] = thr;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      cmd[j] = cond(c, FW_V_ACT0 + j, cmd[j], term);
+      sp[j] = cmd[j];
+    }
+  }
+  return term;
+}
+
+// Dryden FIR at step k: j = k % L; 0 at chunk starts (dryden.py:193-261 as wired
+// by pyfly.py:781-783).  un1 / u0: N(0,1) samples of channels (u0,u1,u2,u3) at k-1, k.
+template <typename T>
+FW_HD void dryden(const DevCfg<T>& c, int k, const T* un1, const T* u0, T* tl, T* ta) {
+  const bool zero = (k % c.turb_len) == 0;
+  const int chan[6] = {0, 1, 2, 3, 1, 2};
+  T out[6];
+#pragma unroll
+  for (int f = 0; f < 6; f++)
+    out[f] = zero ? T(0) : c.g0[f] * (c.noise_scale * un1[chan[f]]) + c.g1[f] * (c.noise_scale * u0[chan[f]]);
+  tl[0] = out[0];
+  tl[1] = out[1];
+  tl[2] = out[2];
+  ta[0] = out[3];
+  ta[1] = out[4];
+  ta[2] = out[5];
+}
+
+// ---------------------------------------------------------------------------
+// One PyFly.step for one aircraft (pyfly.py:1358-1420).
+//   y[19]     ODE state (in/out)            der[8] roll pitch yaw Va alpha beta elev ail (in/out;
+//             only der[6..7] are read: the t == 0 elevator/aileron values)
+//   cmd[3]    raw commands in, constrained out
+//   dmask     bit r set <=> der[r] was (re)computed.  On failure the stored state
+//             holds the committed part of the save (history[-1] semantics); the
+//             caller keeps its previous der[r] for the clear bits.
+// Returns termination code (0 = success).
+// ---------------------------------------------------------------------------
+template <typename T>
+FW_HD int sim_step_masked(const DevCfg<T>& c, T* y, T* der, T* cmd, const T* wind, const T* tl, const T* ta, int& nfev,
+                          int& nacc, uint32_t& dmask, T* sy, T* sf, int stride) {
+  dmask = 0;
+  StepCtx<T> X;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    X.wind[i] = wind[i];
+    X.tl[i] = tl[i];
+    X.ta[i] = ta[i];
+  }
+  X.elev0 = der[6];
+  X.ail0 = der[7];
+  nfev = 0;
+  nacc = 0;
+  int term = constrain_commands(c, cmd, X.sp);
+  if (term) return term;
+  T y1[NY];
+#pragma unroll
+  for (int i = 0; i < NY; i++) y1[i] = y[i];
+  term = rk45(c, X, y1, sy, sf, stride, nfev, nacc);
+  if (term < 0) return 0;  // solver failure: reference keeps sol.y[:, -1]; never observed
+  if (term) return term;
+
+  // ---- _set_states_from_ode_solution(save=True) (pyfly.py:1852-1881) ----
+  const T n = sqrt(y1[0] * y1[0] + y1[1] * y1[1] + y1[2] * y1[2] + y1[3] * y1[3]);
+  const T e0 = y1[0] / n, e1 = y1[1] / n, e2 = y1[2] / n, e3 = y1[3] / n;
+  y[0] = e0;
+  y[1] = e1;
+  y[2] = e2;
+  y[3] = e3;
+  T eul[3];
+  eul[0] = atan2(T(2) * (e0 * e1 + e2 * e3), e0 * e0 + e3 * e3 - e1 * e1 - e2 * e2);
+  eul[1] = asin(T(2) * (e0 * e2 - e1 * e3));
+  eul[2] = atan2(T(2) * (e0 * e3 + e1 * e2), e0 * e0 + e1 * e1 - e2 * e2 - e3 * e3);
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    eul[i] = cond(c, FW_V_ROLL + i, eul[i], term);
+    if (term) return term;
+    der[i] = eul[i];
+    dmask |= 1u << i;
+  }
+  // ODE states: the last RHS evaluation saw the very same y1, so these conditions
+  // cannot fail here; they still clip/commit in order.
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const T v = cond(c, FW_V_OMEGA_P + i, y1[4 + i], term);
+    if (term) return term;
+    y[4 + i] = v;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    const T v = cond(c, FW_V_ACT0 + j, y1[13 + j], term);
+    if (term) return term;
+    y[13 + j] = v;
+    y[16 + j] = (c.dotmask & (1u << j)) ? clipv(y1[16 + j], -c.dot_max[j], c.dot_max[j]) : y1[16 + j];
+  }
+  if (c.elevon) {
+    const T ail = cond(c, FW_V_AILERON, (-y[13] + y[14]) / T(2), term);
+    if (term) return term;
+    der[7] = ail;
+    dmask |= 1u << 7;
+    const T elev = cond(c, FW_V_ELEVATOR, (y[13] + y[14]) / T(2), term);
+    if (term) return term;
+    der[6] = elev;
+    dmask |= 1u << 6;
+  } else {
+    der[6] = y[13];
+    der[7] = y[14];
+    dmask |= 3u << 6;
+  }
+  // ---- post-step airspeed factors, Euler branch (pyfly.py:1398-1406) ----
+  T va[3];
+  if (c.euler_exact) airspeed_vec_euler(der[0], der[1], der[2], wind, tl, y + 10, va);
+  else airspeed_vec(y, wind, tl, y + 10, va);
+  const T Va_raw = sqrt(va[0] * va[0] + va[1] * va[1] + va[2] * va[2]);
+  const T al = atan2(va[2], va[0]);
+  const T be = asin(va[1] / Va_raw);
+  const T Va = cond(c, FW_V_VA, Va_raw, term);
+  if (term) return term;
+  der[3] = Va;
+  dmask |= 1u << 3;
+  const T alc = cond(c, FW_V_ALPHA, al, term);
+  if (term) return term;
+  der[4] = alc;
+  dmask |= 1u << 4;
+  const T bec = cond(c, FW_V_BETA, be, term);
+  if (term) return term;
+  der[5] = bec;
+  dmask |= 1u << 5;
+  return 0;
+}
+
+// AttitudeQuaternion._from_euler_angles (pyfly.py:714-737)
+template <typename T>
+FW_HD void euler_to_quat(T phi, T th, T psi, T* q) {
+  const T cps = cos(psi / T(2)), sps = sin(psi / T(2)), cth = cos(th / T(2)), sth = sin(th / T(2)),
+          cph = cos(phi / T(2)), sph = sin(phi / T(2));
+  q[0] = cps * cth * cph + sps * sth * sph;
+  q[1] = cps * cth * sph - sps * sth * cph;
+  q[2] = cps * sth * cph + sps * cth * sph;
+  q[3] = sps * cth * cph - cps * sth * sph;
+}
+
+// Post-reset derived states (pyfly.py:1296-1311): Va/alpha/beta from Euler
+// angles (turbulence is 0 at k = 0), elevator/aileron .value.
+template <typename T>
+FW_HD void reset_derived(const DevCfg<T>& c, const T* y, const T* wind, T* der) {
+  const T zero[3] = {T(0), T(0), T(0)};
+  T va[3];
+  airspeed_vec_euler(der[0], der[1], der[2], wind, zero, y + 10, va);
+  const T Va_raw = sqrt(va[0] * va[0] + va[1] * va[1] + va[2] * va[2]);
+  int term = 0;
+  der[4] = cond<T>(c, FW_V_ALPHA, (T)atan2(va[2], va[0]), term);
+  der[5] = cond<T>(c, FW_V_BETA, (T)asin(va[1] / Va_raw), term);
+  der[3] = cond(c, FW_V_VA, Va_raw, term);
+  if (c.elevon) {
+    der[6] = cond(c, FW_V_ELEVATOR, (y[13] + y[14]) / T(2), term);
+    der[7] = cond(c, FW_V_AILERON, (-y[13] + y[14]) / T(2), term);
+  } else {
+    der[6] = y[13];
+    der[7] = y[14];
+  }
+  if (c.disabled_inputs & 1) der[6] = T(0);  // disabled ControlVariable.reset (pyfly.py:359-363)
+  if (c.disabled_inputs & 2) der[7] = T(0);
+}
+
+// ===========================================================================
+// gym env epilogue (fixed_wing.py)
+// ===========================================================================
+template <typename T>
+FW_HD T pymod(T a, T b) {
+  T r = fmod(a, b);
+  if (r != T(0) && ((r < T(0)) != (b < T(0)))) r += b;
+  return r;
+}
+
+// _get_error (fixed_wing.py:1318-1344); val = current .value of the target state
+template <typename T>
+FW_HD T target_error(const DevCfg<T>& c, int k, T tgt, T val) {
+  if (c.target_wrap[k]) {
+    const T pi = T(PI_D);
+    T dist = pymod(val - tgt + pi, T(2) * pi) - pi;
+    if (dist < -pi) dist += T(2) * pi;
+    return dist;
+  }
+  return tgt - val;
+}
+
+// _get_goal_status()["all"] (fixed_wing.py:1346-1361)
+template <typename T>
+FW_HD bool goal_all(const DevCfg<T>& c, const T* tgt, const T* vals) {
+  bool all = true;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    if (!c.has_bound[k]) continue;
+    const T err = target_error(c, k, tgt[k], vals[k]);
+    if (!(fabs(err) <= c.target_bound[k])) all = false;
+  }
+  return all;
+}
+
+// _get_next_target (fixed_wing.py:1363-1471): constant / compensate(Va)
+template <typename T>
+FW_HD void next_target(const DevCfg<T>& c, int steps_tgt, T* tgt) {
+  T res[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    T r = tgt[k];
+    if (c.target_class[k] == FW_TGT_COMPENSATE) {
+      const T pitch_tar = tgt[1];
+      const T deg = T(PI_D / 180.0);
+      if (pitch_tar <= T(-2.5) * deg) {
+        const T va_target = tgt[2];
+        const T va_end = T(28.434) - T(40.0841) * pitch_tar;
+        T slope = T(0);
+        if (va_target <= va_end) {
+          const T a = va_target < va_end * T(0.95) ? T(1) : T(1) - va_target / (va_end * T(1.5));
+          slope = T(7) * (a > T(0) ? a : T(0));
+        }
+        r = va_target + (slope * (-tgt[1]) - T(0.25)) * c.dt;
+      } else if (pitch_tar >= T(5) * deg) {
+        const T va_end = T(26.27) - T(41.2529) * pitch_tar;
+        const T va_target = tgt[2];
+        if (va_target > va_end) r = steps_tgt < 750 ? va_target + (va_end - va_target) * T(1) / T(150) : va_end;
+        else r = va_target;
+      }
+    }
+    if (c.target_wrap[k] && fabs(r) > T(PI_D)) r = sgn(r) * (fmod(fabs(r), T(PI_D)) - T(PI_D));
+    res[k] = r;
+  }
+  tgt[0] = res[0];
+  tgt[1] = res[1];
+  tgt[2] = res[2];
+}
+
+// linear_action_scaling (fixed_wing.py:630-652)
+template <typename T>
+FW_HD T scale_fwd(const DevCfg<T>& c, int i, T a) {
+  return (c.act_high[i] - c.act_low[i]) * (a - c.scale_low) / (c.scale_high - c.scale_low) + c.act_low[i];
+}
+template <typename T>
+FW_HD T scale_bwd(const DevCfg<T>& c, int i, T a) {
+  return (c.scale_high - c.scale_low) * (a - c.act_low[i]) / (c.act_high[i] - c.act_low[i]) + c.scale_low;
+}
+
+}  // namespace fw

@@ -1,0 +1,1093 @@
+// fw_kernels.hip -- gfx950 kernels and the C ABI of libfwsim.so (include/fwsim.h).
+//
+// Data layout in HBM (one handle = one GPU): every per-aircraft quantity is a
+// row of a structure-of-arrays block, [rows][ld] with ld = N rounded up to a
+// multiple of 64, so lane i of a wave touches element i of each row: every
+// global access below is a coalesced dword (or dwordx2 for fp64) per lane.
+//
+// Kernels (one lane = one aircraft, 256-thread blocks, no LDS, no MFMA -- the
+// work is elementwise ODE integration):
+//   k_env_step   FixedWingAircraft.step + PyFly.step + masked auto-reset (hot path)
+//   k_sim_step   PyFly.step only
+//   k_reset      masked reset (sampled with Philox or injected values)
+//   k_observe    get_observation of the current state
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "fw_device.hpp"
+
+using namespace fw;
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define FW_HIP(expr)                                                                              \
+  do {                                                                                            \
+    hipError_t e_ = (expr);                                                                       \
+    if (e_ != hipSuccess) return set_err(FW_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int BLOCK = 256;
+constexpr int RING = FW_MAX_WINDOW - 1;  // max previous actions kept
+
+// ---------------------------------------------------------------------------
+// SoA state block pointers
+// ---------------------------------------------------------------------------
+template <typename T>
+struct State {
+  int64_t n, ld;
+  T* y;            // [19][ld]
+  T* der;          // [8][ld]
+  T* wind;         // [3][ld]
+  T* target;       // [3][ld]
+  T* cmd;          // [3][ld] last constrained commands
+  T* ep_ret;       // [ld]
+  T* act_ring;     // [act_window][3][ld]
+  T* cmd_ring;     // [cmd_window][3][ld] or null
+  uint32_t* steps;    // [ld]: steps_count | steps_for_current_target << 16
+  uint32_t* goal;     // [4][ld] 128-bit goal history shift register (bit 0 newest)
+  uint32_t* episode;  // [ld]
+  const T* noise;     // injected N(0,1) turbulence noise [4][noise_len][ld] or null
+  int64_t noise_len;
+  uint32_t key0, key1;  // Philox key = seed
+  uint32_t env_offset;
+};
+
+template <typename T>
+__device__ __forceinline__ T ld_(const T* p, int64_t row, int64_t ld, int64_t i) {
+  return p[row * ld + i];
+}
+template <typename T>
+__device__ __forceinline__ void st_(T* p, int64_t row, int64_t ld, int64_t i, T v) {
+  p[row * ld + i] = v;
+}
+
+// N(0,1) turbulence noise sample (4 channels) of step index k of the current episode
+template <typename T>
+__device__ __forceinline__ void noise4(const State<T>& s, int64_t i, uint32_t episode, int k, T u[4]) {
+  if (s.noise) {
+    if (k < s.noise_len) {
+#pragma unroll
+      for (int ch = 0; ch < 4; ch++) u[ch] = s.noise[((int64_t)ch * s.noise_len + k) * s.ld + i];
+    } else {
+      u[0] = u[1] = u[2] = u[3] = T(0);
+    }
+    return;
+  }
+  uint32_t r[4];
+  philox(s.key0, s.key1, s.env_offset + (uint32_t)i, episode, 1u, (uint32_t)k, r);
+  normal4<T>(r, u);
+}
+
+template <typename T>
+__device__ __forceinline__ void turbulence_at(const DevCfg<T>& c, const State<T>& s, int64_t i, uint32_t episode, int k,
+                                              T tl[3], T ta[3]) {
+  tl[0] = tl[1] = tl[2] = ta[0] = ta[1] = ta[2] = T(0);
+  if (!c.turbulence) return;
+  if (k % c.turb_len == 0) return;
+  T un1[4], u0[4];
+  noise4(s, i, episode, k - 1, un1);
+  noise4(s, i, episode, k, u0);
+  dryden(c, k, un1, u0, tl, ta);
+}
+
+// value of an observed / rewarded state variable from the stored state
+template <typename T>
+__device__ __forceinline__ T state_value(int var, const T* y, const T* der) {
+  switch (var) {
+    case FW_V_ROLL: return der[0];
+    case FW_V_PITCH: return der[1];
+    case FW_V_YAW: return der[2];
+    case FW_V_VA: return der[3];
+    case FW_V_ALPHA: return der[4];
+    case FW_V_BETA: return der[5];
+    case FW_V_ELEVATOR: return der[6];
+    case FW_V_AILERON: return der[7];
+    case FW_V_THROTTLE: return y[15];
+    case FW_V_ACT0: return y[13];
+    case FW_V_ACT1: return y[14];
+    case FW_V_ACT2: return y[15];
+    default: return y[4 + (var - FW_V_OMEGA_P)];
+  }
+}
+
+// get_observation (fixed_wing.py:1113-1262): length-1 vector observation.
+// seqA / seqC: newest-first sequences of raw actions / constrained commands
+// (index 0 = latest), nseq = number of valid entries (= steps_count).
+template <typename T>
+__device__ __forceinline__ void observe(const DevCfg<T>& c, const T* y, const T* der, const T* tgt, int steps,
+                                        const T (*seqA)[3], const T (*seqC)[3], T* out, int64_t stride) {
+  for (int o = 0; o < c.n_obs; o++) {
+    const fw_obs_entry E = c.obs[o];
+    T val;
+    if (E.kind == FW_OBS_STATE) {
+      val = state_value(E.var, y, der);
+    } else if (E.kind == FW_OBS_TARGET_ABS) {
+      val = tgt[E.var];
+    } else if (E.kind == FW_OBS_TARGET_REL) {
+      const int tv[3] = {FW_V_ROLL, FW_V_PITCH, FW_V_VA};
+      val = target_error(c, E.var, tgt[E.var], state_value(tv[E.var], y, der));
+    } else {  // action window
+      const int ai = E.var;
+      if (steps - 1 < 0) {
+        const int av[3] = {FW_V_ELEVATOR, FW_V_AILERON, FW_V_THROTTLE};
+        val = state_value(av[ai], y, der);
+        if (c.scale_actions) val = scale_bwd(c, ai, val);
+      } else {
+        // all indices static (runtime-indexed private arrays would go to scratch)
+        const bool sa = c.scale_actions;
+        const int w = E.window < steps ? E.window : steps;  // entries in the window
+        float acc = 0.0f;                                    // np.sum(..., dtype=np.float32)
+#pragma unroll
+        for (int j = RING - 1; j >= 0; j--) {                // oldest diff first
+          if (j + 1 < w) {
+            const T d0 = sa ? seqA[j][0] - seqA[j + 1][0] : seqC[j][0] - seqC[j + 1][0];
+            const T d1 = sa ? seqA[j][1] - seqA[j + 1][1] : seqC[j][1] - seqC[j + 1][1];
+            const T d2 = sa ? seqA[j][2] - seqA[j + 1][2] : seqC[j][2] - seqC[j + 1][2];
+            acc += (float)fabs(ai == 0 ? d0 : (ai == 1 ? d1 : d2));
+          }
+        }
+        val = (T)acc;
+      }
+    }
+    if (E.norm) val = (val - (T)E.mean) / (T)E.var_;
+    out[(int64_t)o * stride] = val;
+  }
+}
+
+// get_reward (fixed_wing.py:941-1111), form "absolute"
+template <typename T>
+__device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* der, const T* tgt, int steps,
+                                       const T (*seqA)[3]) {
+  T tv[3] = {T(0), T(0), T(0)}, ts[3] = {T(0), T(0), T(0)};
+  for (int f = 0; f < c.n_rew; f++) {
+    const fw_rew_factor F = c.rew[f];
+    T val = T(0);
+    if (F.kind == FW_REW_ACTION_VALUE) {
+      val = fabs(seqA[0][0]) + fabs(seqA[0][1]) + fabs(seqA[0][2]);
+    } else if (F.kind == FW_REW_ACTION_DELTA) {
+      if (steps > 1) {
+        const int w = F.window < steps ? F.window : steps;
+#pragma unroll
+        for (int j = RING - 1; j >= 0; j--) {
+          if (j + 1 < w) {
+#pragma unroll
+            for (int a = 0; a < 3; a++) val += fabs(seqA[j][a] - seqA[j + 1][a]);
+          }
+        }
+      }
+    } else if (F.kind == FW_REW_ACTION_BOUND) {
+#pragma unroll
+      for (int a = 0; a < 3; a++) {
+        const T x = seqA[0][a];
+        const T hi = x > c.bmax ? x - c.bmax : T(0);
+        const T lo = x < c.bmin ? x - c.bmin : T(0);
+        val += fabs(hi) + fabs(lo);
+      }
+    } else if (F.kind == FW_REW_STATE_VALUE) {
+      val = state_value(F.var, y, der);
+    } else {
+      const int tvv[3] = {FW_V_ROLL, FW_V_PITCH, FW_V_VA};
+      val = target_error(c, F.var, tgt[F.var], state_value(tvv[F.var], y, der));
+    }
+    if (F.fun == FW_FUN_LINEAR) {
+      val = fabs(val) / (T)F.scaling;
+      val = val < T(0) ? T(0) : val;
+      val = val > (T)F.max ? (T)F.max : val;
+    } else {
+      val = val * val / (T)F.scaling;
+    }
+    const T sg = sgn((T)F.sign);
+    if (F.shaping) ts[F.fun] += val * sg;
+    else tv[F.fun] += val * sg;
+  }
+  T r = T(0);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    if (!c.term_present[k]) continue;
+    const T v = (k == FW_FUN_EXPONENTIAL) ? T(-1) + exp(tv[k] + ts[k]) : tv[k] + ts[k];
+    r += c.term_weight[k] * v;
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// reset of one lane: PyFly.reset (pyfly.py:1262-1311) + FixedWingAircraft.reset
+// (fixed_wing.py:414-481) incl. sample_target (:654-746).  init: FW_NINIT values
+// (NaN = sample) or null; tin: 3 targets (NaN = sample) or null.
+// ---------------------------------------------------------------------------
+template <typename T>
+struct Draws {
+  uint32_t k0, k1, cid, ep, blk;
+  uint32_t r[4];
+  int used;
+  __device__ __forceinline__ T next() {
+    if (used == 4) {
+      philox(k0, k1, cid, ep, 0u, blk++, r);
+      used = 0;
+    }
+    return u01<T>(r[used++]);
+  }
+  __device__ __forceinline__ T uniform(T lo, T hi) { return lo + (hi - lo) * next(); }  // numpy uniform
+};
+
+template <typename T>
+__device__ __forceinline__ void reset_lane(const DevCfg<T>& c, const State<T>& s, int64_t i, const T* init, const T* tin,
+                                           T* y, T* der, T* wind, T* tgt) {
+  const int64_t ld = s.n;  // injected init / target arrays are dense [rows][N]
+  const uint32_t episode = s.episode[i] + 1u;
+  s.episode[i] = episode;
+  Draws<T> D{s.key0, s.key1, s.env_offset + (uint32_t)i, episode, 0u, {0, 0, 0, 0}, 4};
+  int term = 0;
+  T st[12];
+#pragma unroll
+  for (int k = 0; k < 12; k++) {  // roll pitch yaw p q r n e d u v w
+    const T given = init ? init[k * ld + i] : T(NAN);
+    const int var = k;  // fw_var order matches for these 12
+    const T smp = D.uniform(c.init_min[var], c.init_max[var]);
+    st[k] = isnan(given) ? smp : cond(c, var, given, term);  // Variable.reset (pyfly.py:83-104)
+  }
+#pragma unroll
+  for (int j = 0; j < 3; j++) {  // ControlVariable.reset (pyfly.py:340-366)
+    const T gv = init ? init[(FW_I_ACT0 + 2 * j) * ld + i] : T(NAN);
+    const T gd = init ? init[(FW_I_ACT0 + 2 * j + 1) * ld + i] : T(NAN);
+    const T smp = D.uniform(c.init_min[FW_V_ACT0 + j], c.init_max[FW_V_ACT0 + j]);
+    if (isnan(gv)) {
+      y[13 + j] = smp;
+      y[16 + j] = T(0);
+    } else {
+      y[13 + j] = cond(c, FW_V_ACT0 + j, gv, term);
+      const T d = isnan(gd) ? T(0) : gd;
+      y[16 + j] = (c.dotmask & (1u << j)) ? clipv(d, -c.dot_max[j], c.dot_max[j]) : d;
+    }
+  }
+  // Wind.reset (pyfly.py:799-830)
+  {
+    T wn, we, wdn;
+    if (c.wind_random) {
+      const T m = D.uniform(c.wind_mag_min, c.wind_mag_max);
+      wn = D.uniform(-m, m);
+      const T we_max = sqrt(m * m - wn * wn);
+      we = D.uniform(-we_max, we_max);
+      wdn = sqrt(fmax(m * m - wn * wn - we * we, T(0)));
+    } else {
+      wn = D.uniform(c.wind_init_min[0], c.wind_init_max[0]);
+      we = D.uniform(c.wind_init_min[1], c.wind_init_max[1]);
+      wdn = D.uniform(c.wind_init_min[2], c.wind_init_max[2]);
+    }
+    const T gn = init ? init[FW_I_WIND_N * ld + i] : T(NAN);
+    const T ge = init ? init[FW_I_WIND_E * ld + i] : T(NAN);
+    const T gd = init ? init[FW_I_WIND_D * ld + i] : T(NAN);
+    const bool given = !isnan(gn) && !isnan(ge) && !isnan(gd);
+    wind[0] = given ? gn : wn;
+    wind[1] = given ? ge : we;
+    wind[2] = given ? gd : wdn;
+  }
+#pragma unroll
+  for (int k = 0; k < 9; k++) y[4 + k] = st[3 + k];
+  euler_to_quat(st[0], st[1], st[2], y);
+  der[0] = st[0];
+  der[1] = st[1];
+  der[2] = st[2];
+  reset_derived(c, y, wind, der);
+  if (c.has_env) {
+    // sample_target (fixed_wing.py:654-746)
+    const T vals[3] = {der[0], der[1], der[3]};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      T lo = c.target_low[k], hi = c.target_high[k];
+      if (c.has_delta[k]) {
+        lo = fmax(lo, vals[k] - c.target_delta[k]);
+        hi = fmax(fmin(hi, vals[k] + c.target_delta[k]), lo);
+      }
+      const T smp = D.uniform(lo, hi);
+      const T given = tin ? tin[k * ld + i] : T(NAN);
+      tgt[k] = isnan(given) ? smp : given;
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void load_row(const T* p, int rows, int64_t ld, int64_t i, T* dst) {
+  for (int r = 0; r < rows; r++) dst[r] = p[r * ld + i];
+}
+
+template <typename T>
+__device__ __forceinline__ void store_env_fresh(const DevCfg<T>& c, const State<T>& s, int64_t i, const T* y, const T* der,
+                                                const T* wind, const T* tgt) {
+  const int64_t ld = s.ld;
+#pragma unroll
+  for (int k = 0; k < NY; k++) st_(s.y, k, ld, i, y[k]);
+#pragma unroll
+  for (int k = 0; k < 8; k++) st_(s.der, k, ld, i, der[k]);
+#pragma unroll
+  for (int k = 0; k < 3; k++) st_(s.wind, k, ld, i, wind[k]);
+  if (c.has_env) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) st_(s.target, k, ld, i, tgt[k]);
+    const T vals[3] = {der[0], der[1], der[3]};
+    const uint32_t g0 = goal_all(c, tgt, vals) ? 1u : 0u;
+    st_(s.goal, 0, ld, i, g0);
+    st_(s.goal, 1, ld, i, 0u);
+    st_(s.goal, 2, ld, i, 0u);
+    st_(s.goal, 3, ld, i, 0u);
+    st_(s.ep_ret, 0, ld, i, T(0));
+  }
+  s.steps[i] = 0u;
+}
+
+// ===========================================================================
+// kernels
+// ===========================================================================
+template <typename T>
+__global__ __launch_bounds__(BLOCK) void k_reset(const DevCfg<T>* __restrict__ cfgp, State<T> s,
+                                                 const uint8_t* __restrict__ mask, const T* __restrict__ init,
+                                                 const T* __restrict__ tin, T* __restrict__ obs) {
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= s.n) return;
+  if (mask && !mask[i]) return;
+  const DevCfg<T>& c = *cfgp;
+  T y[NY], der[8], wind[3], tgt[3] = {T(0), T(0), T(0)};
+  reset_lane(c, s, i, init, tin, y, der, wind, tgt);
+  store_env_fresh(c, s, i, y, der, wind, tgt);
+  if (obs && c.has_env) {
+    T seq[RING + 1][3];
+    observe(c, y, der, tgt, 0, seq, seq, obs + i * c.n_obs, 1);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(BLOCK) void k_observe(const DevCfg<T>* __restrict__ cfgp, State<T> s, T* __restrict__ obs) {
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= s.n) return;
+  const DevCfg<T>& c = *cfgp;
+  const int64_t ld = s.ld;
+  T y[NY], der[8], tgt[3];
+  load_row(s.y, NY, ld, i, y);
+  load_row(s.der, 8, ld, i, der);
+  load_row(s.target, 3, ld, i, tgt);
+  const int steps = (int)(s.steps[i] & 0xFFFFu);
+  T seqA[RING + 1][3], seqC[RING + 1][3];
+#pragma unroll
+  for (int j = 0; j <= RING; j++)
+#pragma unroll
+    for (int a = 0; a < 3; a++) seqA[j][a] = seqC[j][a] = T(0);
+  // newest-first from the rings
+#pragma unroll
+  for (int j = 0; j < RING; j++) {
+    if (j < c.act_window && steps - 1 - j >= 0) {
+      const int slot = (steps - 1 - j) % c.act_window;
+#pragma unroll
+      for (int a = 0; a < 3; a++) seqA[j][a] = s.act_ring[((int64_t)slot * 3 + a) * ld + i];
+    }
+    if (j < c.cmd_window && steps - 1 - j >= 0) {
+      const int slot = (steps - 1 - j) % c.cmd_window;
+#pragma unroll
+      for (int a = 0; a < 3; a++) seqC[j][a] = s.cmd_ring[((int64_t)slot * 3 + a) * ld + i];
+    }
+  }
+  observe(c, y, der, tgt, steps, seqA, seqC, obs + i * c.n_obs, 1);
+}
+
+template <typename T>
+__global__ __launch_bounds__(BLOCK) void k_sim_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
+                                                    const T* __restrict__ cmd_in, T* __restrict__ cmd_out,
+                                                    uint8_t* __restrict__ success, int32_t* __restrict__ term_out,
+                                                    int32_t* __restrict__ stats) {
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= s.n) return;
+  const DevCfg<T>& c = *cfgp;
+  const int64_t ld = s.ld;
+  T y[NY], der[8], wind[3], cmd[3];
+  load_row(s.y, NY, ld, i, y);
+  der[6] = ld_(s.der, 6, ld, i);
+  der[7] = ld_(s.der, 7, ld, i);
+  load_row(s.wind, 3, ld, i, wind);
+#pragma unroll
+  for (int a = 0; a < 3; a++) cmd[a] = cmd_in[i * 3 + a];
+  const uint32_t sw = s.steps[i];
+  const int k = (int)(sw & 0xFFFFu);
+  T tl[3], ta[3];
+  turbulence_at(c, s, i, s.episode[i], k, tl, ta);
+  int nfev = 0, nacc = 0;
+  uint32_t dmask = 0;
+  __shared__ T lds[2 * NY * BLOCK];  // accepted RK state y and f of the block's aircraft
+  const int term = sim_step_masked(c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
+                                   lds + NY * BLOCK + threadIdx.x, BLOCK);
+  if (term) {  // uncommitted derived values keep their previous (history[-1]) value
+#pragma unroll
+    for (int r = 0; r < 6; r++)
+      if (!(dmask & (1u << r))) der[r] = ld_(s.der, r, ld, i);
+  }
+#pragma unroll
+  for (int r = 0; r < NY; r++) st_(s.y, r, ld, i, y[r]);
+#pragma unroll
+  for (int r = 0; r < 8; r++) st_(s.der, r, ld, i, der[r]);
+#pragma unroll
+  for (int a = 0; a < 3; a++) st_(s.cmd, a, ld, i, cmd[a]);
+  s.steps[i] = (sw & 0xFFFF0000u) | (uint32_t)((k + 1) & 0xFFFF);  // cur_sim_step += 1 (pyfly.py:1418)
+  if (cmd_out)
+#pragma unroll
+    for (int a = 0; a < 3; a++) cmd_out[i * 3 + a] = cmd[a];
+  if (success) success[i] = term == 0;
+  if (term_out) term_out[i] = term;
+  if (stats) stats[i] = nfev | (nacc << 16);
+}
+
+template <typename T>
+__global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
+                                                    const T* __restrict__ actions, T* __restrict__ obs_out,
+                                                    T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
+                                                    int32_t* __restrict__ term_out, T* __restrict__ tobs_out,
+                                                    T* __restrict__ episode_out, int32_t* __restrict__ stats,
+                                                    int auto_reset) {
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= s.n) return;
+  const DevCfg<T>& c = *cfgp;
+  const int64_t ld = s.ld;
+
+  T y[NY], der[8], wind[3], tgt[3], a[3];
+  load_row(s.y, NY, ld, i, y);
+  der[6] = ld_(s.der, 6, ld, i);
+  der[7] = ld_(s.der, 7, ld, i);
+  load_row(s.wind, 3, ld, i, wind);
+  load_row(s.target, 3, ld, i, tgt);
+#pragma unroll
+  for (int q = 0; q < 3; q++) a[q] = actions[i * 3 + q];
+  const uint32_t sw = s.steps[i];
+  const int steps0 = (int)(sw & 0xFFFFu);
+  const int steps_tgt0 = (int)(sw >> 16);
+  const uint32_t episode = s.episode[i];
+
+  // ---- FixedWingAircraft.step prologue (fixed_wing.py:491-506) ----
+  T cmd[3];
+#pragma unroll
+  for (int q = 0; q < 3; q++) cmd[q] = c.scale_actions ? scale_fwd(c, q, clipv(a[q], c.scale_low, c.scale_high)) : a[q];
+
+  // ---- PyFly.step ----
+  T tl[3], ta[3];
+  turbulence_at(c, s, i, episode, steps0, tl, ta);
+  int nfev = 0, nacc = 0;
+  uint32_t dmask = 0;
+  __shared__ T lds[2 * NY * BLOCK];  // accepted RK state y and f of the block's aircraft
+  const int sterm = sim_step_masked(c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
+                                    lds + NY * BLOCK + threadIdx.x, BLOCK);
+  // keep the epilogue's loads (action ring, goal bits, ...) below the integrator:
+  // hoisted above it they would sit in VGPRs for the whole RK loop
+  asm volatile("" ::: "memory");
+  if (sterm) {
+#pragma unroll
+    for (int r = 0; r < 6; r++)
+      if (!(dmask & (1u << r))) der[r] = ld_(s.der, r, ld, i);
+  }
+  const int steps = steps0 + 1;
+  const int steps_tgt = steps_tgt0 + 1;
+
+  // ---- action / command histories (newest first) ----
+  T seqA[RING + 1][3], seqC[RING + 1][3];
+#pragma unroll
+  for (int q = 0; q < 3; q++) {
+    seqA[0][q] = a[q];
+    seqC[0][q] = cmd[q];
+  }
+#pragma unroll
+  for (int j = 1; j <= RING; j++) {
+#pragma unroll
+    for (int q = 0; q < 3; q++) seqA[j][q] = seqC[j][q] = T(0);
+    // previous action j = action number steps-j (1-based) -> slot (steps-j-1) % window
+    if (j <= c.act_window && steps - j >= 1) {
+      const int slot = (steps - j - 1) % c.act_window;
+#pragma unroll
+      for (int q = 0; q < 3; q++) seqA[j][q] = s.act_ring[((int64_t)slot * 3 + q) * ld + i];
+    }
+    if (j <= c.cmd_window && steps - j >= 1) {
+      const int slot = (steps - j - 1) % c.cmd_window;
+#pragma unroll
+      for (int q = 0; q < 3; q++) seqC[j][q] = s.cmd_ring[((int64_t)slot * 3 + q) * ld + i];
+    }
+  }
+  {
+    const int slot = (steps - 1) % c.act_window;
+#pragma unroll
+    for (int q = 0; q < 3; q++) s.act_ring[((int64_t)slot * 3 + q) * ld + i] = a[q];
+    if (c.cmd_window) {
+      const int cs = (steps - 1) % c.cmd_window;
+#pragma unroll
+      for (int q = 0; q < 3; q++) s.cmd_ring[((int64_t)cs * 3 + q) * ld + i] = cmd[q];
+    }
+  }
+
+  // ---- epilogue (fixed_wing.py:511-628) ----
+  bool done = false;
+  int term = FW_TERM_NONE;
+  if (steps >= c.steps_max && c.steps_max > 0) {
+    done = true;
+    term = FW_TERM_STEPS;
+  }
+  T reward;
+  uint32_t g[4];
+  load_row(s.goal, 4, ld, i, g);
+  if (sterm == 0) {
+    if (c.streak_req > 0) {
+      const T vals[3] = {der[0], der[1], der[3]};
+      const uint32_t bit = goal_all(c, tgt, vals) ? 1u : 0u;
+      g[3] = (g[3] << 1) | (g[2] >> 31);
+      g[2] = (g[2] << 1) | (g[1] >> 31);
+      g[1] = (g[1] << 1) | (g[0] >> 31);
+      g[0] = (g[0] << 1) | bit;
+      if (steps_tgt >= c.streak_req) {
+        int cnt = 0, rem = c.streak_req;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+          const int take = rem >= 32 ? 32 : (rem > 0 ? rem : 0);
+          const uint32_t m = take == 32 ? 0xFFFFFFFFu : ((1u << take) - 1u);
+          cnt += __builtin_popcount(g[w] & m);
+          rem -= take;
+        }
+        if ((double)cnt / (double)c.streak_req >= (double)c.streak_frac && c.on_success == 1) {
+          done = true;
+          term = FW_TERM_SUCCESS;
+        }
+      }
+    }
+    reward = reward_of(c, y, der, tgt, steps, seqA);
+    next_target(c, steps_tgt, tgt);
+  } else {
+    done = true;
+    reward = c.step_fail_timesteps ? (T)(steps - c.steps_max) : c.step_fail_value;
+    term = sterm;
+  }
+  const T ep_ret = ld_(s.ep_ret, 0, ld, i) + reward;
+
+  // ---- observation (also the terminal observation) ----
+  T* orow = obs_out + i * c.n_obs;
+  if (done && tobs_out) observe(c, y, der, tgt, steps, seqA, seqC, tobs_out + i * c.n_obs, 1);
+
+  rew_out[i] = reward;
+  done_out[i] = done ? 1 : 0;
+  if (term_out) term_out[i] = term;
+  if (stats) stats[i] = nfev | (nacc << 16);
+
+  // wavefront-uniform skip of the reset path when no lane of the wave is done
+  const bool do_reset = done && auto_reset;
+  if (__ballot(do_reset)) {
+    if (do_reset) {
+      if (episode_out) {
+        episode_out[i * 2 + 0] = ep_ret;
+        episode_out[i * 2 + 1] = (T)steps;
+      }
+      T yr[NY], dr[8], wr[3], tr[3];
+      reset_lane(c, s, i, (const T*)nullptr, (const T*)nullptr, yr, dr, wr, tr);
+      store_env_fresh(c, s, i, yr, dr, wr, tr);
+      T seq0[RING + 1][3];
+      observe(c, yr, dr, tr, 0, seq0, seq0, orow, 1);
+      return;
+    }
+  }
+  if (done && episode_out) {
+    episode_out[i * 2 + 0] = ep_ret;
+    episode_out[i * 2 + 1] = (T)steps;
+  }
+  observe(c, y, der, tgt, steps, seqA, seqC, orow, 1);
+#pragma unroll
+  for (int r = 0; r < NY; r++) st_(s.y, r, ld, i, y[r]);
+#pragma unroll
+  for (int r = 0; r < 8; r++) st_(s.der, r, ld, i, der[r]);
+#pragma unroll
+  for (int k = 0; k < 3; k++) st_(s.target, k, ld, i, tgt[k]);
+#pragma unroll
+  for (int w = 0; w < 4; w++) st_(s.goal, w, ld, i, g[w]);
+  st_(s.ep_ret, 0, ld, i, ep_ret);
+  s.steps[i] = (uint32_t)(steps & 0xFFFF) | ((uint32_t)(steps_tgt & 0xFFFF) << 16);
+}
+
+}  // namespace
+
+// ===========================================================================
+// host side: handle, config conversion, launches, C ABI
+// ===========================================================================
+struct fw_handle {
+  int device = 0;
+  int precision = FW_F32;
+  int64_t n = 0, ld = 0;
+  fw_sim_config sim{};
+  fw_env_config env{};
+  bool has_env = false;
+  int act_window = 1, cmd_window = 0;
+  void* dcfg = nullptr;
+  void* base = nullptr;
+  size_t base_bytes = 0;
+  uint64_t seed = 0;
+  int64_t env_offset = 0;
+  const void* noise = nullptr;
+  int64_t noise_len = 0;
+  // offsets (bytes) of the SoA blocks inside base
+  size_t o_y, o_der, o_wind, o_target, o_cmd, o_epret, o_act, o_cmdring, o_steps, o_goal, o_episode;
+};
+
+namespace {
+
+template <typename T>
+void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
+  std::memset(&d, 0, sizeof(d));
+  const fw_sim_config& s = h->sim;
+  const double* P = s.param;
+  d.t_bound = s.dt;
+  d.dt = (T)s.dt;
+  d.rtol = (T)s.rtol;
+  d.atol = (T)s.atol;
+  d.half_rho = (T)(0.5 * s.rho);
+  d.rho = (T)s.rho;
+  d.S = (T)P[FW_P_S_WING];
+  d.b = (T)P[FW_P_B];
+  d.c = (T)P[FW_P_C];
+  d.mass = (T)P[FW_P_MASS];
+  d.inv_mass = (T)(1.0 / P[FW_P_MASS]);
+  d.mg = (T)(P[FW_P_MASS] * s.g);
+  d.inv_Jy = (T)(1.0 / P[FW_P_JY]);
+  {  // gammas pyfly.py:1098-1116
+    const double Jx = P[FW_P_JX], Jy = P[FW_P_JY], Jz = P[FW_P_JZ], I02 = -P[FW_P_JXZ];
+    double G[9];
+    G[0] = Jx * Jz - I02 * I02;
+    G[1] = (std::fabs(I02) * (Jx - Jy + Jz)) / G[0];
+    G[2] = (Jz * (Jz - Jy) + I02 * I02) / G[0];
+    G[3] = Jz / G[0];
+    G[4] = std::fabs(I02) / G[0];
+    G[5] = (Jz - Jx) / Jy;
+    G[6] = std::fabs(I02) / Jy;
+    G[7] = ((Jx - Jy) * Jx + I02 * I02) / G[0];
+    G[8] = Jx / G[0];
+    for (int k = 0; k < 9; k++) d.gam[k] = (T)G[k];
+  }
+  d.M = (T)P[FW_P_M];
+  d.a0 = (T)P[FW_P_A0];
+  d.pi_e_ar = (T)(3.141592653589793 * P[FW_P_E] * (P[FW_P_B] * P[FW_P_B] / P[FW_P_S_WING]));
+  d.CL0 = (T)P[FW_P_C_L_0]; d.CLa = (T)P[FW_P_C_L_ALPHA]; d.CLq = (T)P[FW_P_C_L_Q]; d.CLde = (T)P[FW_P_C_L_DELTA_E];
+  d.CDp = (T)P[FW_P_C_D_P]; d.CDq = (T)P[FW_P_C_D_Q]; d.CDb1 = (T)P[FW_P_C_D_BETA1]; d.CDb2 = (T)P[FW_P_C_D_BETA2];
+  d.CDde = (T)P[FW_P_C_D_DELTA_E];
+  d.Cm0 = (T)P[FW_P_C_M_0]; d.Cma = (T)P[FW_P_C_M_ALPHA]; d.Cmq = (T)P[FW_P_C_M_Q]; d.Cmde = (T)P[FW_P_C_M_DELTA_E];
+  d.Cmfp = (T)P[FW_P_C_M_FP];
+  d.CY0 = (T)P[FW_P_C_Y_0]; d.CYb = (T)P[FW_P_C_Y_BETA]; d.CYp = (T)P[FW_P_C_Y_P]; d.CYr = (T)P[FW_P_C_Y_R];
+  d.CYda = (T)P[FW_P_C_Y_DELTA_A]; d.CYdr = (T)P[FW_P_C_Y_DELTA_R];
+  d.Cl0 = (T)P[FW_P_C_L0_ROLL]; d.Clb = (T)P[FW_P_C_L_BETA]; d.Clp = (T)P[FW_P_C_L_P]; d.Clr = (T)P[FW_P_C_L_R];
+  d.Clda = (T)P[FW_P_C_L_DELTA_A]; d.Cldr = (T)P[FW_P_C_L_DELTA_R];
+  d.Cn0 = (T)P[FW_P_C_N_0]; d.Cnb = (T)P[FW_P_C_N_BETA]; d.Cnp = (T)P[FW_P_C_N_P]; d.Cnr = (T)P[FW_P_C_N_R];
+  d.Cnda = (T)P[FW_P_C_N_DELTA_A]; d.Cndr = (T)P[FW_P_C_N_DELTA_R];
+  d.kmotor = (T)P[FW_P_K_MOTOR];
+  d.prop_k = (T)(0.5 * s.rho * P[FW_P_S_PROP] * P[FW_P_C_PROP]);
+  d.kTP = (T)P[FW_P_K_T_P];
+  d.kOmega = (T)P[FW_P_K_OMEGA];
+  d.Sprop = (T)P[FW_P_S_PROP];
+  d.Cprop = (T)P[FW_P_C_PROP];
+  for (int j = 0; j < 3; j++) {
+    const fw_actuator& A = s.act[j];
+    if (A.order == 1) {
+      d.ac[j][0] = (T)(-1.0 / A.tau); d.ac[j][1] = 0; d.ac[j][2] = (T)(1.0 / A.tau);
+      d.ac[j][3] = 0; d.ac[j][4] = 0; d.ac[j][5] = 0;
+    } else {
+      d.ac[j][0] = 0; d.ac[j][1] = 1; d.ac[j][2] = 0;
+      d.ac[j][3] = (T)(-(A.omega_0 * A.omega_0)); d.ac[j][4] = (T)(-2 * A.zeta * A.omega_0);
+      d.ac[j][5] = (T)(A.omega_0 * A.omega_0);
+    }
+    d.dot_max[j] = (T)A.dot_max;
+    if (std::isfinite(A.dot_max)) d.dotmask |= 1u << j;
+  }
+  for (int v = 0; v < FW_NVAR; v++) {
+    const fw_limits& L = s.lim[v];
+    d.lim[v] = Lim<T>{(T)L.value_min, (T)L.value_max, (T)L.constraint_min, (T)L.constraint_max};
+    d.init_min[v] = (T)L.init_min;
+    d.init_max[v] = (T)L.init_max;
+    if (std::isfinite(L.constraint_min) || std::isfinite(L.constraint_max)) d.cmask |= 1u << v;
+    if (std::isfinite(L.value_min) || std::isfinite(L.value_max)) d.clipmask |= 1u << v;
+    if (L.wrap) d.wrapmask |= 1u << v;
+  }
+  auto limited = [&](int v) { return ((d.clipmask | d.wrapmask) >> v) & 1u; };
+  d.trig_alpha = limited(FW_V_ALPHA);
+  d.trig_beta = limited(FW_V_BETA);
+  // Euler-angle clipping (not the +-pi wrap, a no-op on atan2 output) changes the post-step rotation
+  d.euler_exact = ((d.clipmask >> FW_V_ROLL) | (d.clipmask >> FW_V_PITCH) | (d.clipmask >> FW_V_YAW)) & 1u;
+  d.elevon = s.elevon;
+  d.disabled_inputs = s.disabled_inputs;
+  d.turbulence = s.turbulence;
+  d.turb_len = s.turb_len > 0 ? s.turb_len : 1;
+  d.wind_random = s.wind_random;
+  d.wind_mag_min = (T)s.wind_mag_min;
+  d.wind_mag_max = (T)s.wind_mag_max;
+  for (int k = 0; k < 3; k++) {
+    d.wind_init_min[k] = (T)s.wind_init_min[k];
+    d.wind_init_max[k] = (T)s.wind_init_max[k];
+  }
+  for (int k = 0; k < 6; k++) {
+    d.g0[k] = (T)s.dryden_g0[k];
+    d.g1[k] = (T)s.dryden_g1[k];
+  }
+  d.noise_scale = (T)std::sqrt(3.141592653589793 / (double)d.turb_len);
+
+  d.has_env = h->has_env;
+  d.act_window = h->act_window;
+  d.cmd_window = h->cmd_window;
+  if (h->has_env) {
+    const fw_env_config& e = h->env;
+    d.steps_max = e.steps_max;
+    d.n_obs = e.n_obs;
+    d.scale_actions = e.scale_actions;
+    d.has_bounds = e.has_bounds;
+    d.streak_req = e.streak_req;
+    d.on_success = e.on_success;
+    d.n_rew = e.n_rew;
+    d.step_fail_timesteps = e.step_fail_timesteps;
+    d.scale_low = (T)e.scale_low;
+    d.scale_high = (T)e.scale_high;
+    d.bmax = (T)(e.scale_high * e.bounds_multiplier);
+    d.bmin = (T)(e.scale_low * e.bounds_multiplier);
+    for (int k = 0; k < 3; k++) {
+      d.act_low[k] = (T)e.act_low[k];
+      d.act_high[k] = (T)e.act_high[k];
+      d.target_class[k] = e.target_class[k];
+      d.target_wrap[k] = e.target_wrap[k];
+      d.target_low[k] = (T)e.target_low[k];
+      d.target_high[k] = (T)e.target_high[k];
+      d.has_delta[k] = !std::isnan(e.target_delta[k]);
+      d.target_delta[k] = d.has_delta[k] ? (T)e.target_delta[k] : T(0);
+      d.has_bound[k] = !std::isnan(e.target_bound[k]);
+      d.target_bound[k] = d.has_bound[k] ? (T)e.target_bound[k] : T(0);
+      d.term_weight[k] = (T)e.term_weight[k];
+      d.term_present[k] = e.term_present[k];
+    }
+    d.streak_frac = (T)e.streak_frac;
+    d.step_fail_value = (T)e.step_fail_value;
+    std::memcpy(d.obs, e.obs, sizeof(d.obs));
+    std::memcpy(d.rew, e.rew, sizeof(d.rew));
+  }
+}
+
+int validate(const fw_sim_config* s, const fw_env_config* e) {
+  if (!s) return set_err(FW_E_INVALID, "sim config is NULL");
+  if (!(s->dt > 0)) return set_err(FW_E_INVALID, "dt must be > 0");
+  for (int j = 0; j < 3; j++)
+    if (s->act[j].order != 1 && s->act[j].order != 2) return set_err(FW_E_INVALID, "actuator order must be 1 or 2");
+  if (s->turbulence && s->turb_len < 2) return set_err(FW_E_INVALID, "turb_len must be >= 2");
+  if (e) {
+    if (e->n_obs < 1 || e->n_obs > FW_MAX_OBS) return set_err(FW_E_INVALID, "n_obs out of range");
+    if (e->n_rew < 0 || e->n_rew > FW_MAX_REW) return set_err(FW_E_INVALID, "n_rew out of range");
+    if (e->steps_max > 65535) return set_err(FW_E_UNSUPPORTED, "steps_max > 65535");
+    if (e->streak_req > 128) return set_err(FW_E_UNSUPPORTED, "success_streak_req > 128");
+    for (int o = 0; o < e->n_obs; o++)
+      if (e->obs[o].kind == FW_OBS_ACTION_WINDOW && (e->obs[o].window < 1 || e->obs[o].window > FW_MAX_WINDOW))
+        return set_err(FW_E_UNSUPPORTED, "action window out of range");
+    for (int r = 0; r < e->n_rew; r++)
+      if (e->rew[r].kind == FW_REW_ACTION_DELTA && (e->rew[r].window < 1 || e->rew[r].window > FW_MAX_WINDOW))
+        return set_err(FW_E_UNSUPPORTED, "reward window out of range");
+  }
+  return FW_OK;
+}
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int upload_cfg(fw_handle* h) {
+  if (h->precision == FW_F64) {
+    DevCfg<double> d;
+    fill_devcfg(h, d);
+    FW_HIP(hipMemcpy(h->dcfg, &d, sizeof(d), hipMemcpyHostToDevice));
+  } else {
+    DevCfg<float> d;
+    fill_devcfg(h, d);
+    FW_HIP(hipMemcpy(h->dcfg, &d, sizeof(d), hipMemcpyHostToDevice));
+  }
+  return FW_OK;
+}
+
+template <typename T>
+State<T> state_of(const fw_handle* h) {
+  State<T> s;
+  char* b = (char*)h->base;
+  s.n = h->n;
+  s.ld = h->ld;
+  s.y = (T*)(b + h->o_y);
+  s.der = (T*)(b + h->o_der);
+  s.wind = (T*)(b + h->o_wind);
+  s.target = (T*)(b + h->o_target);
+  s.cmd = (T*)(b + h->o_cmd);
+  s.ep_ret = (T*)(b + h->o_epret);
+  s.act_ring = (T*)(b + h->o_act);
+  s.cmd_ring = h->cmd_window ? (T*)(b + h->o_cmdring) : nullptr;
+  s.steps = (uint32_t*)(b + h->o_steps);
+  s.goal = (uint32_t*)(b + h->o_goal);
+  s.episode = (uint32_t*)(b + h->o_episode);
+  s.noise = (const T*)h->noise;
+  s.noise_len = h->noise_len;
+  s.key0 = (uint32_t)(h->seed & 0xFFFFFFFFu);
+  s.key1 = (uint32_t)(h->seed >> 32);
+  s.env_offset = (uint32_t)h->env_offset;
+  return s;
+}
+
+unsigned grid_of(const fw_handle* h) { return (unsigned)((h->n + BLOCK - 1) / BLOCK); }
+
+int check_launch() {
+  FW_HIP(hipGetLastError());
+  return FW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fw_abi_version(void) { return FWSIM_ABI_VERSION; }
+
+int fw_last_error(char* buf, size_t len) {
+  if (!buf || !len) return FW_E_INVALID;
+  std::snprintf(buf, len, "%s", g_err.c_str());
+  return FW_OK;
+}
+
+int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs, int32_t precision, int32_t device,
+              fw_handle** out) {
+  if (!out) return set_err(FW_E_INVALID, "out is NULL");
+  *out = nullptr;
+  int v = validate(sim, env);
+  if (v) return v;
+  if (n_envs < 1 || n_envs > (int64_t)1 << 31) return set_err(FW_E_INVALID, "n_envs out of range");
+  if (precision != FW_F32 && precision != FW_F64) return set_err(FW_E_INVALID, "precision must be FW_F32 or FW_F64");
+  fw_handle* h = new (std::nothrow) fw_handle();
+  if (!h) return set_err(FW_E_NOMEM, "host allocation failed");
+  h->device = device;
+  h->precision = precision;
+  h->n = n_envs;
+  h->ld = (n_envs + 63) / 64 * 64;
+  h->sim = *sim;
+  h->has_env = env != nullptr;
+  if (env) {
+    h->env = *env;
+    int wa = 1, wc = 0;
+    for (int o = 0; o < env->n_obs; o++)
+      if (env->obs[o].kind == FW_OBS_ACTION_WINDOW) {
+        if (env->scale_actions) wa = std::max(wa, env->obs[o].window - 1);
+        else wc = std::max(wc, env->obs[o].window - 1);
+      }
+    for (int r = 0; r < env->n_rew; r++)
+      if (env->rew[r].kind == FW_REW_ACTION_DELTA) wa = std::max(wa, env->rew[r].window - 1);
+    h->act_window = std::max(wa, 1);
+    h->cmd_window = wc;
+  }
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    delete h;
+    return set_err(FW_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  }
+  const size_t T_ = precision == FW_F64 ? 8 : 4;
+  const size_t row = align_up((size_t)h->ld * T_, 256), row32 = align_up((size_t)h->ld * 4, 256);
+  size_t off = 0;
+  h->o_y = off; off += FW_NY * row;
+  h->o_der = off; off += 8 * row;
+  h->o_wind = off; off += 3 * row;
+  h->o_target = off; off += 3 * row;
+  h->o_cmd = off; off += 3 * row;
+  h->o_epret = off; off += row;
+  h->o_act = off; off += (size_t)h->act_window * 3 * row;
+  h->o_cmdring = off; off += (size_t)h->cmd_window * 3 * row;
+  h->o_steps = off; off += row32;
+  h->o_goal = off; off += 4 * row32;
+  h->o_episode = off; off += row32;
+  // rows are ld elements apart: the padding above is folded into ld for simplicity
+  h->base_bytes = off;
+  e = hipMalloc(&h->base, off);
+  if (e == hipSuccess) e = hipMemset(h->base, 0, off);
+  if (e == hipSuccess) e = hipMalloc(&h->dcfg, precision == FW_F64 ? sizeof(DevCfg<double>) : sizeof(DevCfg<float>));
+  if (e != hipSuccess) {
+    if (h->base) (void)hipFree(h->base);
+    delete h;
+    return set_err(FW_E_HIP, std::string("device allocation: ") + hipGetErrorString(e));
+  }
+  v = upload_cfg(h);
+  if (v) {
+    (void)hipFree(h->base);
+    (void)hipFree(h->dcfg);
+    delete h;
+    return v;
+  }
+  *out = h;
+  return FW_OK;
+}
+
+int fw_destroy(fw_handle* h) {
+  if (!h) return FW_OK;
+  (void)hipSetDevice(h->device);
+  if (h->base) (void)hipFree(h->base);
+  if (h->dcfg) (void)hipFree(h->dcfg);
+  delete h;
+  return FW_OK;
+}
+
+int fw_num_envs(const fw_handle* h, int64_t* n) {
+  if (!h || !n) return set_err(FW_E_INVALID, "NULL argument");
+  *n = h->n;
+  return FW_OK;
+}
+
+int fw_num_obs(const fw_handle* h, int32_t* n) {
+  if (!h || !n) return set_err(FW_E_INVALID, "NULL argument");
+  *n = h->has_env ? h->env.n_obs : 0;
+  return FW_OK;
+}
+
+int fw_seed(fw_handle* h, uint64_t seed, int64_t env_offset) {
+  if (!h) return set_err(FW_E_INVALID, "NULL handle");
+  h->seed = seed;
+  h->env_offset = env_offset;
+  return FW_OK;
+}
+
+int fw_set_noise(fw_handle* h, const void* noise_dev, int64_t len) {
+  if (!h) return set_err(FW_E_INVALID, "NULL handle");
+  if (noise_dev && len < 1) return set_err(FW_E_INVALID, "noise length must be >= 1");
+  h->noise = noise_dev;
+  h->noise_len = noise_dev ? len : 0;
+  return FW_OK;
+}
+
+int fw_update_config(fw_handle* h, const fw_sim_config* sim, const fw_env_config* env) {
+  if (!h) return set_err(FW_E_INVALID, "NULL handle");
+  int v = validate(sim, env);
+  if (v) return v;
+  if ((env != nullptr) != h->has_env) return set_err(FW_E_INVALID, "env config presence cannot change");
+  if (env) {
+    // windows decide the ring sizes allocated at create time
+    fw_handle tmp = *h;
+    tmp.env = *env;
+    int wa = 1, wc = 0;
+    for (int o = 0; o < env->n_obs; o++)
+      if (env->obs[o].kind == FW_OBS_ACTION_WINDOW) {
+        if (env->scale_actions) wa = std::max(wa, env->obs[o].window - 1);
+        else wc = std::max(wc, env->obs[o].window - 1);
+      }
+    for (int r = 0; r < env->n_rew; r++)
+      if (env->rew[r].kind == FW_REW_ACTION_DELTA) wa = std::max(wa, env->rew[r].window - 1);
+    if (wa != h->act_window || wc != h->cmd_window || env->n_obs != h->env.n_obs)
+      return set_err(FW_E_UNSUPPORTED, "config update may not change observation layout or window sizes");
+    h->env = *env;
+  }
+  h->sim = *sim;
+  FW_HIP(hipSetDevice(h->device));
+  FW_HIP(hipDeviceSynchronize());
+  return upload_cfg(h);
+}
+
+int fw_reset(fw_handle* h, const uint8_t* mask_dev, const void* init_dev, const void* target_dev, void* obs_dev,
+             void* stream) {
+  if (!h) return set_err(FW_E_INVALID, "NULL handle");
+  FW_HIP(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  if (h->precision == FW_F64)
+    hipLaunchKernelGGL(k_reset<double>, dim3(grid_of(h)), dim3(BLOCK), 0, st, (const DevCfg<double>*)h->dcfg,
+                       state_of<double>(h), mask_dev, (const double*)init_dev, (const double*)target_dev,
+                       (double*)obs_dev);
+  else
+    hipLaunchKernelGGL(k_reset<float>, dim3(grid_of(h)), dim3(BLOCK), 0, st, (const DevCfg<float>*)h->dcfg,
+                       state_of<float>(h), mask_dev, (const float*)init_dev, (const float*)target_dev, (float*)obs_dev);
+  return check_launch();
+}
+
+int fw_observe(fw_handle* h, void* obs_dev, void* stream) {
+  if (!h || !obs_dev) return set_err(FW_E_INVALID, "NULL argument");
+  if (!h->has_env) return set_err(FW_E_INVALID, "handle has no env config");
+  FW_HIP(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  if (h->precision == FW_F64)
+    hipLaunchKernelGGL(k_observe<double>, dim3(grid_of(h)), dim3(BLOCK), 0, st, (const DevCfg<double>*)h->dcfg,
+                       state_of<double>(h), (double*)obs_dev);
+  else
+    hipLaunchKernelGGL(k_observe<float>, dim3(grid_of(h)), dim3(BLOCK), 0, st, (const DevCfg<float>*)h->dcfg,
+                       state_of<float>(h), (float*)obs_dev);
+  return check_launch();
+}
+
+int fw_sim_step(fw_handle* h, const void* commands_dev, void* commands_out_dev, uint8_t* success_dev, int32_t* term_dev,
+                int32_t* stats_dev, void* stream) {
+  if (!h || !commands_dev) return set_err(FW_E_INVALID, "NULL argument");
+  FW_HIP(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  if (h->precision == FW_F64)
+    hipLaunchKernelGGL(k_sim_step<double>, dim3(grid_of(h)), dim3(BLOCK), 0, st, (const DevCfg<double>*)h->dcfg,
+                       state_of<double>(h), (const double*)commands_dev, (double*)commands_out_dev, success_dev,
+                       term_dev, stats_dev);
+  else
+    hipLaunchKernelGGL(k_sim_step<float>, dim3(grid_of(h)), dim3(BLOCK), 0, st, (const DevCfg<float>*)h->dcfg,
+                       state_of<float>(h), (const float*)commands_dev, (float*)commands_out_dev, success_dev, term_dev,
+                       stats_dev);
+  return check_launch();
+}
+
+int fw_env_step(fw_handle* h, const void* actions_dev, void* obs_dev, void* reward_dev, uint8_t* done_dev,
+                int32_t* term_dev, void* terminal_obs_dev, void* episode_dev, int32_t* stats_dev, int32_t auto_reset,
+                void* stream) {
+  if (!h || !actions_dev || !obs_dev || !reward_dev || !done_dev) return set_err(FW_E_INVALID, "NULL argument");
+  if (!h->has_env) return set_err(FW_E_INVALID, "handle has no env config");
+  FW_HIP(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  if (h->precision == FW_F64)
+    hipLaunchKernelGGL(k_env_step<double>, dim3(grid_of(h)), dim3(BLOCK), 0, st, (const DevCfg<double>*)h->dcfg,
+                       state_of<double>(h), (const double*)actions_dev, (double*)obs_dev, (double*)reward_dev,
+                       done_dev, term_dev, (double*)terminal_obs_dev, (double*)episode_dev, stats_dev, auto_reset);
+  else
+    hipLaunchKernelGGL(k_env_step<float>, dim3(grid_of(h)), dim3(BLOCK), 0, st, (const DevCfg<float>*)h->dcfg,
+                       state_of<float>(h), (const float*)actions_dev, (float*)obs_dev, (float*)reward_dev, done_dev,
+                       term_dev, (float*)terminal_obs_dev, (float*)episode_dev, stats_dev, auto_reset);
+  return check_launch();
+}
+
+static int block_info(const fw_handle* h, int32_t block, size_t* off, int* rows, size_t* esz) {
+  const size_t T_ = h->precision == FW_F64 ? 8 : 4;
+  switch (block) {
+    case FW_BLK_ODE: *off = h->o_y; *rows = FW_NY; *esz = T_; return FW_OK;
+    case FW_BLK_DERIVED: *off = h->o_der; *rows = 8; *esz = T_; return FW_OK;
+    case FW_BLK_TARGET: *off = h->o_target; *rows = 3; *esz = T_; return FW_OK;
+    case FW_BLK_WIND: *off = h->o_wind; *rows = 3; *esz = T_; return FW_OK;
+    case FW_BLK_STEPS: *off = h->o_steps; *rows = 1; *esz = 4; return FW_OK;
+    case FW_BLK_COMMAND: *off = h->o_cmd; *rows = 3; *esz = T_; return FW_OK;
+    default: return set_err(FW_E_INVALID, "unknown state block");
+  }
+}
+
+// Blocks are exchanged densely as [rows][N].
+int fw_get_state(fw_handle* h, int32_t block, void* dst_dev, void* stream) {
+  if (!h || !dst_dev) return set_err(FW_E_INVALID, "NULL argument");
+  size_t off, esz;
+  int rows;
+  int v = block_info(h, block, &off, &rows, &esz);
+  if (v) return v;
+  FW_HIP(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t row = align_up((size_t)h->ld * esz, 256);
+  FW_HIP(hipMemcpy2DAsync(dst_dev, h->n * esz, (char*)h->base + off, row, h->n * esz, rows, hipMemcpyDeviceToDevice,
+                          st));
+  return FW_OK;
+}
+
+int fw_set_state(fw_handle* h, int32_t block, const void* src_dev, void* stream) {
+  if (!h || !src_dev) return set_err(FW_E_INVALID, "NULL argument");
+  size_t off, esz;
+  int rows;
+  int v = block_info(h, block, &off, &rows, &esz);
+  if (v) return v;
+  FW_HIP(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t row = align_up((size_t)h->ld * esz, 256);
+  FW_HIP(hipMemcpy2DAsync((char*)h->base + off, row, src_dev, h->n * esz, h->n * esz, rows, hipMemcpyDeviceToDevice,
+                          st));
+  return FW_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,170 @@
+"""Engine: one libfwsim handle = N aircraft resident on one GPU.
+
+Thin, allocation-free-per-step wrapper over the C ABI (include/fwsim.h): device
+buffers are torch tensors on the handle's device, passed by data_ptr() together
+with torch's current HIP stream, so every call is asynchronous and ordered with
+the caller's torch work (policy forward, rollout buffer writes, RCCL).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native
+from . import config as C
+
+F32, F64 = 0, 1
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class Engine:
+    def __init__(self, sim_spec, env_spec=None, num_envs=1, device=None, precision="float32"):
+        if not torch.cuda.is_available():
+            raise _native.FwError("no HIP device visible: the fixed-wing engine runs on MI355X only (no CPU fallback)")
+        self.lib = _native.load()
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        if precision not in ("float32", "float64"):
+            raise ValueError("precision must be 'float32' or 'float64'")
+        self.precision = precision
+        self.dtype = torch.float32 if precision == "float32" else torch.float64
+        self.n = int(num_envs)
+        self.sim_spec, self.env_spec = sim_spec, env_spec
+        self._sim_cfg = sim_spec.struct()
+        self._env_cfg = env_spec.struct() if env_spec is not None else None
+        h = ctypes.c_void_p()
+        _native.check(self.lib.fw_create(ctypes.byref(self._sim_cfg),
+                                         ctypes.byref(self._env_cfg) if self._env_cfg is not None else None,
+                                         self.n, F32 if precision == "float32" else F64, self.device.index,
+                                         ctypes.byref(h)), "fw_create")
+        self.h = h
+        self.n_obs = env_spec.n_obs if env_spec is not None else 0
+        dev, dt = self.device, self.dtype
+        n = self.n
+        # persistent per-step I/O buffers (no allocation in the step path)
+        self.obs = torch.zeros(n, max(self.n_obs, 1), dtype=dt, device=dev)
+        self.terminal_obs = torch.zeros_like(self.obs)
+        self.reward = torch.zeros(n, dtype=dt, device=dev)
+        self.done = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.term = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.episode = torch.zeros(n, 2, dtype=dt, device=dev)
+        self.stats = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.success = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.cmd_out = torch.zeros(n, 3, dtype=dt, device=dev)
+        self._noise = None
+        self.seed(0)
+
+    # ------------------------------------------------------------------
+    def stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.fw_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
+    def seed(self, seed, env_offset=0):
+        """Philox key; env i of this engine draws from stream (seed, env_offset + i)."""
+        seed = 0 if seed is None else int(seed)
+        _native.check(self.lib.fw_seed(self.h, seed % (1 << 64), int(env_offset)), "fw_seed")
+        self._seed = seed
+
+    def update_config(self, sim_spec=None, env_spec=None):
+        if sim_spec is not None:
+            self.sim_spec = sim_spec
+        if env_spec is not None:
+            self.env_spec = env_spec
+        self._sim_cfg = self.sim_spec.struct()
+        self._env_cfg = self.env_spec.struct() if self.env_spec is not None else None
+        _native.check(self.lib.fw_update_config(self.h, ctypes.byref(self._sim_cfg),
+                                                ctypes.byref(self._env_cfg) if self._env_cfg is not None else None),
+                      "fw_update_config")
+
+    def set_noise(self, noise):
+        """Inject N(0,1) turbulence noise, array-like [n][4][len] or [4][len] (shared), or None."""
+        if noise is None:
+            self._noise = None
+            _native.check(self.lib.fw_set_noise(self.h, None, 0), "fw_set_noise")
+            return
+        a = torch.as_tensor(np.asarray(noise), dtype=self.dtype)
+        if a.dim() == 2:
+            a = a.unsqueeze(0).expand(self.n, *a.shape)
+        if a.shape[0] != self.n or a.shape[1] != 4:
+            raise ValueError("noise must be [n][4][len] or [4][len]")
+        L = a.shape[2]
+        ld = (self.n + 63) // 64 * 64
+        buf = torch.zeros(4, L, ld, dtype=self.dtype, device=self.device)
+        buf[:, :, :self.n] = a.permute(1, 2, 0).to(self.device)
+        self._noise = buf
+        _native.check(self.lib.fw_set_noise(self.h, _ptr(buf), L), "fw_set_noise")
+
+    # ------------------------------------------------------------------
+    def reset(self, mask=None, init=None, target=None, want_obs=True):
+        """Masked reset.  init: [FW_NINIT][n] (NaN = sample), target: [3][n] (NaN = sample)."""
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        it = None
+        if init is not None:
+            it = torch.as_tensor(np.asarray(init), dtype=self.dtype).to(self.device).contiguous()
+            assert it.shape == (C.FW_NINIT, self.n)
+        tg = None
+        if target is not None:
+            tg = torch.as_tensor(np.asarray(target), dtype=self.dtype).to(self.device).contiguous()
+            assert tg.shape == (3, self.n)
+        obs = self.obs if (want_obs and self.n_obs) else None
+        _native.check(self.lib.fw_reset(self.h, _ptr(m), _ptr(it), _ptr(tg), _ptr(obs), self.stream()), "fw_reset")
+        return self.obs if obs is not None else None
+
+    def sim_step(self, commands, stats=False):
+        """PyFly.step for all aircraft.  commands: tensor [n][3] on device (elevator, aileron, throttle)."""
+        cmd = commands.to(device=self.device, dtype=self.dtype).contiguous()
+        _native.check(self.lib.fw_sim_step(self.h, _ptr(cmd), _ptr(self.cmd_out), _ptr(self.success), _ptr(self.term),
+                                           _ptr(self.stats) if stats else None, self.stream()), "fw_sim_step")
+        return self.success, self.term
+
+    def env_step(self, actions, auto_reset=True, stats=False, terminal_obs=True, episode=True):
+        act = actions if (actions.dtype == self.dtype and actions.device == self.device and actions.is_contiguous()) \
+            else actions.to(device=self.device, dtype=self.dtype).contiguous()
+        _native.check(self.lib.fw_env_step(self.h, _ptr(act), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
+                                           _ptr(self.term), _ptr(self.terminal_obs) if terminal_obs else None,
+                                           _ptr(self.episode) if episode else None,
+                                           _ptr(self.stats) if stats else None, int(bool(auto_reset)),
+                                           self.stream()), "fw_env_step")
+        return self.obs, self.reward, self.done, self.term
+
+    def observe(self):
+        _native.check(self.lib.fw_observe(self.h, _ptr(self.obs), self.stream()), "fw_observe")
+        return self.obs
+
+    # ------------------------------------------------------------------
+    _ROWS = {C.FW_BLK_ODE: C.FW_NY, C.FW_BLK_DERIVED: 8, C.FW_BLK_TARGET: 3, C.FW_BLK_WIND: 3, C.FW_BLK_STEPS: 1,
+             C.FW_BLK_COMMAND: 3}
+
+    def get_block(self, blk):
+        rows = self._ROWS[blk]
+        dt = torch.int32 if blk == C.FW_BLK_STEPS else self.dtype
+        out = torch.empty(rows, self.n, dtype=dt, device=self.device)
+        _native.check(self.lib.fw_get_state(self.h, blk, _ptr(out), self.stream()), "fw_get_state")
+        return out
+
+    def set_block(self, blk, value):
+        rows = self._ROWS[blk]
+        dt = torch.int32 if blk == C.FW_BLK_STEPS else self.dtype
+        v = torch.as_tensor(value, dtype=dt).to(self.device).reshape(rows, self.n).contiguous()
+        _native.check(self.lib.fw_set_state(self.h, blk, _ptr(v), self.stream()), "fw_set_state")
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def steps(self):
+        s = self.get_block(C.FW_BLK_STEPS)[0]
+        return s & 0xFFFF, (s >> 16) & 0xFFFF
