@@ -30,6 +30,7 @@ namespace fw {
 
 constexpr int NY = FW_NY;
 constexpr double PI_D = 3.141592653589793;
+constexpr int MAX_NFEV = 6000;  // RHS evaluations per step before the step is declared a solver failure
 
 template <typename T>
 struct Lim {
@@ -46,6 +47,7 @@ struct DevCfg {
   T half_rho, S, b, c, mass, inv_mass, mg, inv_Jy;
   T gam[9];
   T M, a0, pi_e_ar;
+  T sig_c;                   // exp(2 M a0) = e^{-M(a-a0)} e^{M(a+a0)} (stall-blend constant)
   T CL0, CLa, CLq, CLde, CDp, CDq, CDb1, CDb2, CDde, Cm0, Cma, Cmq, Cmde, Cmfp;
   T CY0, CYb, CYp, CYr, CYda, CYdr, Cl0, Clb, Clp, Clr, Clda, Cldr, Cn0, Cnb, Cnp, Cnr, Cnda, Cndr;
   T kmotor, prop_k, kTP, kOmega;
@@ -297,7 +299,10 @@ FW_HD int rhs(const DevCfg<T>& c0, const StepCtx<T>& X, bool first, const T* y, 
   airspeed_vec(y, X.wind, X.tl, vel, va);
   const T Va_raw = fsqrt(va[0] * va[0] + va[1] * va[1] + va[2] * va[2]);
   T alpha = atan2(va[2], va[0]);
-  const T sb_raw = fdiv(va[1], Va_raw);
+  T sb_raw = fdiv(va[1], Va_raw);
+  // |v|/|va| <= 1 exactly; the 1-ulp reciprocal of the fp32 path can push the
+  // ratio past 1 in pure sideslip, where asin would return NaN
+  if (sizeof(T) == 4) sb_raw = clipv(sb_raw, T(-1), T(1));
   T beta = asin(sb_raw);
   const T Va = cond(c, FW_V_VA, Va_raw, term);
   alpha = cond(c, FW_V_ALPHA, alpha, term);
@@ -327,10 +332,12 @@ FW_HD int rhs(const DevCfg<T>& c0, const StepCtx<T>& X, bool first, const T* y, 
   const T fg2 = c.mg * (e3 * e3 + e0 * e0 - e1 * e1 - e2 * e2);
   const T ex1 = fexp(-c.M * (alpha - c.a0));
   const T ex2 = fexp(c.M * (alpha + c.a0));
-  // stall blend; an overflowed exponential means sigma == 1 to working precision
-  T sigma = fdiv(T(1) + ex1 + ex2, (T(1) + ex1) * (T(1) + ex2));
-  const T huge = sizeof(T) == 4 ? T(3.0e38f) : T(1e300);
-  if (ex1 > huge || ex2 > huge) sigma = T(1);
+  // stall blend sigma = (1+e1+e2) / ((1+e1)(1+e2)) (pyfly.py:1541-1543).  Since
+  // e1 e2 = exp(2 M a0) = C, the denominator is S + C with S = 1+e1+e2, so
+  // sigma = 1 / (1 + C/S): the same value, but it never forms the ~1e38 product
+  // (whose fp32 reciprocal flushes to 0 and flips sigma from 1 to 0 deep in
+  // stall) and it is exactly 1 when an exponential overflows.
+  const T sigma = frcp(T(1) + c.sig_c * frcp(T(1) + ex1 + ex2));
   const T sgna = sgn(alpha);
   const T CLlin = c.CL0 + c.CLa * alpha;
   const T CL = (T(1) - sigma) * CLlin + sigma * (T(2) * sgna * sa * sa * ca);
@@ -451,6 +458,12 @@ FW_HD int rk45(const DevCfg<T>& c, const StepCtx<T>& X, T* y_io, T* __restrict__
       const int term = rhs(c, X, stage == 0, ys, K);
       if (term) {
         result = term;
+        active = false;
+      }
+      // hard bound on work per step so that no input can keep a wave spinning:
+      // scipy's own TOO_SMALL_STEP exit needs < 2100 evaluations from any h <= dt
+      if (nfev >= MAX_NFEV) {
+        result = -1;
         active = false;
       }
     }
@@ -576,7 +589,7 @@ FW_HD int rk45(const DevCfg<T>& c, const StepCtx<T>& X, T* y_io, T* __restrict__
         } else {
           h_abs *= fmax(0.2, 0.9 * (double)fpow(en, T(-0.2)));
           rejected = true;
-          if (h_abs < min_step) {  // TOO_SMALL_STEP: solver failure
+          if (!(h_abs >= min_step)) {  // TOO_SMALL_STEP (or a NaN step size): solver failure
             result = -1;
             active = false;
           } else {

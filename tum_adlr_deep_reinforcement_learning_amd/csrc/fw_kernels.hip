@@ -674,6 +674,7 @@ void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
   d.M = (T)P[FW_P_M];
   d.a0 = (T)P[FW_P_A0];
   d.pi_e_ar = (T)(3.141592653589793 * P[FW_P_E] * (P[FW_P_B] * P[FW_P_B] / P[FW_P_S_WING]));
+  d.sig_c = (T)std::exp(2.0 * P[FW_P_M] * P[FW_P_A0]);
   d.CL0 = (T)P[FW_P_C_L_0]; d.CLa = (T)P[FW_P_C_L_ALPHA]; d.CLq = (T)P[FW_P_C_L_Q]; d.CLde = (T)P[FW_P_C_L_DELTA_E];
   d.CDp = (T)P[FW_P_C_D_P]; d.CDq = (T)P[FW_P_C_D_Q]; d.CDb1 = (T)P[FW_P_C_D_BETA1]; d.CDb2 = (T)P[FW_P_C_D_BETA2];
   d.CDde = (T)P[FW_P_C_D_DELTA_E];
