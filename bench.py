@@ -152,7 +152,8 @@ def main():
         try:
             with open(pmc) as f:
                 pm = json.load(f)
-            if pm.get("envs") == n and pm.get("precision") == args.precision:
+            if pm.get("envs") == n and pm.get("precision") == args.precision and \
+                    bool(pm.get("turbulence")) == bool(args.turbulence):
                 traffic = pm.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None

@@ -243,8 +243,9 @@ int fw_sim_step(fw_handle* h, const void* commands_dev, void* commands_out_dev, 
 /* FixedWingAircraft.step for all envs (+ VecEnv auto-reset when auto_reset != 0).
  * actions_dev [N][3]; obs_dev [N][n_obs]; reward_dev [N]; done_dev uint8[N];
  * term_dev int32[N]; terminal_obs_dev [N][n_obs] (written for done envs only,
- * may be NULL); episode_dev [N][2] = (return, length) written for done envs
- * (may be NULL); stats_dev as in fw_sim_step (may be NULL).                  */
+ * may be NULL); episode_dev [N][5] = (return, length, final target roll,
+ * pitch, Va) written for done envs (may be NULL); stats_dev as in fw_sim_step
+ * (may be NULL).                                                             */
 int fw_env_step(fw_handle* h, const void* actions_dev, void* obs_dev, void* reward_dev, uint8_t* done_dev,
                 int32_t* term_dev, void* terminal_obs_dev, void* episode_dev, int32_t* stats_dev,
                 int32_t auto_reset, void* stream);

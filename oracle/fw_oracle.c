@@ -11,7 +11,7 @@
  *                          golden fixtures were generated with)
  *   FixedWingAircraft.step magpie/libs/fixed-wing-gym/gym_fixed_wing/fixed_wing.py:483-628
  *
- * Parity is pinned by tests/golden/*.npz, produced by running the reference
+ * Parity is pinned by the .npz fixtures in tests/golden/, produced by running the reference
  * itself (tests/golden/gen_golden.py).  Reference file:line citations are on
  * every function below (pyfly.py = magpie/libs/pyfly/pyfly/pyfly.py,
  * fixed_wing.py = magpie/libs/fixed-wing-gym/gym_fixed_wing/fixed_wing.py).

@@ -580,14 +580,19 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
   if (term_out) term_out[i] = term;
   if (stats) stats[i] = nfev | (nacc << 16);
 
+  // Monitor episode record + the episode's final target (info["target"] of the done step)
+  if (done && episode_out) {
+    T* e = episode_out + i * 5;
+    e[0] = ep_ret;
+    e[1] = (T)steps;
+    e[2] = tgt[0];
+    e[3] = tgt[1];
+    e[4] = tgt[2];
+  }
   // wavefront-uniform skip of the reset path when no lane of the wave is done
   const bool do_reset = done && auto_reset;
   if (__ballot(do_reset)) {
     if (do_reset) {
-      if (episode_out) {
-        episode_out[i * 2 + 0] = ep_ret;
-        episode_out[i * 2 + 1] = (T)steps;
-      }
       T yr[NY], dr[8], wr[3], tr[3];
       reset_lane(c, s, i, (const T*)nullptr, (const T*)nullptr, yr, dr, wr, tr);
       store_env_fresh(c, s, i, yr, dr, wr, tr);
@@ -595,10 +600,6 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
       observe(c, yr, dr, tr, 0, seq0, seq0, orow, 1);
       return;
     }
-  }
-  if (done && episode_out) {
-    episode_out[i * 2 + 0] = ep_ret;
-    episode_out[i * 2 + 1] = (T)steps;
   }
   observe(c, y, der, tgt, steps, seqA, seqC, orow, 1);
 #pragma unroll

@@ -51,7 +51,7 @@ class Engine:
         self.reward = torch.zeros(n, dtype=dt, device=dev)
         self.done = torch.zeros(n, dtype=torch.uint8, device=dev)
         self.term = torch.zeros(n, dtype=torch.int32, device=dev)
-        self.episode = torch.zeros(n, 2, dtype=dt, device=dev)
+        self.episode = torch.zeros(n, 5, dtype=dt, device=dev)  # return, length, final target x3
         self.stats = torch.zeros(n, dtype=torch.int32, device=dev)
         self.success = torch.zeros(n, dtype=torch.uint8, device=dev)
         self.cmd_out = torch.zeros(n, 3, dtype=dt, device=dev)

@@ -1,0 +1,288 @@
+"""Device-resident VecEnv with the Stable-Baselines3 0.10 surface.
+
+``FixedWingVecEnv`` replaces ``VecNormalize(SubprocVecEnv([FixedWingAircraft(...)] * n))``'s
+inner part -- the reference runs one OS process per env
+(stable_baselines3/common/vec_env/subproc_vec_env.py:17-208) and pickles every
+observation through a pipe; here all N aircraft live in HBM and one fused
+kernel steps them.  Method names, signatures and auto-reset semantics follow
+``VecEnv`` (base_vec_env.py:48-200) and the SubprocVecEnv worker
+(subproc_vec_env.py:25-31): when an env is done, ``info["terminal_observation"]``
+holds its last observation and the returned observation is the first one of
+the next episode.  Monitor statistics (common/monitor.py:88-115) are reported
+as ``info["episode"] = {"r", "l", "t"}`` for done envs.
+
+Step results are numpy arrays (SB3 semantics) unless ``return_tensors=True``,
+in which case they stay on the device as torch tensors (no host sync).
+"""
+import collections.abc
+import time
+
+import numpy as np
+import torch
+
+from . import config as C
+from .engine import Engine
+from .spaces import Box
+
+try:  # subclass SB3's VecEnv when available so isinstance checks pass
+    from stable_baselines3.common.vec_env.base_vec_env import VecEnv as _SB3VecEnv  # pragma: no cover
+except Exception:  # noqa: BLE001
+    _SB3VecEnv = None
+
+
+class VecEnv(_SB3VecEnv if _SB3VecEnv is not None else object):
+    """Minimal restatement of SB3's abstract VecEnv (base_vec_env.py:48-200)."""
+
+    metadata = {"render.modes": []}
+
+    def __init__(self, num_envs, observation_space, action_space):
+        self.num_envs = num_envs
+        self.observation_space = observation_space
+        self.action_space = action_space
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def get_images(self):
+        raise NotImplementedError
+
+    def render(self, mode="human"):
+        raise NotImplementedError("rendering is not part of the device engine")
+
+    @property
+    def unwrapped(self):
+        return self
+
+    def getattr_depth_check(self, name, already_found):
+        return None
+
+    def _get_indices(self, indices):
+        if indices is None:
+            indices = range(self.num_envs)
+        elif isinstance(indices, int):
+            indices = [indices]
+        return indices
+
+
+def termination_name(code, dynamics=("elevon_right", "elevon_left", "throttle")):
+    """Termination code -> the reference's info["termination"] string."""
+    code = int(code)
+    if code == C.FW_TERM_STEPS:
+        return "steps"
+    if code == C.FW_TERM_SUCCESS:
+        return "success"
+    v = code - 1
+    if C.FW_V_ACT0 <= v <= C.FW_V_ACT2:
+        return dynamics[v - C.FW_V_ACT0]
+    if 0 <= v < len(C.VAR_NAMES):
+        return C.VAR_NAMES[v]
+    return "solver"
+
+
+class _Infos(collections.abc.Sequence):
+    """Per-env info dicts, materialised on first access (65536 dicts per step are
+    the dominant host cost of the SB3 surface, and most callers touch few)."""
+
+    def __init__(self, n, done, term, tobs, episode, targets, t_elapsed, dynamics, with_target):
+        self._n = n
+        self._done, self._term, self._tobs, self._ep = done, term, tobs, episode
+        self._tgt = targets
+        self._t = t_elapsed
+        self._dyn = dynamics
+        self._with_target = with_target
+        self._cache = {}
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(self._n))]
+        if i < 0:
+            i += self._n
+        d = self._cache.get(i)
+        if d is None:
+            d = {}
+            if self._done[i]:
+                d["terminal_observation"] = self._tobs[i]
+                d["termination"] = termination_name(self._term[i], self._dyn)
+                ep = self._ep[i]
+                d["episode"] = {"r": round(float(ep[0]), 6), "l": int(round(float(ep[1]))), "t": round(self._t, 6)}
+                if self._with_target:
+                    d["target"] = {"roll": float(ep[2]), "pitch": float(ep[3]), "Va": float(ep[4])}
+            elif self._with_target:
+                t = self._tgt[:, i]
+                d["target"] = {"roll": float(t[0]), "pitch": float(t[1]), "Va": float(t[2])}
+            self._cache[i] = d
+        return d
+
+
+class FixedWingVecEnv(VecEnv):
+    """N FixedWingAircraft environments stepped by one fused MI355X kernel.
+
+    Construction mirrors ``FixedWingAircraft(config_path, sim_config_path=...,
+    sim_parameter_path=..., config_kw=..., sim_config_kw=...)``
+    (fixed_wing.py:14-24) plus the batch size and device.
+    """
+
+    def __init__(self, num_envs=1, config_path=None, config_kw=None, sim_config_path=None, sim_parameter_path=None,
+                 sim_config_kw=None, device=None, precision="float32", seed=None, return_tensors=False,
+                 info_target=True, curriculum_level=1, env_offset=0):
+        self.spec = C.EnvSpec(config_path, config_kw, sim_config_path, sim_parameter_path, sim_config_kw,
+                              curriculum_level=curriculum_level)
+        obs_space = Box(self.spec.obs_low, self.spec.obs_high, dtype=np.float32)
+        act_space = Box(self.spec.action_space_low, self.spec.action_space_high, dtype=np.float32)
+        VecEnv.__init__(self, int(num_envs), obs_space, act_space)
+        self.engine = Engine(self.spec.sim, self.spec, self.num_envs, device=device, precision=precision)
+        self.device = self.engine.device
+        self.return_tensors = return_tensors
+        self.info_target = info_target
+        self.env_offset = int(env_offset)
+        self.training = True
+        self._actions = None
+        self._t_start = time.time()
+        self._dyn = tuple(self.spec.sim.dynamics)
+        self.seed(seed if seed is not None else 0)
+        self._reset_pending = True
+
+    @property
+    def cfg(self):
+        return self.spec.cfg
+
+    # ---------------------------------------------------------------- VecEnv API
+    def seed(self, seed=None):
+        """SubprocVecEnv.seed gives env i the seed ``seed + i`` (subproc_vec_env.py:120-123); here env i
+        draws from Philox stream (seed, env_offset + i)."""
+        s = 0 if seed is None else int(seed)
+        self.engine.seed(s, env_offset=self.env_offset)
+        return [s + i for i in range(self.num_envs)]
+
+    def reset(self):
+        obs = self.engine.reset()
+        self._reset_pending = False
+        return self._out(obs)
+
+    def step_async(self, actions):
+        if isinstance(actions, torch.Tensor):
+            a = actions.to(device=self.device, dtype=self.engine.dtype)
+        else:
+            a = torch.as_tensor(np.asarray(actions), dtype=self.engine.dtype).to(self.device, non_blocking=True)
+        self._actions = a.reshape(self.num_envs, -1).contiguous()
+
+    def step_wait(self):
+        if self._actions is None:
+            raise RuntimeError("step_wait() without step_async()")
+        eng = self.engine
+        obs, rew, done, term = eng.env_step(self._actions, auto_reset=True)
+        self._actions = None
+        if self.return_tensors:
+            return obs, rew, done.bool(), self._infos_lazy_device()
+        done_np = done.cpu().numpy().astype(bool)
+        infos = self._infos(done_np)
+        return obs.cpu().numpy().astype(np.float32), rew.cpu().numpy().astype(np.float32), done_np, infos
+
+    def _infos(self, done_np):
+        eng = self.engine
+        term = eng.term.cpu().numpy()
+        anyd = bool(done_np.any())
+        tobs = eng.terminal_obs.cpu().numpy().astype(np.float32) if anyd else None
+        ep = eng.episode.cpu().numpy() if anyd else None
+        tgt = eng.get_block(C.FW_BLK_TARGET).cpu().numpy() if self.info_target else None
+        return _Infos(self.num_envs, done_np, term, tobs, ep, tgt, time.time() - self._t_start, self._dyn,
+                      self.info_target)
+
+    def _infos_lazy_device(self):
+        """Device mode: infos are built only if the caller asks for them (triggers a sync)."""
+        env = self
+
+        class _Lazy(collections.abc.Sequence):
+            _inner = None
+
+            def _get(self):
+                if self._inner is None:
+                    self._inner = env._infos(env.engine.done.cpu().numpy().astype(bool))
+                return self._inner
+
+            def __len__(self):
+                return env.num_envs
+
+            def __getitem__(self, i):
+                return self._get()[i]
+
+        return _Lazy()
+
+    def close(self):
+        self.engine.close()
+
+    def get_attr(self, attr_name, indices=None):
+        idx = list(self._get_indices(indices))
+        if attr_name == "target":
+            t = self.engine.get_block(C.FW_BLK_TARGET).cpu().numpy()
+            return [{"roll": float(t[0, i]), "pitch": float(t[1, i]), "Va": float(t[2, i])} for i in idx]
+        if attr_name == "simulator":
+            from .pyfly import SimulatorView
+            return [SimulatorView(self.engine, i) for i in idx]
+        if attr_name in ("cfg", "observation_space", "action_space", "training", "steps_max"):
+            val = {"cfg": self.spec.cfg, "observation_space": self.observation_space,
+                   "action_space": self.action_space, "training": self.training,
+                   "steps_max": self.spec.steps_max}[attr_name]
+            return [val for _ in idx]
+        if attr_name == "steps_count":
+            s, _ = self.engine.steps()
+            s = s.cpu().numpy()
+            return [int(s[i]) for i in idx]
+        raise AttributeError("FixedWingVecEnv has no per-env attribute %r" % attr_name)
+
+    def set_attr(self, attr_name, value, indices=None):
+        if attr_name == "training":
+            self.training = value
+            return
+        raise AttributeError("setting %r is not supported on the device env" % attr_name)
+
+    def env_method(self, method_name, *method_args, indices=None, **method_kwargs):
+        idx = list(self._get_indices(indices))
+        if method_name == "reset":
+            return self._reset_some(idx, *method_args, **method_kwargs)
+        if method_name == "set_curriculum_level":
+            self.set_curriculum_level(*method_args, **method_kwargs)
+            return [None for _ in idx]
+        if method_name == "seed":
+            return [self.seed(*method_args, **method_kwargs)[i] for i in idx]
+        if method_name in ("render", "save_history"):
+            raise NotImplementedError("%s is host-side plotting; out of scope for the device engine" % method_name)
+        raise AttributeError("unsupported env_method %r" % method_name)
+
+    # --------------------------------------------------------------- extras
+    def set_curriculum_level(self, level):
+        """FixedWingAircraft.set_curriculum_level (fixed_wing.py:334-412) for all envs."""
+        self.spec.set_curriculum_level(level)
+        self.engine.update_config(self.spec.sim, self.spec)
+
+    def _reset_some(self, idx, state=None, target=None, turbulence_noise=None):
+        """FixedWingAircraft.reset(state=..., target=...) for the envs in ``idx``."""
+        n = self.num_envs
+        mask = np.zeros(n, np.uint8)
+        mask[idx] = 1
+        init = None
+        if state is not None:
+            states = [None] * n
+            for i in idx:
+                states[i] = state
+            init = C.init_array(states, n, self.spec.sim)
+        tgt = None
+        if target is not None:
+            tgt = np.full((3, n), np.nan)
+            for i in idx:
+                for k, v in target.items():
+                    tgt[C.TARGET_INDEX[k], i] = v
+        if turbulence_noise is not None:
+            if len(idx) != n:
+                raise NotImplementedError("turbulence_noise for a subset of the envs")
+            self.engine.set_noise(turbulence_noise)
+        obs = self.engine.reset(mask=mask, init=init, target=tgt)
+        o = obs.cpu().numpy().astype(np.float32)
+        return [o[i] for i in idx]
+
+    def _out(self, t):
+        return t if self.return_tensors else t.cpu().numpy().astype(np.float32)
