@@ -1,0 +1,73 @@
+/*
+ * fwrollout.h -- C ABI of the rollout-side kernels in libfwsim.so: the device
+ * RolloutBuffer's GAE scan and the device VecNormalize statistics.
+ *
+ * These are the consumers directly downstream of fw_env_step in SB3's
+ * collect_rollouts.  Same conventions as fwsim.h:
+ * device pointers, `void* stream` = hipStream_t, int return codes,
+ * fw_last_error() for the message.  All buffers are row-major
+ * [n_steps][n_envs] like SB3's numpy buffers (buffer_size, n_envs).
+ *
+ * Reference interfaces replaced (paths relative to magpie/libs/stable-baselines3/):
+ *   fw_gae            RolloutBuffer.compute_returns_and_advantage
+ *                     stable_baselines3/common/buffers.py:304-333
+ *   fw_moments_*      RunningMeanStd.update (np.mean / np.var over the batch)
+ *                     stable_baselines3/common/running_mean_std.py:20-24
+ *   fw_rms_update     RunningMeanStd.update_from_moments  running_mean_std.py:26-40,
+ *                     merged over ranks (the global batch of a sharded VecEnv)
+ *   fw_vecnorm_apply  VecNormalize.step_wait's normalisation + return reset
+ *                     stable_baselines3/common/vec_env/vec_normalize.py:106-131, 133-169
+ */
+#ifndef FWROLLOUT_H
+#define FWROLLOUT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* GAE(lambda) + returns over a [n_steps][n_envs] rollout, float32 storage like SB3.
+ *   rewards, values      [n_steps][n_envs] float
+ *   episode_starts       [n_steps][n_envs] uint8   (SB3's `dones` column: done flag of the
+ *                                                   PREVIOUS step, i.e. _last_dones at add())
+ *   last_values          [n_envs] float            (value of the obs after the last step)
+ *   last_dones           [n_envs] uint8            (dones returned by the last step)
+ *   advantages, returns  [n_steps][n_envs] float   (outputs; may not alias inputs)
+ * Arithmetic reproduces numpy's promotions in the reference loop bit for bit: fp32
+ * deltas, an fp64 running advantage (the last step's 1.0 - bool promotes to float64),
+ * fp32 stores.  One lane per env, sequential in time. */
+int fw_gae(const float* rewards, const float* values, const uint8_t* episode_starts, const float* last_values,
+           const uint8_t* last_dones, int64_t n_steps, int64_t n_envs, double gamma, double gae_lambda,
+           float* advantages, float* returns, void* stream);
+
+/* Batch moments of the columns of x [n][d] (float, row stride ldx >= d) and, optionally,
+ * of the discounted return after the update ret <- ret * gamma + rew (rew may be NULL =
+ * no return column; ret is fp64 [n] and updated in place).
+ * Output (fp64, D = d + (rew != NULL)):  out[0] = n, out[1 .. D] = mean, out[1+D .. 2D] = M2
+ * (sum of squared deviations; np.var = M2 / n).  `workspace` must hold
+ * fw_moments_workspace_bytes(n, d) bytes of device memory. */
+size_t fw_moments_workspace_bytes(int64_t n, int32_t d);
+int fw_moments(const float* x, int64_t n, int32_t d, int64_t ldx, const float* rew, double* ret, double gamma,
+               void* workspace, double* out, void* stream);
+
+/* Merge `n_parts` moment records (each 1 + 2D doubles, rank order, e.g. the all-gather of
+ * fw_moments outputs) into the running statistics with RunningMeanStd.update_from_moments.
+ *   rms layout (fp64): [obs_mean d][obs_var d][obs_count][ret_mean][ret_var][ret_count]
+ * update_obs / update_ret select which RunningMeanStd objects are updated. */
+int fw_rms_update(const double* parts, int32_t n_parts, int32_t d, int32_t has_ret, double* rms, int32_t update_obs,
+                  int32_t update_ret, void* stream);
+
+/* Normalise one step: obs_out = float(clip((obs - mean) / sqrt(var + eps), +-clip_obs)),
+ * rew_out = float(clip(rew / sqrt(ret_var + eps), +-clip_rew)), then ret[done] = 0.
+ * obs_out / rew_out may be NULL (not requested); norm_obs / norm_rew = 0 copies through. */
+int fw_vecnorm_apply(const float* obs, int64_t n, int32_t d, int64_t ldx, const double* rms, double epsilon,
+                     int32_t norm_obs, double clip_obs, float* obs_out, int64_t ld_out, const float* rew,
+                     int32_t norm_rew, double clip_rew, float* rew_out, const uint8_t* done, double* ret,
+                     void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -17,12 +17,14 @@ from tum_adlr_deep_reinforcement_learning_amd.spaces import Box
 from tum_adlr_deep_reinforcement_learning_amd.vec_env import _Infos, termination_name
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "fwsim.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("fwsim.h", "fwrollout.h")]
 
 
 def _declared():
-    src = open(HEADER).read()
-    return sorted(set(re.findall(r"^int\s+(fw_\w+)\s*\(", src, re.M)))
+    names = set()
+    for h in HEADERS:
+        names |= set(re.findall(r"^(?:int|size_t)\s+(fw_\w+)\s*\(", open(h).read(), re.M))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():

@@ -1,0 +1,108 @@
+"""CPU, world_size 2 over gloo: the sharded path's collectives and bookkeeping.
+
+Covers what a sharded run exchanges: the end-of-collection rollout
+all-gather (slab layout -> global env order, SB3 swap_and_flatten order) and the
+VecNormalize moment records (rank-ordered parallel-variance merge == statistics
+of the whole batch), plus the contiguous shard split."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import rollout_oracle as R
+from tum_adlr_deep_reinforcement_learning_amd.rollout import RolloutBuffer
+from tum_adlr_deep_reinforcement_learning_amd.sharding import all_gather_flat, shard_range
+from tum_adlr_deep_reinforcement_learning_amd.spaces import Box
+
+T, N, D, A = 5, 3, 14, 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _field_values(rank):
+    """Deterministic per-rank contents: value encodes (field, t, global env, component)."""
+    g = np.arange(N) + rank * N
+    t = np.arange(T)[:, None]
+    obs = (1000 * t[..., None] + 10 * g[None, :, None] + np.arange(D)[None, None, :] * 0.01).astype(np.float32)
+    act = (-1000 * t[..., None] - 10 * g[None, :, None] - np.arange(A)[None, None, :] * 0.01).astype(np.float32)
+    sc = [(k * 1e5 + 1000 * t + 10 * g[None, :]).astype(np.float32) for k in range(1, 5)]
+    return obs, act, sc
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        buf = RolloutBuffer(T, Box(-np.inf, np.inf, (D,)), Box(-1, 1, (A,)), device="cpu", n_envs=N)
+        obs, act, sc = _field_values(rank)
+        buf.observations.copy_(torch.from_numpy(obs))
+        buf.actions.copy_(torch.from_numpy(act))
+        for view, v in zip((buf.values, buf.log_probs, buf.advantages, buf.returns), sc):
+            view.copy_(torch.from_numpy(v))
+        g = buf.all_gather()
+        flat = [f.numpy().copy() for f in g.flatten()]
+        # moment records of this rank's shard of a global batch
+        rng = np.random.RandomState(0)
+        x = rng.randn(64, D) * rng.uniform(0.5, 20, D) + 3
+        off, cnt = shard_range(64, rank, world)
+        s = x[off:off + cnt]
+        rec = torch.tensor(np.concatenate([[cnt], s.mean(0), ((s - s.mean(0)) ** 2).sum(0)]))
+        recs = all_gather_flat(rec).numpy()
+        q.put((rank, flat, recs, g.n_envs))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_rollout_gather_and_moment_merge():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    res.sort(key=lambda r: r[0])
+    # expected: the unsharded buffer over all 2N envs, flattened env-major (swap_and_flatten)
+    per = [_field_values(r) for r in range(world)]
+    full_obs = np.concatenate([p[0] for p in per], axis=1)
+    full_act = np.concatenate([p[1] for p in per], axis=1)
+    full_sc = [np.concatenate([p[2][k] for p in per], axis=1) for k in range(4)]
+    want = [R.swap_and_flatten(full_obs), R.swap_and_flatten(full_act)] + \
+           [R.swap_and_flatten(s[..., None]) for s in full_sc]
+    for rank, flat, recs, n_envs in res:
+        assert n_envs == world * N
+        for got, exp in zip(flat, want):
+            assert np.array_equal(got, exp.reshape(got.shape)), rank
+    # both ranks see identical records; the rank-ordered merge equals the whole-batch statistics
+    assert np.array_equal(res[0][2], res[1][2])
+    recs = res[0][2]
+    rng = np.random.RandomState(0)
+    x = rng.randn(64, D) * rng.uniform(0.5, 20, D) + 3
+    n, mean, m2 = R.chan_merge([(r[0], r[1:1 + D], r[1 + D:]) for r in recs])
+    assert n == 64
+    np.testing.assert_allclose(mean, x.mean(0), rtol=1e-13, atol=1e-12)
+    np.testing.assert_allclose(m2 / n, x.var(0), rtol=1e-12)
+
+
+def test_shard_range_partitions():
+    for total in (1, 7, 65536, 262144):
+        for w in (1, 2, 3, 8):
+            parts = [shard_range(total, r, w) for r in range(w)]
+            assert sum(c for _, c in parts) == total
+            assert all(parts[i][0] + parts[i][1] == parts[i + 1][0] for i in range(w - 1))

@@ -14,7 +14,9 @@ CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libfwsim.so")
 HEADER = os.path.join(ROOT, "include", "fwsim.h")
-SOURCES = [os.path.join(CSRC, "fw_kernels.hip"), os.path.join(CSRC, "fw_device.hpp"), HEADER]
+HEADERS = [HEADER, os.path.join(ROOT, "include", "fwrollout.h")]
+UNITS = [os.path.join(CSRC, "fw_kernels.hip"), os.path.join(CSRC, "fw_rollout.hip")]
+SOURCES = UNITS + [os.path.join(CSRC, "fw_device.hpp")] + HEADERS
 ARCH = os.environ.get("FWSIM_ARCH", "gfx950")
 
 _lib = None
@@ -39,15 +41,14 @@ EXTRA_FLAGS = ["-fno-slp-vectorize"]  # packed-f32 pairing costs register moves 
 
 
 def build(force=False, verbose=False, out=None, extra=None):
-    """Compile csrc/fw_kernels.hip into lib/libfwsim.so (seconds; cross-compiles without a GPU)."""
+    """Compile csrc/*.hip into lib/libfwsim.so (seconds; cross-compiles without a GPU)."""
     out = out or LIB_PATH
     if out == LIB_PATH and not force and not needs_build():
         return LIB_PATH
     os.makedirs(os.path.dirname(out), exist_ok=True)
     tmp = out + ".tmp"
     flags = EXTRA_FLAGS if extra is None else extra
-    cmd = [_hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared"] + flags + ["-o", tmp,
-           os.path.join(CSRC, "fw_kernels.hip")]
+    cmd = [_hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared"] + flags + ["-o", tmp] + UNITS
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
@@ -77,6 +78,13 @@ SIGNATURES = {
     "fw_get_state": (_c.c_int, [_vp, _i32, _vp, _vp]),
     "fw_set_state": (_c.c_int, [_vp, _i32, _vp, _vp]),
     "fw_update_config": (_c.c_int, [_vp, _vp, _vp]),
+    # include/fwrollout.h
+    "fw_gae": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _c.c_double, _c.c_double, _vp, _vp, _vp]),
+    "fw_moments_workspace_bytes": (_c.c_size_t, [_i64, _i32]),
+    "fw_moments": (_c.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _c.c_double, _vp, _vp, _vp]),
+    "fw_rms_update": (_c.c_int, [_vp, _i32, _i32, _i32, _vp, _i32, _i32, _vp]),
+    "fw_vecnorm_apply": (_c.c_int, [_vp, _i64, _i32, _i64, _vp, _c.c_double, _i32, _c.c_double, _vp, _i64, _vp, _i32,
+                                    _c.c_double, _vp, _vp, _vp, _vp]),
 }
 
 

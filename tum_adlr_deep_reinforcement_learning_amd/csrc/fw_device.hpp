@@ -1,8 +1,9 @@
 // fw_device.hpp -- per-aircraft physics + env epilogue for the fused CDNA4 kernels.
 //
-// One lane owns one aircraft for a whole env step: the 19-element ODE state,
-// the Dormand-Prince stage accumulators and the error estimate all live in
-// VGPRs; nothing but the SoA state row is read or written per step.  Every
+// One lane owns one aircraft for a whole env step: the 19-element ODE state and
+// the current stage input/derivative sit in per-lane LDS slots, the
+// Dormand-Prince accumulators and the error estimate in VGPRs; nothing but the
+// SoA state row is read or written in HBM per step.  Every
 // function is __host__ __device__ so tests/native can also exercise this exact
 // code on the CPU against the independent oracle (oracle/fw_oracle.c).
 //
@@ -22,11 +23,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "../../include/fwsim.h"
 
 #define FW_HD __host__ __device__ __forceinline__
 
 namespace fw {
+
+// records the message returned by fw_last_error (defined in fw_kernels.hip)
+int set_error(int code, const std::string& msg);
 
 constexpr int NY = FW_NY;
 constexpr double PI_D = 3.141592653589793;

@@ -5,8 +5,9 @@
 // multiple of 64, so lane i of a wave touches element i of each row: every
 // global access below is a coalesced dword (or dwordx2 for fp64) per lane.
 //
-// Kernels (one lane = one aircraft, 256-thread blocks, no LDS, no MFMA -- the
-// work is elementwise ODE integration):
+// Kernels (one lane = one aircraft, 256-thread blocks, the RK45 state and
+// stage vectors staged in LDS, no MFMA -- the work is elementwise ODE
+// integration):
 //   k_env_step   FixedWingAircraft.step + PyFly.step + masked auto-reset (hot path)
 //   k_sim_step   PyFly.step only
 //   k_reset      masked reset (sampled with Philox or injected values)
@@ -25,13 +26,18 @@
 using namespace fw;
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
-int set_err(int code, const std::string& msg) {
+// shared by every translation unit of libfwsim.so (fw_rollout.hip), read by fw_last_error
+int fw::set_error(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+
+namespace {
+
+int set_err(int code, const std::string& msg) { return fw::set_error(code, msg); }
 
 #define FW_HIP(expr)                                                                              \
   do {                                                                                            \

@@ -1,0 +1,252 @@
+"""Device-resident PPO rollout collection: RolloutBuffer + GAE kernel + RCCL all-gather.
+
+SURVEY.md 8(f) row 1 and 8(e): the consumer directly downstream of the env step.
+The reference keeps the rollout in host numpy arrays and copies every step
+through ``.cpu()`` (``OnPolicyAlgorithm.collect_rollouts``,
+stable_baselines3/common/on_policy_algorithm.py:126-190; ``RolloutBuffer``,
+stable_baselines3/common/buffers.py:259-389).  Here the buffer is one HBM slab
+per GPU, the advantage scan is the ``fw_gae`` kernel (bit-exact with the
+reference's numpy loop), and a sharded run gathers the slab with ONE
+``all_gather_into_tensor`` (RCCL over xGMI) at the end of the collection -- the
+only collective on the path.
+
+Slab layout (float32, one allocation, so the all-gather is a single call):
+    observations [T][N][D] | actions [T][N][A] | values [T][N] | log_probs [T][N]
+    | advantages [T][N] | returns [T][N]
+84 B per (step, env) for the default task (D = 14, A = 3).  Rewards and
+episode starts live outside the slab (inputs of the scan, not of the update).
+"""
+import collections
+import ctypes
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import _native
+from .sharding import all_gather_flat
+
+RolloutBufferSamples = collections.namedtuple(
+    "RolloutBufferSamples", ["observations", "actions", "old_values", "old_log_prob", "advantages", "returns"])
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _dim(space):
+    return int(np.prod(space.shape))
+
+
+def gae(rewards, values, episode_starts, last_values, last_dones, gamma, gae_lambda, advantages=None, returns=None):
+    """fw_gae on device tensors ([T][N] float32, starts / last_dones uint8); returns (advantages, returns)."""
+    T, N = rewards.shape
+    for t, dt in ((rewards, torch.float32), (values, torch.float32), (episode_starts, torch.uint8)):
+        if t.shape != (T, N) or t.dtype != dt or not t.is_contiguous() or t.device.type != "cuda":
+            raise ValueError("gae: expected contiguous [T][N] device tensors (float32 rewards/values, uint8 starts)")
+    last_values = last_values.reshape(N).to(torch.float32).contiguous()
+    last_dones = last_dones.reshape(N).to(torch.uint8).contiguous()
+    advantages = torch.empty_like(rewards) if advantages is None else advantages
+    returns = torch.empty_like(rewards) if returns is None else returns
+    lib = _native.load()
+    _native.check(lib.fw_gae(_p(rewards), _p(values), _p(episode_starts), _p(last_values), _p(last_dones), T, N,
+                             float(gamma), float(gae_lambda), _p(advantages), _p(returns), _stream(rewards.device)),
+                  "fw_gae")
+    return advantages, returns
+
+
+class RolloutBuffer:
+    """Device RolloutBuffer with SB3 0.10's API (buffers.py:259-389)."""
+
+    def __init__(self, buffer_size, observation_space, action_space, device=None, gae_lambda=1, gamma=0.99, n_envs=1):
+        self.buffer_size, self.n_envs = int(buffer_size), int(n_envs)
+        self.obs_shape = tuple(observation_space.shape)
+        self.obs_dim, self.action_dim = _dim(observation_space), _dim(action_space)
+        self.gae_lambda, self.gamma = gae_lambda, gamma
+        self.device = torch.device(device if device is not None else "cuda")
+        T, N, D, A = self.buffer_size, self.n_envs, self.obs_dim, self.action_dim
+        self.slab = torch.zeros(T * N * (D + A + 4), dtype=torch.float32, device=self.device)
+        self._bind(self.slab, T, N)
+        self.rewards = torch.zeros(T, N, dtype=torch.float32, device=self.device)
+        self.dones = torch.zeros(T, N, dtype=torch.uint8, device=self.device)  # episode starts (SB3's `dones`)
+        self.reset()
+
+    def _bind(self, slab, T, N):
+        D, A = self.obs_dim, self.action_dim
+        o = 0
+        self.observations = slab[o:o + T * N * D].view(T, N, D)
+        o += T * N * D
+        self.actions = slab[o:o + T * N * A].view(T, N, A)
+        o += T * N * A
+        self.values, self.log_probs, self.advantages, self.returns = (
+            slab[o + k * T * N:o + (k + 1) * T * N].view(T, N) for k in range(4))
+
+    def reset(self):
+        self.pos, self.full, self.generator_ready = 0, False, False
+        self.slab.zero_()
+        self.rewards.zero_()
+        self.dones.zero_()
+        self._flat = None
+
+    def size(self):
+        return self.buffer_size if self.full else self.pos
+
+    def add(self, obs, action, reward, done, value, log_prob):
+        """buffers.py:335-361: store one step for all envs (device tensors or arrays)."""
+        p = self.pos
+        dev = self.device
+        self.observations[p].copy_(torch.as_tensor(obs).reshape(self.n_envs, -1).to(dev), non_blocking=True)
+        self.actions[p].copy_(torch.as_tensor(action).reshape(self.n_envs, -1).to(dev), non_blocking=True)
+        self.rewards[p].copy_(torch.as_tensor(reward).reshape(-1).to(dev), non_blocking=True)
+        self.dones[p].copy_(torch.as_tensor(done).reshape(-1).to(dev), non_blocking=True)
+        self.values[p].copy_(value.reshape(-1), non_blocking=True)
+        self.log_probs[p].copy_(log_prob.reshape(-1), non_blocking=True)
+        self.pos += 1
+        if self.pos == self.buffer_size:
+            self.full = True
+
+    def compute_returns_and_advantage(self, last_values, dones):
+        """buffers.py:304-333 on the device (fw_gae)."""
+        lv = torch.as_tensor(last_values).to(self.device).reshape(-1)
+        ld = torch.as_tensor(np.asarray(dones) if not isinstance(dones, torch.Tensor) else dones).to(self.device)
+        gae(self.rewards, self.values.contiguous() if not self.values.is_contiguous() else self.values, self.dones,
+            lv, ld, self.gamma, self.gae_lambda, self.advantages, self.returns)
+
+    # ------------------------------------------------------------- sharding
+    def all_gather(self, group=None):
+        """Gather every rank's slab (one all_gather_into_tensor) -> GatheredRollout over W*N envs.
+        Env g = rank * N + e, i.e. the global env order of the sharded VecEnv."""
+        return GatheredRollout(list(all_gather_flat(self.slab, group)), self)
+
+    def get(self, batch_size=None, generator=None):
+        """buffers.py:363-380: minibatches over the (local) rollout, env-major flattening."""
+        return self.all_gather_local().get(batch_size, generator)
+
+    def all_gather_local(self):
+        return GatheredRollout([self.slab], self)
+
+
+class GatheredRollout:
+    """Rollout slabs of W ranks; ``get`` yields SB3 RolloutBufferSamples over all W*N envs."""
+
+    def __init__(self, slabs, like):
+        self.slabs, self.T, self.N = slabs, like.buffer_size, like.n_envs
+        self.D, self.A = like.obs_dim, like.action_dim
+        self.n_envs = len(slabs) * self.N
+        self._flat = None
+
+    def _field_views(self, slab):
+        T, N, D, A = self.T, self.N, self.D, self.A
+        o = 0
+        obs = slab[o:o + T * N * D].view(T, N, D)
+        o += T * N * D
+        act = slab[o:o + T * N * A].view(T, N, A)
+        o += T * N * A
+        rest = [slab[o + k * T * N:o + (k + 1) * T * N].view(T, N, 1) for k in range(4)]
+        return [obs, act] + rest
+
+    def flatten(self):
+        """swap_and_flatten (buffers.py:70-80) of every field over the global env axis: index g*T + t."""
+        if self._flat is None:
+            per = [self._field_views(s) for s in self.slabs]
+            self._flat = [torch.cat([p[k] for p in per], dim=1).transpose(0, 1).reshape(self.n_envs * self.T, -1)
+                          for k in range(6)]
+        return self._flat
+
+    def get(self, batch_size=None, generator=None, indices=None):
+        obs, act, val, logp, adv, ret = self.flatten()
+        total = self.n_envs * self.T
+        if indices is None:
+            indices = torch.randperm(total, device=obs.device, generator=generator)
+        batch_size = total if batch_size is None else batch_size
+        for s in range(0, total, batch_size):
+            idx = indices[s:s + batch_size]
+            yield RolloutBufferSamples(obs[idx], act[idx], val[idx].flatten(), logp[idx].flatten(),
+                                       adv[idx].flatten(), ret[idx].flatten())
+
+
+# ---------------------------------------------------------------------------
+# policy (the caller of the path; SB3 PPO MlpPolicy defaults, policies.py ActorCriticPolicy)
+# ---------------------------------------------------------------------------
+class MlpActorCritic(nn.Module):
+    """SB3 0.10 PPO ``MlpPolicy`` defaults: separate pi/vf MLPs [64, 64] with tanh, orthogonal
+    init (gains sqrt(2), 0.01 for the action head, 1 for the value head), state-independent
+    log-std initialised to 0, diagonal Gaussian actions."""
+
+    def __init__(self, obs_dim, act_dim, hidden=(64, 64), log_std_init=0.0):
+        super().__init__()
+
+        def mlp():
+            layers, d = [], obs_dim
+            for h in hidden:
+                layers += [nn.Linear(d, h), nn.Tanh()]
+                d = h
+            return nn.Sequential(*layers)
+
+        self.pi, self.vf = mlp(), mlp()
+        self.action_net = nn.Linear(hidden[-1], act_dim)
+        self.value_net = nn.Linear(hidden[-1], 1)
+        self.log_std = nn.Parameter(torch.full((act_dim,), float(log_std_init)))
+        for m, g in ((self.pi, np.sqrt(2)), (self.vf, np.sqrt(2)), (self.action_net, 0.01), (self.value_net, 1.0)):
+            for layer in m.modules() if isinstance(m, nn.Sequential) else [m]:
+                if isinstance(layer, nn.Linear):
+                    nn.init.orthogonal_(layer.weight, gain=g)
+                    nn.init.zeros_(layer.bias)
+
+    def forward(self, obs, deterministic=False):
+        mean = self.action_net(self.pi(obs))
+        values = self.value_net(self.vf(obs))
+        std = self.log_std.exp()
+        actions = mean if deterministic else mean + std * torch.randn_like(mean)
+        log_prob = (-((actions - mean) ** 2) / (2 * std * std) - self.log_std - 0.5 * np.log(2 * np.pi)).sum(-1)
+        return actions, values, log_prob
+
+    def predict_values(self, obs):
+        return self.value_net(self.vf(obs))
+
+
+class RolloutCollector:
+    """OnPolicyAlgorithm.collect_rollouts (on_policy_algorithm.py:126-190) with everything on the device.
+
+    ``env`` is a FixedWingVecEnv (or a VecNormalize-style wrapper around one) built with
+    ``return_tensors=True``.  Per step: copy the last observation into the buffer slot, run the
+    policy on it, clip the actions to the action space, step the env, store reward / episode start /
+    value / log-prob.  No host synchronisation inside the loop."""
+
+    def __init__(self, env, policy, buffer):
+        self.env, self.policy, self.buffer = env, policy, buffer
+        dev = buffer.device
+        space = env.action_space
+        self.low = torch.as_tensor(space.low, device=dev)
+        self.high = torch.as_tensor(space.high, device=dev)
+        self.last_obs = None
+        self.last_dones = torch.zeros(env.num_envs, dtype=torch.uint8, device=dev)
+
+    @torch.no_grad()
+    def collect(self, n_rollout_steps=None):
+        buf, env = self.buffer, self.env
+        n = n_rollout_steps or buf.buffer_size
+        if self.last_obs is None:
+            self.last_obs = env.reset()
+        buf.reset()
+        for t in range(n):
+            obs_slot = buf.observations[t]
+            obs_slot.copy_(self.last_obs)
+            actions, values, log_probs = self.policy(obs_slot)
+            clipped = torch.max(torch.min(actions, self.high), self.low)
+            new_obs, rewards, dones, _ = env.step(clipped)
+            buf.actions[t].copy_(actions)
+            buf.rewards[t].copy_(rewards)
+            buf.dones[t].copy_(self.last_dones)
+            buf.values[t].copy_(values.reshape(-1))
+            buf.log_probs[t].copy_(log_probs)
+            self.last_obs = new_obs
+            self.last_dones = dones.to(torch.uint8).clone()
+        buf.pos, buf.full = n, n == buf.buffer_size
+        last_values = self.policy.predict_values(self.last_obs)
+        buf.compute_returns_and_advantage(last_values, self.last_dones)
+        return buf

@@ -1,0 +1,202 @@
+"""Device VecNormalize: SB3 0.10's normalising wrapper with its statistics in HBM.
+
+Mirrors ``VecNormalize`` (stable_baselines3/common/vec_env/vec_normalize.py:13-260)
+and ``RunningMeanStd`` (common/running_mean_std.py:6-40): same constructor
+arguments, same ``reset`` / ``step_wait`` order of updates (obs statistics, obs
+normalisation, discounted-return update, return statistics, reward
+normalisation, ``ret[news] = 0``), same ``obs_rms`` / ``ret_rms`` attributes.
+Per step it runs ``fw_moments`` (batch mean / M2, fp64) -> ``fw_rms_update``
+(update_from_moments) -> ``fw_vecnorm_apply`` on the device: no host sync.
+
+Sharded runs (one process per GPU, each owning a slice of the envs): the
+statistics must be those of the GLOBAL batch, as with one VecNormalize over all
+envs.  Each rank's moment record (n, mean, M2: 1 + 2D doubles) is all-gathered
+over RCCL and every rank merges the records in rank order (parallel-variance
+formula), so all ranks hold bit-identical statistics.  That is ~250 B per rank
+per step: latency-bound (~10-20 us on xGMI); ``sync_every`` > 1 trades exactness
+for fewer collectives (default 1 = the reference's semantics).
+
+Persistence: ``save`` / ``load`` write the statistics as ``.npz`` (the reference
+pickles the whole wrapper; pickles are not produced or read here).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native
+from .sharding import all_gather_flat
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class _RMSView:
+    """Read-only RunningMeanStd-like view (mean / var / count as numpy, copied on access)."""
+
+    def __init__(self, owner, which):
+        self._o, self._w = owner, which
+
+    def _s(self):
+        return self._o.rms.cpu().numpy()
+
+    @property
+    def mean(self):
+        s, d = self._s(), self._o.obs_dim
+        return s[:d].copy() if self._w == "obs" else float(s[2 * d + 1])
+
+    @property
+    def var(self):
+        s, d = self._s(), self._o.obs_dim
+        return s[d:2 * d].copy() if self._w == "obs" else float(s[2 * d + 2])
+
+    @property
+    def count(self):
+        s, d = self._s(), self._o.obs_dim
+        return float(s[2 * d]) if self._w == "obs" else float(s[2 * d + 3])
+
+
+class VecNormalize:
+    def __init__(self, venv, training=True, norm_obs=True, norm_reward=True, clip_obs=10.0, clip_reward=10.0,
+                 gamma=0.99, epsilon=1e-8, group=None, return_tensors=None):
+        self.venv = venv
+        self.num_envs = venv.num_envs
+        self.observation_space, self.action_space = venv.observation_space, venv.action_space
+        self.training, self.norm_obs, self.norm_reward = training, norm_obs, norm_reward
+        self.clip_obs, self.clip_reward, self.gamma, self.epsilon = clip_obs, clip_reward, gamma, epsilon
+        self.group = group
+        self.return_tensors = getattr(venv, "return_tensors", False) if return_tensors is None else return_tensors
+        venv.return_tensors = True  # the wrapped device env hands over device tensors
+        self.device = venv.device
+        self.obs_dim = int(np.prod(self.observation_space.shape))
+        d, n, dev = self.obs_dim, self.num_envs, self.device
+        rms = np.zeros(2 * d + 4)
+        rms[d:2 * d] = 1.0            # var = 1, count = epsilon 1e-4 (running_mean_std.py:14-16)
+        rms[2 * d] = 1e-4
+        rms[2 * d + 2] = 1.0
+        rms[2 * d + 3] = 1e-4
+        self.rms = torch.tensor(rms, dtype=torch.float64, device=dev)
+        self.ret = torch.zeros(n, dtype=torch.float64, device=dev)
+        self.lib = _native.load()
+        self._ws = torch.empty(int(self.lib.fw_moments_workspace_bytes(n, d)), dtype=torch.uint8, device=dev)
+        self._rec = torch.empty(1 + 2 * (d + 1), dtype=torch.float64, device=dev)
+        self._rec_ret = torch.empty(3, dtype=torch.float64, device=dev)
+        self._zero_rew = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.obs_out = torch.empty(n, d, dtype=torch.float32, device=dev)
+        self.rew_out = torch.empty(n, dtype=torch.float32, device=dev)
+        self.old_obs = None
+        self.old_reward = None
+        self.obs_rms = _RMSView(self, "obs")
+        self.ret_rms = _RMSView(self, "ret")
+
+    # --------------------------------------------------------------- internals
+    def _s(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _gather(self, rec):
+        """Rank-ordered moment records of the global batch ([W][len])."""
+        out = all_gather_flat(rec, self.group)
+        return out, out.shape[0]
+
+    def _update(self, obs, rew):
+        """obs_rms.update(obs) and ret = ret*gamma + rew; ret_rms.update(ret)  (training only)."""
+        d, n = self.obs_dim, self.num_envs
+        L = self.lib
+        s = self._s()
+        if obs is not None:
+            _native.check(L.fw_moments(_p(obs), n, d, d, _p(rew), _p(self.ret), float(self.gamma), _p(self._ws),
+                                       _p(self._rec), s), "fw_moments")
+            parts, W = self._gather(self._rec)
+            _native.check(L.fw_rms_update(_p(parts), W, d, 1, _p(self.rms), 1, 1, s), "fw_rms_update")
+        else:  # return statistics only (reset)
+            _native.check(L.fw_moments(None, n, 0, 0, _p(rew), _p(self.ret), float(self.gamma), _p(self._ws),
+                                       _p(self._rec_ret), s), "fw_moments")
+            parts, W = self._gather(self._rec_ret)
+            # a [1+2*1] record has the layout of a d=0 record with a return column
+            self._ret_only_update(parts, W)
+
+    def _ret_only_update(self, parts, W):
+        d = self.obs_dim
+        tmp = torch.cat([self.rms[2 * d:2 * d + 1], self.rms[2 * d + 1:]])  # [obs_count, ret_mean, ret_var, ret_count]
+        _native.check(self.lib.fw_rms_update(_p(parts), W, 0, 1, _p(tmp), 0, 1, self._s()), "fw_rms_update")
+        self.rms[2 * d + 1:].copy_(tmp[1:])
+
+    def _apply(self, obs, rew, done, obs_out=None):
+        d, n = self.obs_dim, self.num_envs
+        obs_out = self.obs_out if obs_out is None else obs_out
+        _native.check(self.lib.fw_vecnorm_apply(_p(obs), n, d, d, _p(self.rms), float(self.epsilon),
+                                                int(self.norm_obs), float(self.clip_obs),
+                                                _p(obs_out) if obs is not None else None, d, _p(rew),
+                                                int(self.norm_reward), float(self.clip_reward),
+                                                _p(self.rew_out) if rew is not None else None, _p(done),
+                                                _p(self.ret), self._s()), "fw_vecnorm_apply")
+
+    def _out(self, t):
+        return t if self.return_tensors else t.cpu().numpy()
+
+    # --------------------------------------------------------------- VecEnv API
+    def reset(self):
+        """vec_normalize.py:209-220."""
+        obs = self.venv.reset()
+        obs = obs if isinstance(obs, torch.Tensor) else torch.as_tensor(obs, device=self.device)
+        obs = obs.to(torch.float32).contiguous()
+        self.old_obs = obs
+        self.ret.zero_()
+        if self.training:
+            self._update(None, self._zero_rew)
+        self._apply(obs, None, None)
+        return self._out(self.obs_out)
+
+    def step_async(self, actions):
+        self.venv.step_async(actions)
+
+    def step_wait(self):
+        """vec_normalize.py:106-131."""
+        obs, rews, news, infos = self.venv.step_wait()
+        obs = obs.to(torch.float32).contiguous()
+        rews = rews.to(torch.float32).contiguous()
+        self.old_obs, self.old_reward = obs, rews
+        done_u8 = news.to(torch.uint8).contiguous()
+        if self.training:
+            self._update(obs, rews)
+        self._apply(obs, rews, done_u8)
+        if self.return_tensors:
+            return self.obs_out, self.rew_out, news, infos
+        return self.obs_out.cpu().numpy(), self.rew_out.cpu().numpy().astype(np.float64), \
+            news.cpu().numpy().astype(bool), infos
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def normalize_obs(self, obs):
+        o = torch.as_tensor(obs, dtype=torch.float32, device=self.device).reshape(self.num_envs, -1).contiguous()
+        out = torch.empty_like(o)
+        self._apply(o, None, None, obs_out=out)
+        return self._out(out)
+
+    def get_original_obs(self):
+        return self._out(self.old_obs)
+
+    def get_original_reward(self):
+        return self._out(self.old_reward)
+
+    def close(self):
+        self.venv.close()
+
+    def __getattr__(self, name):  # env_method / get_attr / set_attr / seed ... pass through
+        if name in ("venv",):
+            raise AttributeError(name)
+        return getattr(self.venv, name)
+
+    def save(self, path):
+        np.savez(path, rms=self.rms.cpu().numpy(), obs_dim=self.obs_dim, gamma=self.gamma, epsilon=self.epsilon,
+                 clip_obs=self.clip_obs, clip_reward=self.clip_reward, norm_obs=self.norm_obs,
+                 norm_reward=self.norm_reward)
+
+    def load_stats(self, path):
+        with np.load(path, allow_pickle=False) as z:
+            if int(z["obs_dim"]) != self.obs_dim:
+                raise ValueError("observation size mismatch")
+            self.rms.copy_(torch.as_tensor(z["rms"]))
