@@ -87,6 +87,59 @@ def cpu_baseline(seconds=12.0):
                       "on 1 host core in %.1f s" % (steps, dt)}
 
 
+def rollout_leg(spec, n, T, dev, rank, world, precision):
+    """BASELINE configs[2]/[3]: one PPO collect_rollouts of T steps on the device (policy forward,
+    VecNormalize with global statistics, env step, buffer writes, GAE kernel) plus, when sharded, the
+    RCCL all-gather of the rollout slab.  Returns timings of rank-local phases (max over ranks)."""
+    from tum_adlr_deep_reinforcement_learning_amd.rollout import MlpActorCritic, RolloutBuffer, RolloutCollector
+    from tum_adlr_deep_reinforcement_learning_amd.vec_env import FixedWingVecEnv
+    from tum_adlr_deep_reinforcement_learning_amd.vec_normalize import VecNormalize
+    torch.manual_seed(rank)
+    venv = FixedWingVecEnv(n, sim_config_kw={"turbulence": False}, device=dev, precision=precision, seed=1234,
+                           env_offset=rank * n, return_tensors=True, info_target=False)
+    env = VecNormalize(venv)
+    policy = MlpActorCritic(env.observation_space.shape[0], env.action_space.shape[0]).to(dev)
+    buf = RolloutBuffer(T, env.observation_space, env.action_space, device=dev, gae_lambda=0.95, gamma=0.99, n_envs=n)
+    col = RolloutCollector(env, policy, buf)
+    col.collect(min(T, 16))  # warm-up (kernels, allocator, RCCL communicator)
+    buf.all_gather()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    col.collect()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    gathered = buf.all_gather()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t2 = time.perf_counter()
+    # GAE kernel alone, timed with events on its stream (same inputs again)
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    lv = torch.zeros(n, device=dev)
+    e0.record(stream)
+    for _ in range(5):
+        buf.compute_returns_and_advantage(lv, col.last_dones)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    gae_ms = e0.elapsed_time(e1) / 5
+    t = torch.tensor([t1 - t0, t2 - t1, t2 - t0, gae_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    collect_s, gather_s, total_s, gae_ms = [float(x) for x in t]
+    gae_bytes = (4 + 4 + 1 + 4 + 4) * T * n + (4 + 1) * n
+    out = {"horizon": T, "envs_per_gpu": n, "global_envs": n * world, "collect_s": collect_s,
+           "allgather_s": gather_s if world > 1 else 0.0, "env_steps_per_s": n * world * T / total_s,
+           "gathered_bytes_per_gpu": sum(s.numel() * 4 for s in gathered.slabs),
+           "gae_kernel": {"ms": gae_ms, "bytes": gae_bytes, "achieved_GBs": gae_bytes / (gae_ms * 1e-3) / 1e9,
+                          "frac_of_hbm_peak": gae_bytes / (gae_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}}
+    del gathered
+    venv.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -97,6 +150,8 @@ def main():
     ap.add_argument("--turbulence", action="store_true", help="light Dryden turbulence + random steady wind")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--rollout-steps", type=int, default=0,
+                    help="also run one PPO collect_rollouts of this horizon (2048 = BASELINE configs[2]/[3])")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -158,6 +213,11 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    rollout = None
+    if args.rollout_steps > 0:
+        eng.close()
+        rollout = rollout_leg(spec, n, args.rollout_steps, dev, rank, world, args.precision)
+
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -186,6 +246,8 @@ def main():
                          "algorithmic_bytes_per_env_step": rd + wr, "kernel_ms": kern_ms},
             "cpu_baseline": cpu,
         }
+        if rollout is not None:
+            out["rollout"] = rollout
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

@@ -239,3 +239,36 @@ def test_full_size_properties_fp32():
     half = n // 2
     tot_b, _, ode_b = run(3, offset=half, count=n - half)  # shard = the second half of the same batch
     assert torch.equal(tot_b, tot[half:]) and torch.equal(ode_b, ode[:, half:])
+
+
+@pytest.mark.parametrize("precision", ["float64", "float32"])
+def test_generic_and_specialised_kernels_agree(precision, monkeypatch):
+    """The structure-specialised kernel (GymX8Cfg) and the generic DevCfg kernel compute the same step.
+    Not bitwise: the compiler contracts multiply-adds differently in the two instances, so fp64 agrees to
+    ~1e-12 and fp32 to ~1e-6 (both far inside the oracle tolerances above)."""
+    spec = C.EnvSpec(config_kw={"steps_max": 60}, sim_config_kw={"turbulence": False})
+    n = 1024
+
+    def run(generic):
+        if generic:
+            monkeypatch.setenv("FWSIM_GENERIC", "1")
+        else:
+            monkeypatch.delenv("FWSIM_GENERIC", raising=False)
+        eng = _engine(spec.sim, spec, n, precision)
+        eng.seed(9)
+        eng.reset()
+        g = torch.Generator(device="cuda:0")
+        g.manual_seed(3)
+        out = []
+        for _ in range(80 if precision == "float64" else 10):  # fp32 trajectories decorrelate after flips
+            a = torch.rand(n, 3, generator=g, device="cuda:0", dtype=eng.dtype) * 2.4 - 1.2
+            o, r, d, t = eng.env_step(a, stats=True)
+            out.append((o.clone(), r.clone(), d.clone(), t.clone(), eng.stats.clone()))
+        eng.close()
+        return out
+
+    a, b = run(False), run(True)
+    tol = 1e-9 if precision == "float64" else 1e-4
+    for (o1, r1, d1, t1, s1), (o2, r2, d2, t2, s2) in zip(a, b):
+        assert torch.equal(d1, d2) and torch.equal(t1, t2)
+        assert torch.allclose(o1, o2, rtol=tol, atol=tol) and torch.allclose(r1, r2, rtol=tol, atol=tol)

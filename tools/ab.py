@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""A/B kernel variants.
+
+  python tools/ab.py build NAME [hipcc flags...]   (CPU) -> tools/_build/variants/NAME.so
+  python tools/ab.py run [NAME ...]                (GPU) tail fit per variant via FWSIM_LIB
+
+Each variant is the full libfwsim.so compiled with extra -D flags; ``run``
+executes tools/tail.py in a fresh process per variant (FWSIM_LIB selects it)
+and prints one JSON line per variant.
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VDIR = os.path.join(ROOT, "tools", "_build", "variants")
+sys.path.insert(0, ROOT)
+
+
+def build(name, flags):
+    from tum_adlr_deep_reinforcement_learning_amd import _native
+    os.makedirs(VDIR, exist_ok=True)
+    out = os.path.join(VDIR, name + ".so")
+    _native.build(force=True, out=out, extra=_native.EXTRA_FLAGS + list(flags))
+    print("built", out)
+
+
+def run(names):
+    names = names or sorted(f[:-3] for f in os.listdir(VDIR) if f.endswith(".so"))
+    for nm in names:
+        env = dict(os.environ, FWSIM_LIB=os.path.join(VDIR, nm + ".so"))
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "tail.py")], env=env, capture_output=True,
+                           text=True, timeout=400)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not line:
+            print(json.dumps({"variant": nm, "rc": r.returncode, "err": r.stderr[-2000:]}))
+            if r.returncode < 0 or r.returncode > 1:
+                sys.exit(r.returncode if r.returncode > 0 else 1)
+            continue
+        d = json.loads(line[0])
+        print(json.dumps({"variant": nm, "us_per_iter": round(d["fit_us_per_iteration"], 4),
+                          "ms_mean": round(d["ms_mean"], 4), "ms_p50": round(d["ms_p50"], 4),
+                          "intercept_ms": round(d["fit_ms_intercept"], 4), "max_nfev_p50": d["max_nfev_p50"]}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "build":
+        build(sys.argv[2], sys.argv[3:])
+    else:
+        run(sys.argv[2:])

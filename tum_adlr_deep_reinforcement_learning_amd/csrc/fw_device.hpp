@@ -36,7 +36,10 @@ int set_error(int code, const std::string& msg);
 
 constexpr int NY = FW_NY;
 constexpr double PI_D = 3.141592653589793;
-constexpr int MAX_NFEV = 6000;  // RHS evaluations per step before the step is declared a solver failure
+constexpr int MAX_NFEV = 6000;
+#ifndef FW_RELAUNDER
+#define FW_RELAUNDER 1  // re-issue config scalar loads per RHS instead of pinning ~100 constants in SGPRs (spills)
+#endif  // RHS evaluations per step before the step is declared a solver failure
 
 template <typename T>
 struct Lim {
@@ -88,13 +91,40 @@ struct DevCfg {
   fw_rew_factor rew[FW_MAX_REW];
 };
 
+// Compile-time specialisations of a configuration's STRUCTURE (which variables
+// carry constraints / clips / wraps, which actuators have a rate limit, elevon
+// mixing, trig flags).  The values stay in DevCfg (runtime); a SpecCfg view
+// hides the structural fields with constants of the same name, so cond() and
+// the RHS compile to straight-line code containing only the checks this
+// configuration has.  The host picks the instance whose structure equals the
+// runtime one (fw_kernels.hip: spec_of), else the generic DevCfg instance.
+template <typename T, uint32_t CM, uint32_t CLM, uint32_t WM, uint32_t DM, int ELEVON, int TA, int TB, int EE>
+struct SpecCfg : DevCfg<T> {
+  static constexpr uint32_t cmask = CM, clipmask = CLM, wrapmask = WM, dotmask = DM;
+  static constexpr int elevon = ELEVON, trig_alpha = TA, trig_beta = TB, euler_exact = EE;
+};
+// fixed_wing_config.json (gym): omega +-720 deg/s and Va <= 70 constrained; Va, actuators,
+// elevator / aileron / throttle clipped; roll / yaw wrapped; elevon rate limits
+template <typename T>
+using GymX8Cfg = SpecCfg<T, 0x1038u, 0x1F9000u, 0x5u, 0x3u, 1, 0, 0, 0>;
+// pyfly_config.json: as above without the Va constraint
+template <typename T>
+using PyflyX8Cfg = SpecCfg<T, 0x38u, 0x1F9000u, 0x5u, 0x3u, 1, 0, 0, 0>;
+
 // Re-materialise the (wave-uniform) config pointer so the scalar loads of the
 // ~90 aircraft constants are issued where they are used instead of being
 // hoisted out of the RK loop and pinned in SGPRs (which spills them into VGPR
 // lanes).  s_load from the scalar cache costs nothing next to the VALU work.
-template <typename T>
-FW_HD const DevCfg<T>& relaunder(const DevCfg<T>& c) {
+template <typename C>
+FW_HD const C& relaunder(const C& c) {
+#if defined(__HIP_DEVICE_COMPILE__) && FW_RELAUNDER
+  using CPtr = const __attribute__((address_space(4))) C*;
+  CPtr q = (CPtr)(&c);
+  asm volatile("" : "+s"(q));
+  return *(const C*)q;
+#else
   return c;
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -162,11 +192,12 @@ FW_HD T clipv(T x, T lo, T hi) {  // np.clip semantics (NaN propagates)
 }
 
 // Variable.apply_conditions (pyfly.py:114-133).  Records the first violation.
-template <typename T>
-FW_HD T cond(const DevCfg<T>& c, int v, T x, int& term) {
+template <typename T, typename C>
+FW_HD T cond(const C& c, int v, T x, int& term) {
   const uint32_t bit = 1u << v;
-  if (c.cmask & bit) {
-    if (!term && (x < c.lim[v].cmin || x > c.lim[v].cmax)) term = FW_TERM_VAR(v);
+  if (c.cmask & bit) {  // branch-free: first violation wins
+    const bool viol = (x < c.lim[v].cmin) | (x > c.lim[v].cmax);
+    term = (term == 0 && viol) ? FW_TERM_VAR(v) : term;
   }
   if (c.clipmask & bit) x = clipv(x, c.lim[v].vmin, c.lim[v].vmax);
   if (c.wrapmask & bit) {
@@ -260,9 +291,9 @@ FW_HD void airspeed_vec_euler(T phi, T th, T psi, const T* w, const T* tl, const
 // conditioned first (_set_states_from_ode_solution(save=False)), which can
 // terminate the step.  Returns the first violated condition (0 = none).
 // ---------------------------------------------------------------------------
-template <typename T>
-FW_HD int rhs(const DevCfg<T>& c0, const StepCtx<T>& X, bool first, const T* y, T* dy) {
-  const DevCfg<T>& c = relaunder(c0);
+template <typename T, typename C>
+FW_HD int rhs(const C& c0, const StepCtx<T>& X, bool first, const T* y, T* dy) {
+  const C& c = relaunder(c0);
   int term = 0;
   T om[3] = {y[4], y[5], y[6]};
   T vel[3] = {y[10], y[11], y[12]};
@@ -423,8 +454,8 @@ FW_HD int rhs(const DevCfg<T>& c0, const StepCtx<T>& X, bool first, const T* y, 
 // K_j for the stages to come, YB = sum_j B_j K_j, ER = sum_j E_j K_j); per
 // element the sums run j = 0, 1, ... as scipy's np.dot(K[:s].T, a[:s])
 // (rk.py:58-64).
-template <typename T>
-FW_HD int rk45(const DevCfg<T>& c, const StepCtx<T>& X, T* y_io, T* __restrict__ sy, T* __restrict__ sf, int stride,
+template <typename T, typename C>
+FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, T* __restrict__ sy, T* __restrict__ sf, int stride,
                int& nfev, int& nacc) {
   constexpr double A10 = 1.0 / 5;
   constexpr double A20 = 3.0 / 40, A21 = 9.0 / 40;
@@ -456,129 +487,121 @@ FW_HD int rk45(const DevCfg<T>& c, const StepCtx<T>& X, T* y_io, T* __restrict__
   nfev = 0;
   nacc = 0;
 
-  // stage: 0 = f0, 1 = probe, 2..7 = RK stage s = stage - 1 (s = 6: f(t_new, y_new))
+  // stage: 0 = f0, 1 = probe, 2..7 = RK stage s = stage - 1 (s = 6: f(t_new, y_new)).
+  // The RHS and the stage folds run on EVERY lane (finished lanes compute on
+  // dead data): only the writes that define a lane's result (Y/F on accept,
+  // result, counters) are predicated.  Unpredicated folds keep the stage
+  // arrays in place across the wave-uniform stage switch (no phi copies).
   for (int stage = 0;;) {
     if (!any_lane(active)) break;
-    if (active) {
-      nfev++;
+    {
       const int term = rhs(c, X, stage == 0, ys, K);
-      if (term) {
-        result = term;
-        active = false;
-      }
-      // hard bound on work per step so that no input can keep a wave spinning:
-      // scipy's own TOO_SMALL_STEP exit needs < 2100 evaluations from any h <= dt
-      if (nfev >= MAX_NFEV) {
-        result = -1;
-        active = false;
+      if (active) {
+        nfev++;
+        if (term) {
+          result = term;
+          active = false;
+        }
+        // hard bound on work per step so that no input can keep a wave spinning:
+        // scipy's own TOO_SMALL_STEP exit needs < 2100 evaluations from any h <= dt
+        if (nfev >= MAX_NFEV) {
+          result = -1;
+          active = false;
+        }
       }
     }
     bool begin_step = false, begin_attempt = false;
     if (stage == 0) {  // ---- f0; select_initial_step (common.py:68-110)
-      if (active) {
-        T d0s = T(0), d1s = T(0);
+      T d0s = T(0), d1s = T(0);
 #pragma unroll
-        for (int i = 0; i < NY; i++) {
-          F(i) = K[i];
-          const T isc = frcp(atol + fabs(Y(i)) * rtol);
-          const T a = Y(i) * isc, b = K[i] * isc;
-          d0s += a * a;
-          d1s += b * b;
-        }
-        const T d0 = fsqrt(d0s) * inv_sqrt_n;
-        d1 = fsqrt(d1s) * inv_sqrt_n;
-        h0 = (d0 < T(1e-5) || d1 < T(1e-5)) ? 1e-6 : 0.01 * (double)d0 / (double)d1;
-        if (h0 > t_bound) h0 = t_bound;
-        const T h0t = (T)h0;
-#pragma unroll
-        for (int i = 0; i < NY; i++) ys[i] = Y(i) + h0t * F(i);
+      for (int i = 0; i < NY; i++) {
+        F(i) = K[i];
+        const T isc = frcp(atol + fabs(Y(i)) * rtol);
+        const T a = Y(i) * isc, b = K[i] * isc;
+        d0s += a * a;
+        d1s += b * b;
       }
+      const T d0 = fsqrt(d0s) * inv_sqrt_n;
+      d1 = fsqrt(d1s) * inv_sqrt_n;
+      h0 = (d0 < T(1e-5) || d1 < T(1e-5)) ? 1e-6 : 0.01 * (double)d0 / (double)d1;
+      if (h0 > t_bound) h0 = t_bound;
+      const T h0t = (T)h0;
+#pragma unroll
+      for (int i = 0; i < NY; i++) ys[i] = Y(i) + h0t * F(i);
       stage = 1;
     } else if (stage == 1) {  // ---- probe; select_initial_step (common.py:111-134)
-      if (active) {
-        T d2s = T(0);
+      T d2s = T(0);
 #pragma unroll
-        for (int i = 0; i < NY; i++) {
-          const T a = (K[i] - F(i)) * frcp(atol + fabs(Y(i)) * rtol);
-          d2s += a * a;
-        }
-        const double d2 = (double)(fsqrt(d2s) * inv_sqrt_n) / h0;
-        double h1;
-        if ((double)d1 <= 1e-15 && d2 <= 1e-15) h1 = fmax(1e-6, h0 * 1e-3);
-        else h1 = pow(0.01 / fmax((double)d1, d2), 1.0 / 5.0);
-        h_abs = fmin(fmin(100 * h0, h1), t_bound);
-        begin_step = true;
+      for (int i = 0; i < NY; i++) {
+        const T a = (K[i] - F(i)) * frcp(atol + fabs(Y(i)) * rtol);
+        d2s += a * a;
       }
+      const double d2 = (double)(fsqrt(d2s) * inv_sqrt_n) / h0;
+      double h1;
+      if ((double)d1 <= 1e-15 && d2 <= 1e-15) h1 = fmax(1e-6, h0 * 1e-3);
+      else h1 = pow(0.01 / fmax((double)d1, d2), 1.0 / 5.0);
+      h_abs = fmin(fmin(100 * h0, h1), t_bound);
+      begin_step = active;
       stage = 2;
     } else if (stage == 2) {  // K = K1
-      if (active) {
 #pragma unroll
-        for (int i = 0; i < NY; i++) {
-          ys[i] = Y(i) + (F(i) * T(A20) + K[i] * T(A21)) * ht;
-          P3[i] = F(i) * T(A30) + K[i] * T(A31);
-          P4[i] = F(i) * T(A40) + K[i] * T(A41);
-          P5[i] = F(i) * T(A50) + K[i] * T(A51);
-          YB[i] = F(i) * T(B0);
-          ER[i] = F(i) * T(E0);
-        }
+      for (int i = 0; i < NY; i++) {
+        ys[i] = Y(i) + (F(i) * T(A20) + K[i] * T(A21)) * ht;
+        P3[i] = F(i) * T(A30) + K[i] * T(A31);
+        P4[i] = F(i) * T(A40) + K[i] * T(A41);
+        P5[i] = F(i) * T(A50) + K[i] * T(A51);
+        YB[i] = F(i) * T(B0);
+        ER[i] = F(i) * T(E0);
       }
       stage = 3;
     } else if (stage == 3) {  // K = K2
-      if (active) {
 #pragma unroll
-        for (int i = 0; i < NY; i++) {
-          P3[i] += K[i] * T(A32);
-          P4[i] += K[i] * T(A42);
-          P5[i] += K[i] * T(A52);
-          YB[i] += K[i] * T(B2);
-          ER[i] += K[i] * T(E2);
-          ys[i] = Y(i) + P3[i] * ht;
-        }
+      for (int i = 0; i < NY; i++) {
+        P3[i] += K[i] * T(A32);
+        P4[i] += K[i] * T(A42);
+        P5[i] += K[i] * T(A52);
+        YB[i] += K[i] * T(B2);
+        ER[i] += K[i] * T(E2);
+        ys[i] = Y(i) + P3[i] * ht;
       }
       stage = 4;
     } else if (stage == 4) {  // K = K3
-      if (active) {
 #pragma unroll
-        for (int i = 0; i < NY; i++) {
-          P4[i] += K[i] * T(A43);
-          P5[i] += K[i] * T(A53);
-          YB[i] += K[i] * T(B3);
-          ER[i] += K[i] * T(E3);
-          ys[i] = Y(i) + P4[i] * ht;
-        }
+      for (int i = 0; i < NY; i++) {
+        P4[i] += K[i] * T(A43);
+        P5[i] += K[i] * T(A53);
+        YB[i] += K[i] * T(B3);
+        ER[i] += K[i] * T(E3);
+        ys[i] = Y(i) + P4[i] * ht;
       }
       stage = 5;
     } else if (stage == 5) {  // K = K4
-      if (active) {
 #pragma unroll
-        for (int i = 0; i < NY; i++) {
-          P5[i] += K[i] * T(A54);
-          YB[i] += K[i] * T(B4);
-          ER[i] += K[i] * T(E4);
-          ys[i] = Y(i) + P5[i] * ht;
-        }
+      for (int i = 0; i < NY; i++) {
+        P5[i] += K[i] * T(A54);
+        YB[i] += K[i] * T(B4);
+        ER[i] += K[i] * T(E4);
+        ys[i] = Y(i) + P5[i] * ht;
       }
       stage = 6;
     } else if (stage == 6) {  // K = K5; ys <- y_new
-      if (active) {
 #pragma unroll
-        for (int i = 0; i < NY; i++) {
-          YB[i] += K[i] * T(B5);
-          ER[i] += K[i] * T(E5);
-          ys[i] = Y(i) + ht * YB[i];
-        }
+      for (int i = 0; i < NY; i++) {
+        YB[i] += K[i] * T(B5);
+        ER[i] += K[i] * T(E5);
+        ys[i] = Y(i) + ht * YB[i];
       }
       stage = 7;
     } else {  // K = f(t_new, y_new): error norm + step control (rk.py:138-173)
-      if (active) {
-        T es = T(0);
+      T es = T(0);
 #pragma unroll
-        for (int i = 0; i < NY; i++) {
-          const T e = (ER[i] + K[i] * T(E6)) * ht;
-          const T q = e * frcp(atol + fmax(fabs(Y(i)), fabs(ys[i])) * rtol);
-          es += q * q;
-        }
-        const T en = fsqrt(es) * inv_sqrt_n;
+      for (int i = 0; i < NY; i++) {
+        const T e = (ER[i] + K[i] * T(E6)) * ht;
+        const T q = e * frcp(atol + fmax(fabs(Y(i)), fabs(ys[i])) * rtol);
+        es += q * q;
+      }
+      const T en = fsqrt(es) * inv_sqrt_n;
+      if (active) {
         if (en < T(1)) {
           double factor = (en == T(0)) ? 10.0 : fmin(10.0, 0.9 * (double)fpow(en, T(-0.2)));
           if (rejected) factor = fmin(1.0, factor);
@@ -633,8 +656,8 @@ FW_HD int rk45(const DevCfg<T>& c, const StepCtx<T>& X, T* y_io, T* __restrict__
 // Actuation.set_and_constrain_commands (pyfly.py:545-582).  cmd in/out in input
 // order (elevator, aileron, throttle); sp = dynamics set-points.
 // ---------------------------------------------------------------------------
-template <typename T>
-FW_HD int constrain_commands(const DevCfg<T>& c, T* cmd, T* sp) {
+template <typename T, typename C>
+FW_HD int constrain_commands(const C& c, T* cmd, T* sp) {
   int term = 0;
   if (c.elevon) {
     T er = T(-1) * cmd[1] + cmd[0], el = cmd[1] + cmd[0];
@@ -688,8 +711,8 @@ FW_HD void dryden(const DevCfg<T>& c, int k, const T* un1, const T* u0, T* tl, T
 //             caller keeps its previous der[r] for the clear bits.
 // Returns termination code (0 = success).
 // ---------------------------------------------------------------------------
-template <typename T>
-FW_HD int sim_step_masked(const DevCfg<T>& c, T* y, T* der, T* cmd, const T* wind, const T* tl, const T* ta, int& nfev,
+template <typename T, typename C>
+FW_HD int sim_step_masked(const C& c, T* y, T* der, T* cmd, const T* wind, const T* tl, const T* ta, int& nfev,
                           int& nacc, uint32_t& dmask, T* sy, T* sf, int stride) {
   dmask = 0;
   StepCtx<T> X;
@@ -794,8 +817,8 @@ FW_HD void euler_to_quat(T phi, T th, T psi, T* q) {
 
 // Post-reset derived states (pyfly.py:1296-1311): Va/alpha/beta from Euler
 // angles (turbulence is 0 at k = 0), elevator/aileron .value.
-template <typename T>
-FW_HD void reset_derived(const DevCfg<T>& c, const T* y, const T* wind, T* der) {
+template <typename T, typename C>
+FW_HD void reset_derived(const C& c, const T* y, const T* wind, T* der) {
   const T zero[3] = {T(0), T(0), T(0)};
   T va[3];
   airspeed_vec_euler(der[0], der[1], der[2], wind, zero, y + 10, va);

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -46,6 +47,9 @@ int set_err(int code, const std::string& msg) { return fw::set_error(code, msg);
   } while (0)
 
 constexpr int BLOCK = 256;
+#ifndef FW_LDS_STATE
+#define FW_LDS_STATE 1  // 0 = y/f in VGPRs (measured: 512 VGPRs + spills, slower)
+#endif
 constexpr int RING = FW_MAX_WINDOW - 1;  // max previous actions kept
 
 // ---------------------------------------------------------------------------
@@ -407,14 +411,14 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const DevCfg<T>* __restrict__
   observe(c, y, der, tgt, steps, seqA, seqC, obs + i * c.n_obs, 1);
 }
 
-template <typename T>
+template <typename T, typename C>
 __global__ __launch_bounds__(BLOCK) void k_sim_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
                                                     const T* __restrict__ cmd_in, T* __restrict__ cmd_out,
                                                     uint8_t* __restrict__ success, int32_t* __restrict__ term_out,
                                                     int32_t* __restrict__ stats) {
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (i >= s.n) return;
-  const DevCfg<T>& c = *cfgp;
+  const C& c = *reinterpret_cast<const C*>(cfgp);  // structural specialisation view (fw_device.hpp SpecCfg)
   const int64_t ld = s.ld;
   T y[NY], der[8], wind[3], cmd[3];
   load_row(s.y, NY, ld, i, y);
@@ -452,7 +456,7 @@ __global__ __launch_bounds__(BLOCK) void k_sim_step(const DevCfg<T>* __restrict_
   if (stats) stats[i] = nfev | (nacc << 16);
 }
 
-template <typename T>
+template <typename T, typename C>
 __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
                                                     const T* __restrict__ actions, T* __restrict__ obs_out,
                                                     T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
@@ -461,7 +465,7 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
                                                     int auto_reset) {
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (i >= s.n) return;
-  const DevCfg<T>& c = *cfgp;
+  const C& c = *reinterpret_cast<const C*>(cfgp);  // structural specialisation view (fw_device.hpp SpecCfg)
   const int64_t ld = s.ld;
 
   T y[NY], der[8], wind[3], tgt[3], a[3];
@@ -487,9 +491,14 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
   turbulence_at(c, s, i, episode, steps0, tl, ta);
   int nfev = 0, nacc = 0;
   uint32_t dmask = 0;
+#if FW_LDS_STATE
   __shared__ T lds[2 * NY * BLOCK];  // accepted RK state y and f of the block's aircraft
   const int sterm = sim_step_masked(c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
                                     lds + NY * BLOCK + threadIdx.x, BLOCK);
+#else
+  T ry[NY], rf[NY];  // accepted RK state y and f in VGPRs
+  const int sterm = sim_step_masked(c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, ry, rf, 1);
+#endif
   // keep the epilogue's loads (action ring, goal bits, ...) below the integrator:
   // hoisted above it they would sit in VGPRs for the whole RK loop
   asm volatile("" ::: "memory");
@@ -640,6 +649,7 @@ struct fw_handle {
   int64_t env_offset = 0;
   const void* noise = nullptr;
   int64_t noise_len = 0;
+  int spec = 0;  // 0 = generic DevCfg kernels, 1 = GymX8Cfg, 2 = PyflyX8Cfg (structure matched at upload)
   // offsets (bytes) of the SoA blocks inside base
   size_t o_y, o_der, o_wind, o_target, o_cmd, o_epret, o_act, o_cmdring, o_steps, o_goal, o_episode;
 };
@@ -804,18 +814,48 @@ int validate(const fw_sim_config* s, const fw_env_config* e) {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Which compiled structural specialisation (fw_device.hpp SpecCfg) matches this config.
+template <typename S, typename T>
+bool same_structure(const DevCfg<T>& d) {
+  return d.cmask == S::cmask && d.clipmask == S::clipmask && d.wrapmask == S::wrapmask && d.dotmask == S::dotmask &&
+         d.elevon == S::elevon && d.trig_alpha == S::trig_alpha && d.trig_beta == S::trig_beta &&
+         d.euler_exact == S::euler_exact;
+}
+
+template <typename T>
+int spec_of(const DevCfg<T>& d) {
+  if (std::getenv("FWSIM_GENERIC")) return 0;  // A/B switch for tests and profiling
+  if (same_structure<GymX8Cfg<T>>(d)) return 1;
+  if (same_structure<PyflyX8Cfg<T>>(d)) return 2;
+  return 0;
+}
+
 int upload_cfg(fw_handle* h) {
   if (h->precision == FW_F64) {
     DevCfg<double> d;
     fill_devcfg(h, d);
+    h->spec = spec_of(d);
     FW_HIP(hipMemcpy(h->dcfg, &d, sizeof(d), hipMemcpyHostToDevice));
   } else {
     DevCfg<float> d;
     fill_devcfg(h, d);
+    h->spec = spec_of(d);
     FW_HIP(hipMemcpy(h->dcfg, &d, sizeof(d), hipMemcpyHostToDevice));
   }
   return FW_OK;
 }
+
+// launch KERNEL<T, C> with C chosen by the handle's structural specialisation
+#define FW_LAUNCH_SPEC(KERNEL, T, h, st, ...)                                                                     \
+  do {                                                                                                           \
+    const dim3 g_(grid_of(h)), b_(BLOCK);                                                                        \
+    if ((h)->spec == 1)                                                                                          \
+      hipLaunchKernelGGL((KERNEL<T, GymX8Cfg<T>>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);      \
+    else if ((h)->spec == 2)                                                                                     \
+      hipLaunchKernelGGL((KERNEL<T, PyflyX8Cfg<T>>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);    \
+    else                                                                                                         \
+      hipLaunchKernelGGL((KERNEL<T, DevCfg<T>>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);        \
+  } while (0)
 
 template <typename T>
 State<T> state_of(const fw_handle* h) {
@@ -1028,13 +1068,11 @@ int fw_sim_step(fw_handle* h, const void* commands_dev, void* commands_out_dev, 
   FW_HIP(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
   if (h->precision == FW_F64)
-    hipLaunchKernelGGL(k_sim_step<double>, dim3(grid_of(h)), dim3(BLOCK), 0, st, (const DevCfg<double>*)h->dcfg,
-                       state_of<double>(h), (const double*)commands_dev, (double*)commands_out_dev, success_dev,
-                       term_dev, stats_dev);
+    FW_LAUNCH_SPEC(k_sim_step, double, h, st, state_of<double>(h), (const double*)commands_dev,
+                   (double*)commands_out_dev, success_dev, term_dev, stats_dev);
   else
-    hipLaunchKernelGGL(k_sim_step<float>, dim3(grid_of(h)), dim3(BLOCK), 0, st, (const DevCfg<float>*)h->dcfg,
-                       state_of<float>(h), (const float*)commands_dev, (float*)commands_out_dev, success_dev, term_dev,
-                       stats_dev);
+    FW_LAUNCH_SPEC(k_sim_step, float, h, st, state_of<float>(h), (const float*)commands_dev, (float*)commands_out_dev,
+                   success_dev, term_dev, stats_dev);
   return check_launch();
 }
 
@@ -1046,13 +1084,13 @@ int fw_env_step(fw_handle* h, const void* actions_dev, void* obs_dev, void* rewa
   FW_HIP(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
   if (h->precision == FW_F64)
-    hipLaunchKernelGGL(k_env_step<double>, dim3(grid_of(h)), dim3(BLOCK), 0, st, (const DevCfg<double>*)h->dcfg,
-                       state_of<double>(h), (const double*)actions_dev, (double*)obs_dev, (double*)reward_dev,
-                       done_dev, term_dev, (double*)terminal_obs_dev, (double*)episode_dev, stats_dev, auto_reset);
+    FW_LAUNCH_SPEC(k_env_step, double, h, st, state_of<double>(h), (const double*)actions_dev, (double*)obs_dev,
+                   (double*)reward_dev, done_dev, term_dev, (double*)terminal_obs_dev, (double*)episode_dev, stats_dev,
+                   auto_reset);
   else
-    hipLaunchKernelGGL(k_env_step<float>, dim3(grid_of(h)), dim3(BLOCK), 0, st, (const DevCfg<float>*)h->dcfg,
-                       state_of<float>(h), (const float*)actions_dev, (float*)obs_dev, (float*)reward_dev, done_dev,
-                       term_dev, (float*)terminal_obs_dev, (float*)episode_dev, stats_dev, auto_reset);
+    FW_LAUNCH_SPEC(k_env_step, float, h, st, state_of<float>(h), (const float*)actions_dev, (float*)obs_dev,
+                   (float*)reward_dev, done_dev, term_dev, (float*)terminal_obs_dev, (float*)episode_dev, stats_dev,
+                   auto_reset);
   return check_launch();
 }
 
