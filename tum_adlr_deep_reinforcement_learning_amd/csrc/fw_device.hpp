@@ -454,9 +454,18 @@ FW_HD int rhs(const C& c0, const StepCtx<T>& X, bool first, const T* y, T* dy) {
 // K_j for the stages to come, YB = sum_j B_j K_j, ER = sum_j E_j K_j); per
 // element the sums run j = 0, 1, ... as scipy's np.dot(K[:s].T, a[:s])
 // (rk.py:58-64).
+// Pair layout: the 19-element state is processed as NP = 10 two-element
+// vectors (element 19 is a zero pad), so fp32 folds issue as packed
+// v_pk_fma_f32 / v_pk_mul_f32 (two elements per instruction) and the LDS slots
+// move 8 bytes per access.  fp64 uses the same code (scalarised by the backend).
+template <typename T>
+using V2 = T __attribute__((ext_vector_type(2)));
+constexpr int NP = (NY + 1) / 2;
+
 template <typename T, typename C>
-FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, T* __restrict__ sy, T* __restrict__ sf, int stride,
+FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy, V2<T>* __restrict__ sf, int stride,
                int& nfev, int& nacc) {
+  using V = V2<T>;
   constexpr double A10 = 1.0 / 5;
   constexpr double A20 = 3.0 / 40, A21 = 9.0 / 40;
   constexpr double A30 = 44.0 / 45, A31 = -56.0 / 15, A32 = 32.0 / 9;
@@ -471,14 +480,17 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, T* __restrict__ sy, T* 
   const T inv_sqrt_n = T(0.22941573387056177);  // 1 / sqrt(19)
 
   // y and f (the accepted state and its derivative) live in LDS slots of this
-  // lane (element i at s[i * stride]); only the stage accumulators stay in VGPRs.
-#define Y(i) sy[(i) * stride]
-#define F(i) sf[(i) * stride]
-  T P3[NY], P4[NY], P5[NY], YB[NY], ER[NY], ys[NY], K[NY];
+  // lane (pair p at s[p * stride]); the stage accumulators stay in VGPRs.
+#define Y(p) sy[(p) * stride]
+#define F(p) sf[(p) * stride]
+  V P3[NP], P4[NP], P5[NP], YB[NP], ER[NP], ys[NP], K[NP];
 #pragma unroll
-  for (int i = 0; i < NY; i++) {
-    ys[i] = y_io[i];
-    Y(i) = y_io[i];
+  for (int p = 0; p < NP; p++) {
+    V v;
+    v.x = y_io[2 * p];
+    v.y = 2 * p + 1 < NY ? y_io[2 * p + 1] : T(0);
+    ys[p] = v;
+    Y(p) = v;
   }
   double t = 0.0, h_abs = 0.0, h0 = 0.0, t_new = 0.0, min_step = 0.0;
   T ht = T(0), d1 = T(0);
@@ -486,6 +498,14 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, T* __restrict__ sy, T* 
   int result = 0;
   nfev = 0;
   nacc = 0;
+  // 1 / (atol + |y| rtol) for both lanes of a pair
+  auto iscale = [&](V y) {
+    V r;
+    r.x = frcp(atol + fabs(y.x) * rtol);
+    r.y = frcp(atol + fabs(y.y) * rtol);
+    return r;
+  };
+  auto sq2 = [](V v) { return v.x * v.x + v.y * v.y; };
 
   // stage: 0 = f0, 1 = probe, 2..7 = RK stage s = stage - 1 (s = 6: f(t_new, y_new)).
   // The RHS and the stage folds run on EVERY lane (finished lanes compute on
@@ -495,7 +515,8 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, T* __restrict__ sy, T* 
   for (int stage = 0;;) {
     if (!any_lane(active)) break;
     {
-      const int term = rhs(c, X, stage == 0, ys, K);
+      const int term = rhs(c, X, stage == 0, (const T*)ys, (T*)K);
+      K[NP - 1].y = T(0);  // pad element
       if (active) {
         nfev++;
         if (term) {
@@ -514,12 +535,11 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, T* __restrict__ sy, T* 
     if (stage == 0) {  // ---- f0; select_initial_step (common.py:68-110)
       T d0s = T(0), d1s = T(0);
 #pragma unroll
-      for (int i = 0; i < NY; i++) {
-        F(i) = K[i];
-        const T isc = frcp(atol + fabs(Y(i)) * rtol);
-        const T a = Y(i) * isc, b = K[i] * isc;
-        d0s += a * a;
-        d1s += b * b;
+      for (int p = 0; p < NP; p++) {
+        F(p) = K[p];
+        const V isc = iscale(Y(p));
+        d0s += sq2(Y(p) * isc);
+        d1s += sq2(K[p] * isc);
       }
       const T d0 = fsqrt(d0s) * inv_sqrt_n;
       d1 = fsqrt(d1s) * inv_sqrt_n;
@@ -527,15 +547,12 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, T* __restrict__ sy, T* 
       if (h0 > t_bound) h0 = t_bound;
       const T h0t = (T)h0;
 #pragma unroll
-      for (int i = 0; i < NY; i++) ys[i] = Y(i) + h0t * F(i);
+      for (int p = 0; p < NP; p++) ys[p] = Y(p) + h0t * F(p);
       stage = 1;
     } else if (stage == 1) {  // ---- probe; select_initial_step (common.py:111-134)
       T d2s = T(0);
 #pragma unroll
-      for (int i = 0; i < NY; i++) {
-        const T a = (K[i] - F(i)) * frcp(atol + fabs(Y(i)) * rtol);
-        d2s += a * a;
-      }
+      for (int p = 0; p < NP; p++) d2s += sq2((K[p] - F(p)) * iscale(Y(p)));
       const double d2 = (double)(fsqrt(d2s) * inv_sqrt_n) / h0;
       double h1;
       if ((double)d1 <= 1e-15 && d2 <= 1e-15) h1 = fmax(1e-6, h0 * 1e-3);
@@ -545,60 +562,64 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, T* __restrict__ sy, T* 
       stage = 2;
     } else if (stage == 2) {  // K = K1
 #pragma unroll
-      for (int i = 0; i < NY; i++) {
-        ys[i] = Y(i) + (F(i) * T(A20) + K[i] * T(A21)) * ht;
-        P3[i] = F(i) * T(A30) + K[i] * T(A31);
-        P4[i] = F(i) * T(A40) + K[i] * T(A41);
-        P5[i] = F(i) * T(A50) + K[i] * T(A51);
-        YB[i] = F(i) * T(B0);
-        ER[i] = F(i) * T(E0);
+      for (int p = 0; p < NP; p++) {
+        const V f = F(p);
+        ys[p] = Y(p) + (f * T(A20) + K[p] * T(A21)) * ht;
+        P3[p] = f * T(A30) + K[p] * T(A31);
+        P4[p] = f * T(A40) + K[p] * T(A41);
+        P5[p] = f * T(A50) + K[p] * T(A51);
+        YB[p] = f * T(B0);
+        ER[p] = f * T(E0);
       }
       stage = 3;
     } else if (stage == 3) {  // K = K2
 #pragma unroll
-      for (int i = 0; i < NY; i++) {
-        P3[i] += K[i] * T(A32);
-        P4[i] += K[i] * T(A42);
-        P5[i] += K[i] * T(A52);
-        YB[i] += K[i] * T(B2);
-        ER[i] += K[i] * T(E2);
-        ys[i] = Y(i) + P3[i] * ht;
+      for (int p = 0; p < NP; p++) {
+        P3[p] += K[p] * T(A32);
+        P4[p] += K[p] * T(A42);
+        P5[p] += K[p] * T(A52);
+        YB[p] += K[p] * T(B2);
+        ER[p] += K[p] * T(E2);
+        ys[p] = Y(p) + P3[p] * ht;
       }
       stage = 4;
     } else if (stage == 4) {  // K = K3
 #pragma unroll
-      for (int i = 0; i < NY; i++) {
-        P4[i] += K[i] * T(A43);
-        P5[i] += K[i] * T(A53);
-        YB[i] += K[i] * T(B3);
-        ER[i] += K[i] * T(E3);
-        ys[i] = Y(i) + P4[i] * ht;
+      for (int p = 0; p < NP; p++) {
+        P4[p] += K[p] * T(A43);
+        P5[p] += K[p] * T(A53);
+        YB[p] += K[p] * T(B3);
+        ER[p] += K[p] * T(E3);
+        ys[p] = Y(p) + P4[p] * ht;
       }
       stage = 5;
     } else if (stage == 5) {  // K = K4
 #pragma unroll
-      for (int i = 0; i < NY; i++) {
-        P5[i] += K[i] * T(A54);
-        YB[i] += K[i] * T(B4);
-        ER[i] += K[i] * T(E4);
-        ys[i] = Y(i) + P5[i] * ht;
+      for (int p = 0; p < NP; p++) {
+        P5[p] += K[p] * T(A54);
+        YB[p] += K[p] * T(B4);
+        ER[p] += K[p] * T(E4);
+        ys[p] = Y(p) + P5[p] * ht;
       }
       stage = 6;
     } else if (stage == 6) {  // K = K5; ys <- y_new
 #pragma unroll
-      for (int i = 0; i < NY; i++) {
-        YB[i] += K[i] * T(B5);
-        ER[i] += K[i] * T(E5);
-        ys[i] = Y(i) + ht * YB[i];
+      for (int p = 0; p < NP; p++) {
+        YB[p] += K[p] * T(B5);
+        ER[p] += K[p] * T(E5);
+        ys[p] = Y(p) + ht * YB[p];
       }
       stage = 7;
     } else {  // K = f(t_new, y_new): error norm + step control (rk.py:138-173)
       T es = T(0);
 #pragma unroll
-      for (int i = 0; i < NY; i++) {
-        const T e = (ER[i] + K[i] * T(E6)) * ht;
-        const T q = e * frcp(atol + fmax(fabs(Y(i)), fabs(ys[i])) * rtol);
-        es += q * q;
+      for (int p = 0; p < NP; p++) {
+        const V e = (ER[p] + K[p] * T(E6)) * ht;
+        const V y0 = Y(p), y1 = ys[p];
+        V sc;
+        sc.x = frcp(atol + fmax(fabs(y0.x), fabs(y1.x)) * rtol);
+        sc.y = frcp(atol + fmax(fabs(y0.y), fabs(y1.y)) * rtol);
+        es += sq2(e * sc);
       }
       const T en = fsqrt(es) * inv_sqrt_n;
       if (active) {
@@ -608,9 +629,9 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, T* __restrict__ sy, T* 
           h_abs *= factor;
           t = t_new;
 #pragma unroll
-          for (int i = 0; i < NY; i++) {
-            Y(i) = ys[i];
-            F(i) = K[i];
+          for (int p = 0; p < NP; p++) {
+            Y(p) = ys[p];
+            F(p) = K[p];
           }
           nacc++;
           if (t - t_bound >= 0.0) active = false;  // OdeSolver.step: finished (base.py:203-204)
@@ -642,11 +663,15 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, T* __restrict__ sy, T* 
       h_abs = fabs(h);
       ht = (T)h;
 #pragma unroll
-      for (int i = 0; i < NY; i++) ys[i] = Y(i) + (F(i) * T(A10)) * ht;
+      for (int p = 0; p < NP; p++) ys[p] = Y(p) + (F(p) * T(A10)) * ht;
     }
   }
 #pragma unroll
-  for (int i = 0; i < NY; i++) y_io[i] = Y(i);
+  for (int p = 0; p < NP; p++) {
+    const V v = Y(p);
+    y_io[2 * p] = v.x;
+    if (2 * p + 1 < NY) y_io[2 * p + 1] = v.y;
+  }
 #undef Y
 #undef F
   return result;
@@ -713,7 +738,7 @@ FW_HD void dryden(const DevCfg<T>& c, int k, const T* un1, const T* u0, T* tl, T
 // ---------------------------------------------------------------------------
 template <typename T, typename C>
 FW_HD int sim_step_masked(const C& c, T* y, T* der, T* cmd, const T* wind, const T* tl, const T* ta, int& nfev,
-                          int& nacc, uint32_t& dmask, T* sy, T* sf, int stride) {
+                          int& nacc, uint32_t& dmask, V2<T>* sy, V2<T>* sf, int stride) {
   dmask = 0;
   StepCtx<T> X;
 #pragma unroll

@@ -433,9 +433,9 @@ __global__ __launch_bounds__(BLOCK) void k_sim_step(const DevCfg<T>* __restrict_
   turbulence_at(c, s, i, s.episode[i], k, tl, ta);
   int nfev = 0, nacc = 0;
   uint32_t dmask = 0;
-  __shared__ T lds[2 * NY * BLOCK];  // accepted RK state y and f of the block's aircraft
+  __shared__ V2<T> lds[2 * NP * BLOCK];  // accepted RK state y and f of the block's aircraft (pairs)
   const int term = sim_step_masked(c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
-                                   lds + NY * BLOCK + threadIdx.x, BLOCK);
+                                   lds + NP * BLOCK + threadIdx.x, BLOCK);
   if (term) {  // uncommitted derived values keep their previous (history[-1]) value
 #pragma unroll
     for (int r = 0; r < 6; r++)
@@ -492,11 +492,11 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
   int nfev = 0, nacc = 0;
   uint32_t dmask = 0;
 #if FW_LDS_STATE
-  __shared__ T lds[2 * NY * BLOCK];  // accepted RK state y and f of the block's aircraft
+  __shared__ V2<T> lds[2 * NP * BLOCK];  // accepted RK state y and f of the block's aircraft (pairs)
   const int sterm = sim_step_masked(c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
-                                    lds + NY * BLOCK + threadIdx.x, BLOCK);
+                                    lds + NP * BLOCK + threadIdx.x, BLOCK);
 #else
-  T ry[NY], rf[NY];  // accepted RK state y and f in VGPRs
+  V2<T> ry[NP], rf[NP];  // accepted RK state y and f in VGPRs
   const int sterm = sim_step_masked(c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, ry, rf, 1);
 #endif
   // keep the epilogue's loads (action ring, goal bits, ...) below the integrator:
