@@ -37,6 +37,9 @@ int set_error(int code, const std::string& msg);
 constexpr int NY = FW_NY;
 constexpr double PI_D = 3.141592653589793;
 constexpr int MAX_NFEV = 6000;
+#ifndef FW_ER_LDS
+#define FW_ER_LDS 1  // DOPRI error sum in LDS: frees 20 VGPRs of the RK loop (measured -3%)
+#endif
 #ifndef FW_RELAUNDER
 #define FW_RELAUNDER 1  // re-issue config scalar loads per RHS instead of pinning ~100 constants in SGPRs (spills)
 #endif  // RHS evaluations per step before the step is declared a solver failure
@@ -57,6 +60,10 @@ struct DevCfg {
   T gam[9];
   T M, a0, pi_e_ar;
   T sig_c;                   // exp(2 M a0) = e^{-M(a-a0)} e^{M(a+a0)} (stall-blend constant)
+  // host-folded constant products of the force model (one multiply each in the RHS)
+  T qS, qSc, qSb;            // rho/2 S, rho/2 S c, rho/2 S b
+  T kCLq, kCDq, kCmq, hb;    // C_L_q c/2, C_D_q c/2, C_m_q b/2 (pyfly.py:1579 uses b), b/2
+  T inv_pi_e_ar, kTP2;       // 1/(pi e AR), k_T_P k_Omega^2
   T CL0, CLa, CLq, CLde, CDp, CDq, CDb1, CDb2, CDde, Cm0, Cma, Cmq, Cmde, Cmfp;
   T CY0, CYb, CYp, CYr, CYda, CYdr, Cl0, Clb, Clp, Clr, Clda, Cldr, Cn0, Cnb, Cnp, Cnr, Cnda, Cndr;
   T kmotor, prop_k, kTP, kOmega;
@@ -168,6 +175,36 @@ FW_HD float fpow(float a, float p) {  // a > 0
 #endif
 }
 
+// atan2 for the RHS.  fp64: libm.  fp32: octant reduction + a degree-8 polynomial
+// in t^2 for atan(t), t in [0, 1] (fitted by tools/atan_fit in DESIGN.md; max abs
+// error 1.0e-7 rad, i.e. ~1 ulp at pi/4) -- ~20 instructions instead of the ~45 of
+// the correctly-rounded library routine, which matters because every RHS needs two.
+FW_HD double fatan2(double y, double x) { return atan2(y, x); }
+FW_HD float fatan2(float y, float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  const float t = mn * __builtin_amdgcn_rcpf(mx);
+  const float q = t * t;
+  float p = 0.0029030926525592804f;
+  p = fmaf(p, q, -0.016281209886074066f);
+  p = fmaf(p, q, 0.043036505579948425f);
+  p = fmaf(p, q, -0.07533437758684158f);
+  p = fmaf(p, q, 0.10654566437005997f);
+  p = fmaf(p, q, -0.14207105338573456f);
+  p = fmaf(p, q, 0.19993050396442413f);
+  p = fmaf(p, q, -0.3333309292793274f);
+  p = fmaf(p, q, 1.0f);
+  float r = t * p;
+  r = ay > ax ? 1.5707963267948966f - r : r;
+  r = x < 0.0f ? 3.141592653589793f - r : r;
+  r = mx == 0.0f ? 0.0f : r;
+  return copysignf(r, y);
+#else
+  return atan2f(y, x);
+#endif
+}
+
 // ---------------------------------------------------------------------------
 // small helpers
 // ---------------------------------------------------------------------------
@@ -185,10 +222,14 @@ FW_HD T sgn(T x) {
 }
 
 template <typename T>
-FW_HD T clipv(T x, T lo, T hi) {  // np.clip semantics (NaN propagates)
-  x = x < lo ? lo : x;
-  x = x > hi ? hi : x;
-  return x;
+FW_HD T clipv(T x, T lo, T hi) {
+  // np.clip for every non-NaN x in one v_med3_f32 (fp32) / v_max+v_min (fp64).  A NaN x
+  // clamps to lo instead of propagating: NaN states fail the step via the step-size
+  // control anyway (rk45: !(h_abs >= min_step)).
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (sizeof(T) == 4) return __builtin_amdgcn_fmed3f(x, lo, hi);
+#endif
+  return fmin(fmax(x, lo), hi);
 }
 
 // Variable.apply_conditions (pyfly.py:114-133).  Records the first violation.
@@ -334,13 +375,13 @@ FW_HD int rhs(const C& c0, const StepCtx<T>& X, bool first, const T* y, T* dy) {
   }
   T va[3];
   airspeed_vec(y, X.wind, X.tl, vel, va);
-  const T Va_raw = fsqrt(va[0] * va[0] + va[1] * va[1] + va[2] * va[2]);
-  T alpha = atan2(va[2], va[0]);
-  T sb_raw = fdiv(va[1], Va_raw);
-  // |v|/|va| <= 1 exactly; the 1-ulp reciprocal of the fp32 path can push the
-  // ratio past 1 in pure sideslip, where asin would return NaN
-  if (sizeof(T) == 4) sb_raw = clipv(sb_raw, T(-1), T(1));
-  T beta = asin(sb_raw);
+  // Va = |va|, alpha = atan2(w, u), beta = asin(v / Va) = atan2(v, sqrt(u^2 + w^2))
+  // (pyfly.py:1506-1511, _calculate_airspeed_factors :1830-1850)
+  const T rxz2 = va[0] * va[0] + va[2] * va[2];
+  const T rxz = fsqrt(rxz2);
+  const T Va_raw = fsqrt(rxz2 + va[1] * va[1]);
+  T alpha = fatan2(va[2], va[0]);
+  T beta = fatan2(va[1], rxz);
   const T Va = cond(c, FW_V_VA, Va_raw, term);
   alpha = cond(c, FW_V_ALPHA, alpha, term);
   beta = cond(c, FW_V_BETA, beta, term);
@@ -350,20 +391,20 @@ FW_HD int rhs(const C& c0, const StepCtx<T>& X, bool first, const T* y, T* dy) {
     sa = sin(alpha);
     ca = cos(alpha);
   } else {  // sin/cos of atan2(z, x) without the transcendental
-    const T rxz2 = va[0] * va[0] + va[2] * va[2];
-    const T irxz = frcp(fsqrt(rxz2));
+    const T irxz = frcp(rxz);
     sa = rxz2 > T(0) ? va[2] * irxz : T(0);
     ca = rxz2 > T(0) ? va[0] * irxz : T(1);
   }
   if (c.trig_beta) {
     sb = sin(beta);
     cb = cos(beta);
-  } else {  // beta = asin(s): sin = s, cos = sqrt(1 - s^2)
-    sb = sb_raw;
-    cb = fsqrt(fmax(T(1) - sb_raw * sb_raw, T(0)));
+  } else {  // sin / cos of beta = asin(v / Va): v / Va and sqrt(u^2 + w^2) / Va
+    const T iVr = frcp(Va_raw);
+    sb = va[1] * iVr;
+    cb = rxz * iVr;
   }
 
-  const T pre = c.half_rho * (Va * Va) * c.S;
+  const T V2a = Va * Va;
   const T fg0 = c.mg * (T(2) * (e1 * e3 - e2 * e0));
   const T fg1 = c.mg * (T(2) * (e2 * e3 + e1 * e0));
   const T fg2 = c.mg * (e3 * e3 + e0 * e0 - e1 * e1 - e2 * e2);
@@ -375,28 +416,30 @@ FW_HD int rhs(const C& c0, const StepCtx<T>& X, bool first, const T* y, T* dy) {
   // (whose fp32 reciprocal flushes to 0 and flips sigma from 1 to 0 deep in
   // stall) and it is exactly 1 when an exponential overflows.
   const T sigma = frcp(T(1) + c.sig_c * frcp(T(1) + ex1 + ex2));
+  const T osig = T(1) - sigma;
   const T sgna = sgn(alpha);
   const T CLlin = c.CL0 + c.CLa * alpha;
-  const T CL = (T(1) - sigma) * CLlin + sigma * (T(2) * sgna * sa * sa * ca);
-  const T inv2Va = frcp(T(2) * Va);
-  const T flift = pre * (CL + c.CLq * c.c * inv2Va * q + c.CLde * elev);
-  const T CD = c.CDp + fdiv((T(1) - sigma) * (CLlin * CLlin), c.pi_e_ar) + sigma * (T(2) * sgna * (sa * sa * sa));
+  const T CL = osig * CLlin + sigma * (T(2) * sgna * sa * sa * ca);
+  const T iVa = frcp(Va);
+  const T qn = q * iVa;  // q / Va
+  // lift / drag / pitch moment per unit dynamic pressure (pyfly.py:1529-1579)
+  const T flift = c.qS * V2a * (CL + c.kCLq * qn + c.CLde * elev);
+  const T CD = c.CDp + osig * (CLlin * CLlin) * c.inv_pi_e_ar + sigma * (T(2) * sgna * (sa * sa * sa));
   const T CDb = c.CDb1 * beta + c.CDb2 * beta * beta;
-  const T fdrag = pre * (CD + CDb + c.CDq * c.c * inv2Va * q + c.CDde * elev * elev);
-  const T Cm = (T(1) - sigma) * (c.Cm0 + c.Cma * alpha) + sigma * (c.Cmfp * sgna * sa * sa);
-  const T mm = pre * c.c * (Cm + c.Cmq * c.b * inv2Va * q + c.Cmde * elev);
-  const T bp = c.b * inv2Va * p, br = c.b * inv2Va * r;
-  const T fy = pre * (c.CY0 + c.CYb * beta + c.CYp * bp + c.CYr * br + c.CYda * ail);
-  const T ll = pre * c.b * (c.Cl0 + c.Clb * beta + c.Clp * bp + c.Clr * br + c.Clda * ail);
-  const T nn = pre * c.b * (c.Cn0 + c.Cnb * beta + c.Cnp * bp + c.Cnr * br + c.Cnda * ail);
+  const T fdrag = c.qS * V2a * (CD + CDb + c.kCDq * qn + c.CDde * elev * elev);
+  const T Cm = osig * (c.Cm0 + c.Cma * alpha) + sigma * (c.Cmfp * sgna * sa * sa);
+  const T mm = c.qSc * V2a * (Cm + c.kCmq * qn + c.Cmde * elev);
+  const T bp = c.hb * p * iVa, br = c.hb * r * iVa;
+  const T fy = c.qS * V2a * (c.CY0 + c.CYb * beta + c.CYp * bp + c.CYr * br + c.CYda * ail);
+  const T ll = c.qSb * V2a * (c.Cl0 + c.Clb * beta + c.Clp * bp + c.Clr * br + c.Clda * ail);
+  const T nn = c.qSb * V2a * (c.Cn0 + c.Cnb * beta + c.Cnp * bp + c.Cnr * br + c.Cnda * ail);
   // f_aero = R_euler(0, alpha, beta) . [-D, Y, -L]
   const T fa0 = ca * cb * (-fdrag) + ca * sb * fy - sa * (-flift);
   const T fa1 = -sb * (-fdrag) + cb * fy;
   const T fa2 = sa * cb * (-fdrag) + sa * sb * fy + ca * (-flift);
   const T Vd = Va + thr * (c.kmotor - Va);
   const T fprop = c.prop_k * Vd * (Vd - Va);
-  const T kt = c.kOmega * thr;
-  const T tprop = -c.kTP * kt * kt;
+  const T tprop = -c.kTP2 * (thr * thr);
   const T f0 = fprop + fg0 + fa0, f1 = fg1 + fa1, f2 = fg2 + fa2;
   const T t0 = ll + tprop, t1 = mm, t2 = nn;
 
@@ -464,7 +507,7 @@ constexpr int NP = (NY + 1) / 2;
 
 template <typename T, typename C>
 FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy, V2<T>* __restrict__ sf, int stride,
-               int& nfev, int& nacc) {
+               int& nfev, int& nacc, V2<T>* __restrict__ se = nullptr) {
   using V = V2<T>;
   constexpr double A10 = 1.0 / 5;
   constexpr double A20 = 3.0 / 40, A21 = 9.0 / 40;
@@ -483,7 +526,14 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
   // lane (pair p at s[p * stride]); the stage accumulators stay in VGPRs.
 #define Y(p) sy[(p) * stride]
 #define F(p) sf[(p) * stride]
+#if FW_ER_LDS
+  // error accumulator in this lane's third LDS slot (registers go to the live stage vectors)
+#define ERV(p) se[(p) * stride]
+  V P3[NP], P4[NP], P5[NP], YB[NP], ys[NP], K[NP];
+#else
   V P3[NP], P4[NP], P5[NP], YB[NP], ER[NP], ys[NP], K[NP];
+#define ERV(p) ER[p]
+#endif
 #pragma unroll
   for (int p = 0; p < NP; p++) {
     V v;
@@ -569,7 +619,7 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
         P4[p] = f * T(A40) + K[p] * T(A41);
         P5[p] = f * T(A50) + K[p] * T(A51);
         YB[p] = f * T(B0);
-        ER[p] = f * T(E0);
+        ERV(p) = f * T(E0);
       }
       stage = 3;
     } else if (stage == 3) {  // K = K2
@@ -579,7 +629,7 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
         P4[p] += K[p] * T(A42);
         P5[p] += K[p] * T(A52);
         YB[p] += K[p] * T(B2);
-        ER[p] += K[p] * T(E2);
+        ERV(p) += K[p] * T(E2);
         ys[p] = Y(p) + P3[p] * ht;
       }
       stage = 4;
@@ -589,7 +639,7 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
         P4[p] += K[p] * T(A43);
         P5[p] += K[p] * T(A53);
         YB[p] += K[p] * T(B3);
-        ER[p] += K[p] * T(E3);
+        ERV(p) += K[p] * T(E3);
         ys[p] = Y(p) + P4[p] * ht;
       }
       stage = 5;
@@ -598,7 +648,7 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
       for (int p = 0; p < NP; p++) {
         P5[p] += K[p] * T(A54);
         YB[p] += K[p] * T(B4);
-        ER[p] += K[p] * T(E4);
+        ERV(p) += K[p] * T(E4);
         ys[p] = Y(p) + P5[p] * ht;
       }
       stage = 6;
@@ -606,7 +656,7 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
 #pragma unroll
       for (int p = 0; p < NP; p++) {
         YB[p] += K[p] * T(B5);
-        ER[p] += K[p] * T(E5);
+        ERV(p) += K[p] * T(E5);
         ys[p] = Y(p) + ht * YB[p];
       }
       stage = 7;
@@ -614,7 +664,7 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
       T es = T(0);
 #pragma unroll
       for (int p = 0; p < NP; p++) {
-        const V e = (ER[p] + K[p] * T(E6)) * ht;
+        const V e = (ERV(p) + K[p] * T(E6)) * ht;
         const V y0 = Y(p), y1 = ys[p];
         V sc;
         sc.x = frcp(atol + fmax(fabs(y0.x), fabs(y1.x)) * rtol);
@@ -674,6 +724,7 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
   }
 #undef Y
 #undef F
+#undef ERV
   return result;
 }
 
@@ -736,9 +787,17 @@ FW_HD void dryden(const DevCfg<T>& c, int k, const T* un1, const T* u0, T* tl, T
 //             caller keeps its previous der[r] for the clear bits.
 // Returns termination code (0 = success).
 // ---------------------------------------------------------------------------
-template <typename T, typename C>
+struct KeepY {  // default: y stays live in registers across the integration
+  template <typename T>
+  FW_HD void operator()(T*) const {}
+};
+
+// `reload(y)` runs right after the integration and may re-read the pre-step
+// state from memory (the kernels do: keeping 19 values live across the RK loop
+// costs registers the loop needs).
+template <typename T, typename C, typename R = KeepY>
 FW_HD int sim_step_masked(const C& c, T* y, T* der, T* cmd, const T* wind, const T* tl, const T* ta, int& nfev,
-                          int& nacc, uint32_t& dmask, V2<T>* sy, V2<T>* sf, int stride) {
+                          int& nacc, uint32_t& dmask, V2<T>* sy, V2<T>* sf, int stride, R reload = R()) {
   dmask = 0;
   StepCtx<T> X;
 #pragma unroll
@@ -756,7 +815,8 @@ FW_HD int sim_step_masked(const C& c, T* y, T* der, T* cmd, const T* wind, const
   T y1[NY];
 #pragma unroll
   for (int i = 0; i < NY; i++) y1[i] = y[i];
-  term = rk45(c, X, y1, sy, sf, stride, nfev, nacc);
+  term = rk45(c, X, y1, sy, sf, stride, nfev, nacc, FW_ER_LDS ? sf + NP * stride : nullptr);
+  reload(y);
   if (term < 0) return 0;  // solver failure: reference keeps sol.y[:, -1]; never observed
   if (term) return term;
 

@@ -411,6 +411,20 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const DevCfg<T>* __restrict__
   observe(c, y, der, tgt, steps, seqA, seqC, obs + i * c.n_obs, 1);
 }
 
+// Re-reads the pre-step ODE state after the RK loop (sim_step_masked's reload hook): the
+// barrier keeps the compiler from reusing the prologue's loads, which would pin 19
+// values in registers for the whole integration.
+template <typename T>
+struct ReloadRow {
+  const T* y;
+  int64_t ld, i;
+  __device__ __forceinline__ void operator()(T* out) const {
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int r = 0; r < NY; r++) out[r] = y[r * ld + i];
+  }
+};
+
 template <typename T, typename C>
 __global__ __launch_bounds__(BLOCK) void k_sim_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
                                                     const T* __restrict__ cmd_in, T* __restrict__ cmd_out,
@@ -433,9 +447,9 @@ __global__ __launch_bounds__(BLOCK) void k_sim_step(const DevCfg<T>* __restrict_
   turbulence_at(c, s, i, s.episode[i], k, tl, ta);
   int nfev = 0, nacc = 0;
   uint32_t dmask = 0;
-  __shared__ V2<T> lds[2 * NP * BLOCK];  // accepted RK state y and f of the block's aircraft (pairs)
+  __shared__ V2<T> lds[(2 + FW_ER_LDS) * NP * BLOCK];  // y, f (+ error sum) of the block's aircraft (pairs)
   const int term = sim_step_masked(c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
-                                   lds + NP * BLOCK + threadIdx.x, BLOCK);
+                                   lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i});
   if (term) {  // uncommitted derived values keep their previous (history[-1]) value
 #pragma unroll
     for (int r = 0; r < 6; r++)
@@ -492,16 +506,20 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
   int nfev = 0, nacc = 0;
   uint32_t dmask = 0;
 #if FW_LDS_STATE
-  __shared__ V2<T> lds[2 * NP * BLOCK];  // accepted RK state y and f of the block's aircraft (pairs)
+  __shared__ V2<T> lds[(2 + FW_ER_LDS) * NP * BLOCK];  // y, f (+ error sum) of the block's aircraft (pairs)
   const int sterm = sim_step_masked(c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
-                                    lds + NP * BLOCK + threadIdx.x, BLOCK);
+                                    lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i});
 #else
   V2<T> ry[NP], rf[NP];  // accepted RK state y and f in VGPRs
   const int sterm = sim_step_masked(c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, ry, rf, 1);
 #endif
   // keep the epilogue's loads (action ring, goal bits, ...) below the integrator:
-  // hoisted above it they would sit in VGPRs for the whole RK loop
+  // hoisted above it they would sit in VGPRs for the whole RK loop.  Actions and
+  // targets are re-read for the same reason.
   asm volatile("" ::: "memory");
+  load_row(s.target, 3, ld, i, tgt);
+#pragma unroll
+  for (int q = 0; q < 3; q++) a[q] = actions[i * 3 + q];
   if (sterm) {
 #pragma unroll
     for (int r = 0; r < 6; r++)
@@ -692,6 +710,18 @@ void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
   d.a0 = (T)P[FW_P_A0];
   d.pi_e_ar = (T)(3.141592653589793 * P[FW_P_E] * (P[FW_P_B] * P[FW_P_B] / P[FW_P_S_WING]));
   d.sig_c = (T)std::exp(2.0 * P[FW_P_M] * P[FW_P_A0]);
+  {
+    const double qS = 0.5 * s.rho * P[FW_P_S_WING];
+    d.qS = (T)qS;
+    d.qSc = (T)(qS * P[FW_P_C]);
+    d.qSb = (T)(qS * P[FW_P_B]);
+    d.kCLq = (T)(P[FW_P_C_L_Q] * P[FW_P_C] * 0.5);
+    d.kCDq = (T)(P[FW_P_C_D_Q] * P[FW_P_C] * 0.5);
+    d.kCmq = (T)(P[FW_P_C_M_Q] * P[FW_P_B] * 0.5);
+    d.hb = (T)(P[FW_P_B] * 0.5);
+    d.inv_pi_e_ar = (T)(1.0 / (3.141592653589793 * P[FW_P_E] * (P[FW_P_B] * P[FW_P_B] / P[FW_P_S_WING])));
+    d.kTP2 = (T)(P[FW_P_K_T_P] * P[FW_P_K_OMEGA] * P[FW_P_K_OMEGA]);
+  }
   d.CL0 = (T)P[FW_P_C_L_0]; d.CLa = (T)P[FW_P_C_L_ALPHA]; d.CLq = (T)P[FW_P_C_L_Q]; d.CLde = (T)P[FW_P_C_L_DELTA_E];
   d.CDp = (T)P[FW_P_C_D_P]; d.CDq = (T)P[FW_P_C_D_Q]; d.CDb1 = (T)P[FW_P_C_D_BETA1]; d.CDb2 = (T)P[FW_P_C_D_BETA2];
   d.CDde = (T)P[FW_P_C_D_DELTA_E];
