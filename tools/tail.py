@@ -25,15 +25,25 @@ eng.reset()
 gen = torch.Generator(device="cuda:0")
 gen.manual_seed(1)
 pool = torch.rand(16, n, 3, generator=gen, device="cuda:0", dtype=eng.dtype) * 2 - 1
+MODE = os.environ.get("TAIL_MODE", "env")  # env | env_noreset | sim
+
+
+def step(a):
+    if MODE == "sim":
+        eng.sim_step(a, stats=True)
+    else:
+        eng.env_step(a, stats=True, auto_reset=(MODE == "env"))
+
+
 for s in range(20):
-    eng.env_step(pool[s % 16], stats=True)
+    step(pool[s % 16])
 torch.cuda.synchronize()
 ms, mx, p999, mean, wmax = [], [], [], [], []
 stream = torch.cuda.current_stream()
 for s in range(steps):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
-    eng.env_step(pool[s % 16], stats=True)
+    step(pool[s % 16])
     e1.record(stream)
     torch.cuda.synchronize()
     nf = (eng.stats & 0xFFFF).cpu().numpy().astype(np.int64)
@@ -46,7 +56,7 @@ for s in range(steps):
 ms, mx = np.array(ms), np.array(mx)
 A = np.stack([np.ones_like(mx, dtype=float), mx.astype(float)], 1)
 coef, *_ = np.linalg.lstsq(A, ms, rcond=None)
-out = {"n": n, "steps": steps, "ms_mean": float(ms.mean()), "ms_p50": float(np.median(ms)),
+out = {"mode": MODE, "n": n, "steps": steps, "ms_mean": float(ms.mean()), "ms_p50": float(np.median(ms)),
        "max_nfev_mean": float(mx.mean()), "max_nfev_p50": float(np.median(mx)), "max_nfev_max": int(mx.max()),
        "nfev_p999_mean": float(np.mean(p999)), "nfev_mean": float(np.mean(mean)),
        "wave_max_nfev_median": float(np.mean(wmax)),

@@ -37,11 +37,14 @@ int set_error(int code, const std::string& msg);
 constexpr int NY = FW_NY;
 constexpr double PI_D = 3.141592653589793;
 constexpr int MAX_NFEV = 6000;
+#ifndef FW_Y_PREFETCH
+#define FW_Y_PREFETCH 0
+#endif
 #ifndef FW_ER_LDS
 #define FW_ER_LDS 1  // DOPRI error sum in LDS: frees 20 VGPRs of the RK loop (measured -3%)
 #endif
 #ifndef FW_RELAUNDER
-#define FW_RELAUNDER 1  // re-issue config scalar loads per RHS instead of pinning ~100 constants in SGPRs (spills)
+#define FW_RELAUNDER 0  // 1: re-issue config scalar loads per RHS (helped the generic kernel; -4.5% slower on the specialised one)
 #endif  // RHS evaluations per step before the step is declared a solver failure
 
 template <typename T>
@@ -564,6 +567,16 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
   // arrays in place across the wave-uniform stage switch (no phi copies).
   for (int stage = 0;;) {
     if (!any_lane(active)) break;
+#if FW_Y_PREFETCH
+    // the accepted state is read by every stage's fold: issue the LDS reads before the
+    // RHS so their latency hides under it (Y changes only on accept, after the folds)
+    V yv[NP];
+#pragma unroll
+    for (int p = 0; p < NP; p++) yv[p] = Y(p);
+#define YR(p) yv[p]
+#else
+#define YR(p) Y(p)
+#endif
     {
       const int term = rhs(c, X, stage == 0, (const T*)ys, (T*)K);
       K[NP - 1].y = T(0);  // pad element
@@ -614,7 +627,7 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
 #pragma unroll
       for (int p = 0; p < NP; p++) {
         const V f = F(p);
-        ys[p] = Y(p) + (f * T(A20) + K[p] * T(A21)) * ht;
+        ys[p] = YR(p) + (f * T(A20) + K[p] * T(A21)) * ht;
         P3[p] = f * T(A30) + K[p] * T(A31);
         P4[p] = f * T(A40) + K[p] * T(A41);
         P5[p] = f * T(A50) + K[p] * T(A51);
@@ -630,7 +643,7 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
         P5[p] += K[p] * T(A52);
         YB[p] += K[p] * T(B2);
         ERV(p) += K[p] * T(E2);
-        ys[p] = Y(p) + P3[p] * ht;
+        ys[p] = YR(p) + P3[p] * ht;
       }
       stage = 4;
     } else if (stage == 4) {  // K = K3
@@ -640,7 +653,7 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
         P5[p] += K[p] * T(A53);
         YB[p] += K[p] * T(B3);
         ERV(p) += K[p] * T(E3);
-        ys[p] = Y(p) + P4[p] * ht;
+        ys[p] = YR(p) + P4[p] * ht;
       }
       stage = 5;
     } else if (stage == 5) {  // K = K4
@@ -649,7 +662,7 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
         P5[p] += K[p] * T(A54);
         YB[p] += K[p] * T(B4);
         ERV(p) += K[p] * T(E4);
-        ys[p] = Y(p) + P5[p] * ht;
+        ys[p] = YR(p) + P5[p] * ht;
       }
       stage = 6;
     } else if (stage == 6) {  // K = K5; ys <- y_new
@@ -657,7 +670,7 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
       for (int p = 0; p < NP; p++) {
         YB[p] += K[p] * T(B5);
         ERV(p) += K[p] * T(E5);
-        ys[p] = Y(p) + ht * YB[p];
+        ys[p] = YR(p) + ht * YB[p];
       }
       stage = 7;
     } else {  // K = f(t_new, y_new): error norm + step control (rk.py:138-173)
@@ -665,7 +678,7 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
 #pragma unroll
       for (int p = 0; p < NP; p++) {
         const V e = (ERV(p) + K[p] * T(E6)) * ht;
-        const V y0 = Y(p), y1 = ys[p];
+        const V y0 = YR(p), y1 = ys[p];
         V sc;
         sc.x = frcp(atol + fmax(fabs(y0.x), fabs(y1.x)) * rtol);
         sc.y = frcp(atol + fmax(fabs(y0.y), fabs(y1.y)) * rtol);
@@ -725,6 +738,7 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
 #undef Y
 #undef F
 #undef ERV
+#undef YR
   return result;
 }
 
