@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FWSIM_ABI_VERSION 1
+#define FWSIM_ABI_VERSION 2
 
 /* ---- error codes ---------------------------------------------------------- */
 #define FW_OK 0
@@ -187,7 +187,27 @@ typedef struct fw_env_config {
   int32_t term_present[3];
   int32_t pad_;
   fw_rew_factor rew[FW_MAX_REW];
+  /* streaming episode metrics (fixed_wing.py:1644-1736), reported per done env through
+   * fw_set_metrics_output; 0 = not tracked (no extra state traffic) */
+  int32_t metrics;
+  int32_t pad2_;
+  double rise_low, rise_high;         /* rise_time metric "low" / "high" (defaults 0.1, 0.9) */
 } fw_env_config;
+
+/* Episode-metric record written for every done env (row-major [N][FW_NMETRIC], handle
+ * precision); NaN where the reference yields NaN.  Per-target entries are (roll, pitch, Va),
+ * goal entries (roll, pitch, Va, all).                                                      */
+#define FW_M_RISE_TIME 0           /* 3 */
+#define FW_M_SETTLING_TIME 3       /* 4 */
+#define FW_M_OVERSHOOT 7           /* 3 */
+#define FW_M_TOTAL_ERROR 10        /* 3 */
+#define FW_M_AVG_ERROR 13          /* 3 */
+#define FW_M_CONTROL_VARIATION 16  /* 1 ("all") */
+#define FW_M_SUCCESS 17            /* 4 (0 / 1) */
+#define FW_M_SUCCESS_TIME_FRAC 21  /* 4 */
+#define FW_M_END_ERROR 25          /* 3 */
+#define FW_NMETRIC 28
+#define FW_M_END_WINDOW 50         /* end_error averages the last 50 errors */
 
 /* explicit reset inputs: SoA [FW_NINIT][N]; NaN = sample like an omitted dict key */
 enum fw_init_field {
@@ -259,6 +279,11 @@ int fw_set_state(fw_handle* h, int32_t block, const void* src_dev, void* stream)
 /* Curriculum / config update between steps (FixedWingAircraft.set_curriculum_level
  * recomputes ranges on the host and pushes a new env/sim config).            */
 int fw_update_config(fw_handle* h, const fw_sim_config* sim, const fw_env_config* env);
+
+/* Register the device buffer [N][FW_NMETRIC] that fw_env_step fills for done envs (the episode
+ * metrics of FixedWingAircraft.get_metric, fixed_wing.py:1644-1736, which the reference puts in
+ * info on done).  NULL stops the writes.  Requires env->metrics at create time. */
+int fw_set_metrics_output(fw_handle* h, void* metrics_dev);
 
 #ifdef __cplusplus
 }

@@ -419,6 +419,7 @@ def env_episode(env, rng, turb_on, n_steps, act_scale=1.2, omega_deg=60.0, polic
         else:
             a = np.array(pid_action(pid, env.simulator), dtype=np.float64)
         o, r, d, info = env.step(a)
+        env._last_info = info
         acts.append(np.asarray(a, dtype=np.float64))
         obs.append(o)
         rew.append(r)
@@ -506,8 +507,55 @@ def gen_pid_set(n_scen=40):
     print("pid set: lengths", lengths)
 
 
+METRIC_KEYS = {"rise_time": ["roll", "pitch", "Va"], "settling_time": ["roll", "pitch", "Va", "all"],
+               "overshoot": ["roll", "pitch", "Va"], "total_error": ["roll", "pitch", "Va"],
+               "avg_error": ["roll", "pitch", "Va"], "control_variation": ["all"],
+               "success": ["roll", "pitch", "Va", "all"], "success_time_frac": ["roll", "pitch", "Va", "all"],
+               "end_error": ["roll", "pitch", "Va"]}
+
+
+def gen_metrics():
+    """Episode metrics reported in info on done (fixed_wing.py:1644-1736), with the histories they
+    are computed from, for PID / random-action episodes that end by steps_max, success or failure."""
+    out = {}
+    rng = np.random.RandomState(4242)
+    cases = [
+        # name, turb, steps_max, policy, omega_deg, act_scale, config_kw
+        ("pid300", False, 300, "pid", 20.0, 1.0, {"action": {"scale_space": False}}),
+        ("pid_done", False, 1500, "pid", 20.0, 1.0,
+         {"action": {"scale_space": False},
+          "target": {"on_success": "done", "success_streak_fraction": 0.9, "success_streak_req": 60}}),
+        ("rand150", False, 150, "rand", 60.0, 1.2, None),
+        ("rand_fail", False, 2000, "rand", 700.0, 1.2, None),
+        ("pid_turb", True, 400, "pid", 20.0, 1.0, {"action": {"scale_space": False}}),
+        ("rand_short", False, 3, "rand", 60.0, 1.0, None),
+    ]
+    for name, turb, smax, pol, omd, asc, ckw in cases:
+        env = make_env(turb, smax, ckw)
+        ep = env_episode(env, rng, turb, smax + 5, act_scale=asc, omega_deg=omd, policy=pol)
+        assert ep["done"][-1], name
+        info = env._last_info
+        p = name + "__"
+        for k, v in ep.items():
+            out[p + k] = v
+        out[p + "steps_max"] = np.array(smax)
+        out[p + "turb_on"] = np.array(turb)
+        out[p + "scale_space"] = np.array(ckw is None or "action" not in ckw)
+        for m, keys in METRIC_KEYS.items():
+            out[p + "metric_" + m] = np.array([float(info[m][k]) for k in keys])
+        for k in ("roll", "pitch", "Va"):
+            out[p + "hist_error_" + k] = np.array(env.history["error"][k], dtype=np.float64)
+        for k in ("roll", "pitch", "Va", "all"):
+            out[p + "hist_goal_" + k] = np.array(env.history["goal"][k], dtype=np.float64)
+        out[p + "hist_command"] = np.array([env.simulator.state[a].history["command"]
+                                            for a in ("elevator", "aileron", "throttle")], dtype=np.float64)
+        print("metrics %s: %d steps, term=%r, success=%s" % (name, len(ep["rew"]), ep["term"][-1],
+                                                             out[p + "metric_success"]))
+    np.savez_compressed(os.path.join(OUT, "env_metrics.npz"), **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["single", "traj", "dryden", "env", "pidset"]
+    which = sys.argv[1:] or ["single", "traj", "dryden", "env", "pidset", "metrics"]
     if "single" in which:
         gen_single_step()
     if "traj" in which:
@@ -518,3 +566,5 @@ if __name__ == "__main__":
         gen_env_seq()
     if "pidset" in which:
         gen_pid_set()
+    if "metrics" in which:
+        gen_metrics()

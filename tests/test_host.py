@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(_native.SIGNATURES), "python signatures out of sync with include/fwsim.h"
-    assert lib.fw_abi_version() == 1
+    assert lib.fw_abi_version() == _native.ABI_VERSION
 
 
 def test_create_validates_without_device():

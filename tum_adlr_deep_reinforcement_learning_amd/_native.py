@@ -20,6 +20,7 @@ SOURCES = UNITS + [os.path.join(CSRC, "fw_device.hpp")] + HEADERS
 ARCH = os.environ.get("FWSIM_ARCH", "gfx950")
 
 _lib = None
+ABI_VERSION = 2  # include/fwsim.h FWSIM_ABI_VERSION
 
 
 class FwError(RuntimeError):
@@ -78,6 +79,7 @@ SIGNATURES = {
     "fw_get_state": (_c.c_int, [_vp, _i32, _vp, _vp]),
     "fw_set_state": (_c.c_int, [_vp, _i32, _vp, _vp]),
     "fw_update_config": (_c.c_int, [_vp, _vp, _vp]),
+    "fw_set_metrics_output": (_c.c_int, [_vp, _vp]),
     # include/fwrollout.h
     "fw_gae": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _c.c_double, _c.c_double, _vp, _vp, _vp]),
     "fw_moments_workspace_bytes": (_c.c_size_t, [_i64, _i32]),
@@ -105,7 +107,7 @@ def load(path=None):
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
-    if lib.fw_abi_version() != 1:
+    if lib.fw_abi_version() != ABI_VERSION:
         raise FwError("libfwsim ABI version mismatch")
     _lib = lib
     return lib

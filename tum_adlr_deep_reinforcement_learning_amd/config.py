@@ -64,6 +64,16 @@ FW_MAX_OBS, FW_MAX_REW, FW_MAX_WINDOW = 32, 8, 16
 
 FW_BLK_ODE, FW_BLK_DERIVED, FW_BLK_TARGET, FW_BLK_WIND, FW_BLK_STEPS, FW_BLK_COMMAND = range(6)
 
+# episode-metric record (include/fwsim.h FW_M_*): name -> (first column, info keys)
+FW_NMETRIC = 28
+METRIC_LAYOUT = {
+    "rise_time": (0, ["roll", "pitch", "Va"]), "settling_time": (3, ["roll", "pitch", "Va", "all"]),
+    "overshoot": (7, ["roll", "pitch", "Va"]), "total_error": (10, ["roll", "pitch", "Va"]),
+    "avg_error": (13, ["roll", "pitch", "Va"]), "control_variation": (16, ["all"]),
+    "success": (17, ["roll", "pitch", "Va", "all"]), "success_time_frac": (21, ["roll", "pitch", "Va", "all"]),
+    "end_error": (25, ["roll", "pitch", "Va"]),
+}
+
 # name of every variable slot (termination strings match the reference's
 # ConstraintException.variable, pyfly.py:11-16)
 VAR_NAMES = ["roll", "pitch", "yaw", "omega_p", "omega_q", "omega_r", "position_n", "position_e", "position_d",
@@ -126,7 +136,9 @@ class FwEnvConfig(ctypes.Structure):
                 ("step_fail_value", ctypes.c_double),
                 ("term_weight", ctypes.c_double * 3), ("term_present", ctypes.c_int32 * 3),
                 ("pad_", ctypes.c_int32),
-                ("rew", FwRewFactor * FW_MAX_REW)]
+                ("rew", FwRewFactor * FW_MAX_REW),
+                ("metrics", ctypes.c_int32), ("pad2_", ctypes.c_int32),
+                ("rise_low", ctypes.c_double), ("rise_high", ctypes.c_double)]
 
 
 # ---------------------------------------------------------------------------
@@ -449,6 +461,7 @@ class EnvSpec:
         if sim_keys:
             raise NotImplementedError("simulator parameter randomisation (%s)" % sorted(sim_keys))
         self.scale_actions = bool(cfg["action"].get("scale_space", False))
+        self.metrics_enabled = True  # track cfg["metrics"] on the device (False: skip that state traffic)
         self.set_curriculum_level(curriculum_level)
         self._build_spaces()
 
@@ -616,6 +629,14 @@ class EnvSpec:
             e.target_delta[i] = cv(p["delta"]) if p.get("delta") is not None else float("nan")
             e.target_bound[i] = cv(p["bound"]) if p.get("bound") is not None else float("nan")
         t = cfg["target"]
+        names = [m["name"] for m in cfg.get("metrics", [])]
+        unknown = set(names) - set(METRIC_LAYOUT)
+        if unknown:
+            raise NotImplementedError("metrics %s" % sorted(unknown))
+        e.metrics = int(bool(names) and self.metrics_enabled)
+        rise = [m for m in cfg.get("metrics", []) if m["name"] == "rise_time"]
+        e.rise_low = float(rise[0].get("low", 0.1)) if rise else 0.1
+        e.rise_high = float(rise[0].get("high", 0.9)) if rise else 0.9
         e.streak_req = int(t["success_streak_req"])
         if e.streak_req > 128:
             raise NotImplementedError("success_streak_req > 128")

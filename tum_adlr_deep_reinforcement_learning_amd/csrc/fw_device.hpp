@@ -97,6 +97,8 @@ struct DevCfg {
   T step_fail_value;
   T term_weight[3];
   int term_present[3];
+  int metrics;                         // streaming episode metrics tracked (fw_env_config.metrics)
+  T rise_low, rise_high;
   fw_obs_entry obs[FW_MAX_OBS];
   fw_rew_factor rew[FW_MAX_REW];
 };
@@ -970,6 +972,22 @@ FW_HD bool goal_all(const DevCfg<T>& c, const T* tgt, const T* vals) {
     if (!(fabs(err) <= c.target_bound[k])) all = false;
   }
   return all;
+}
+
+// _get_goal_status (fixed_wing.py:1346-1361) as bits: bit k = roll / pitch / Va within its bound
+// (targets without a bound report 0), bit 3 = "all" (all bounded targets; True if none)
+template <typename T>
+FW_HD uint32_t goal_status_bits(const DevCfg<T>& c, const T* tgt, const T* vals) {
+  uint32_t bits = 0, all = 1;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    if (!c.has_bound[k]) continue;
+    const T err = target_error(c, k, tgt[k], vals[k]);
+    const uint32_t ok = fabs(err) <= c.target_bound[k] ? 1u : 0u;
+    bits |= ok << k;
+    all &= ok;
+  }
+  return bits | (all << 3);
 }
 
 // _get_next_target (fixed_wing.py:1363-1471): constant / compensate(Va)

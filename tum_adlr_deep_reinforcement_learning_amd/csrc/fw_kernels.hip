@@ -73,7 +73,20 @@ struct State {
   int64_t noise_len;
   uint32_t key0, key1;  // Philox key = seed
   uint32_t env_offset;
+  T* met;             // [MT_ROWS][ld] streaming episode-metric sums (null: metrics off)
+  uint32_t* metu;     // [MU_ROWS][ld] their counters / indices
+  T* met_out;         // [N][FW_NMETRIC] record of done envs (null: not requested)
 };
+
+// streaming episode-metric state (fixed_wing.py:1644-1736 restated over running sums):
+// T rows
+constexpr int MR_E0 = 0, MR_ESUM = 3, MR_EABS = 6, MR_EMIN = 9, MR_EMAX = 12, MR_CV = 15, MR_RING = 16;
+constexpr int MT_ROWS = MR_RING + 3 * FW_M_END_WINDOW;
+// uint32 rows: error count, goal registers (roll/pitch/Va x 128 bit), goal counts (4),
+// settling index (4, ~0u = none), first crossings below the high / low rise limits (3 x 2)
+constexpr int MU_N = 0, MU_GB = 1, MU_GC = 13, MU_SET = 17, MU_RISE = 21;
+constexpr int MU_ROWS = MU_RISE + 6;
+constexpr uint32_t M_NONE = 0xFFFFFFFFu;
 
 template <typename T>
 __device__ __forceinline__ T ld_(const T* p, int64_t row, int64_t ld, int64_t i) {
@@ -234,6 +247,144 @@ __device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* 
 }
 
 // ---------------------------------------------------------------------------
+// Streaming episode metrics.  The reference keeps the whole episode history and
+// evaluates get_metric on done (fixed_wing.py:1644-1736); every metric it reports
+// is a function of running sums, extrema, first-crossing indices, the goal-status
+// shift registers and the last FW_M_END_WINDOW errors, which is what is kept per
+// aircraft here (history["error"] / ["goal"] entry 0 = the reset state, one entry
+// per successful step; one command per step).
+// ---------------------------------------------------------------------------
+// success / settling_time: the deque of the last `req` statuses is full and its mean >= frac
+template <typename T>
+__device__ __forceinline__ bool settled(const DevCfg<T>& c, const uint32_t g[4], uint32_t n) {
+  const int req = c.streak_req;
+  if (req <= 0 || (int64_t)n < req) return false;
+  int cnt = 0, rem = req;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const int take = rem >= 32 ? 32 : (rem > 0 ? rem : 0);
+    const uint32_t m = take == 32 ? 0xFFFFFFFFu : ((1u << take) - 1u);
+    cnt += __builtin_popcount(g[w] & m);
+    rem -= take;
+  }
+  return (double)cnt / (double)req >= (double)c.streak_frac;
+}
+
+template <typename T>
+__device__ __forceinline__ void metrics_init(const DevCfg<T>& c, const State<T>& s, int64_t i, const T* tgt,
+                                             const T* vals) {
+  const int64_t ld = s.ld;
+  const uint32_t gb = goal_status_bits(c, tgt, vals);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const T err = target_error(c, k, tgt[k], vals[k]);
+    st_(s.met, MR_E0 + k, ld, i, err);
+    st_(s.met, MR_ESUM + k, ld, i, err);
+    st_(s.met, MR_EABS + k, ld, i, T(fabs(err)));
+    st_(s.met, MR_EMIN + k, ld, i, err);
+    st_(s.met, MR_EMAX + k, ld, i, err);
+    st_(s.met, MR_RING + k, ld, i, err);
+  }
+  st_(s.met, MR_CV, ld, i, T(0));
+  st_(s.metu, MU_N, ld, i, 1u);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t bit = (gb >> k) & 1u;
+    uint32_t g[4] = {bit, 0u, 0u, 0u};
+    if (k < 3)
+#pragma unroll
+      for (int w = 0; w < 4; w++) st_(s.metu, MU_GB + 4 * k + w, ld, i, g[w]);
+    st_(s.metu, MU_GC + k, ld, i, bit);
+    st_(s.metu, MU_SET + k, ld, i, (c.streak_req > 0 && settled(c, g, 1u)) ? 0u : M_NONE);
+  }
+#pragma unroll
+  for (int r = 0; r < 6; r++) st_(s.metu, MU_RISE + r, ld, i, M_NONE);
+}
+
+// one successful step: errors w.r.t. the NEW targets (fixed_wing.py:575-579), goal statuses
+// `gb` w.r.t. the old ones (:534-537); gall = the updated "all" register
+template <typename T>
+__device__ __forceinline__ void metrics_step(const DevCfg<T>& c, const State<T>& s, int64_t i, const T* tgt,
+                                             const T* vals, uint32_t gb, const uint32_t gall[4]) {
+  const int64_t ld = s.ld;
+  const uint32_t n0 = ld_(s.metu, MU_N, ld, i), b = n0;  // index of the new history entry
+  const int slot = (int)(n0 % FW_M_END_WINDOW), pslot = (int)((n0 - 1) % FW_M_END_WINDOW);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const T err = target_error(c, k, tgt[k], vals[k]);
+    const T prev = ld_(s.met, MR_RING + 3 * pslot + k, ld, i);
+    const T e0 = ld_(s.met, MR_E0 + k, ld, i);
+    st_(s.met, MR_ESUM + k, ld, i, ld_(s.met, MR_ESUM + k, ld, i) + err);
+    st_(s.met, MR_EABS + k, ld, i, ld_(s.met, MR_EABS + k, ld, i) + T(fabs(err)));
+    st_(s.met, MR_EMIN + k, ld, i, fmin(ld_(s.met, MR_EMIN + k, ld, i), err));
+    st_(s.met, MR_EMAX + k, ld, i, fmax(ld_(s.met, MR_EMAX + k, ld, i), err));
+    st_(s.met, MR_RING + 3 * slot + k, ld, i, err);
+    // rise_time: earliest downward crossing of |error| through each limit
+    const T lims[2] = {T(fabs(c.rise_high * e0)), T(fabs(c.rise_low * e0))};
+#pragma unroll
+    for (int w = 0; w < 2; w++) {
+      const int row = MU_RISE + 2 * k + w;
+      if (ld_(s.metu, row, ld, i) == M_NONE && fabs(prev) >= lims[w] && fabs(err) < lims[w]) st_(s.metu, row, ld, i, b);
+    }
+  }
+  if (c.streak_req > 0) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t bit = (gb >> k) & 1u;
+      uint32_t g[4];
+      if (k < 3) {
+#pragma unroll
+        for (int w = 0; w < 4; w++) g[w] = ld_(s.metu, MU_GB + 4 * k + w, ld, i);
+        g[3] = (g[3] << 1) | (g[2] >> 31);
+        g[2] = (g[2] << 1) | (g[1] >> 31);
+        g[1] = (g[1] << 1) | (g[0] >> 31);
+        g[0] = (g[0] << 1) | bit;
+#pragma unroll
+        for (int w = 0; w < 4; w++) st_(s.metu, MU_GB + 4 * k + w, ld, i, g[w]);
+      } else {
+#pragma unroll
+        for (int w = 0; w < 4; w++) g[w] = gall[w];
+      }
+      st_(s.metu, MU_GC + k, ld, i, ld_(s.metu, MU_GC + k, ld, i) + bit);
+      if (ld_(s.metu, MU_SET + k, ld, i) == M_NONE && settled(c, g, n0 + 1u)) st_(s.metu, MU_SET + k, ld, i, b);
+    }
+  }
+  st_(s.metu, MU_N, ld, i, n0 + 1u);
+}
+
+// the record of a done episode (get_metric for every cfg metric), layout FW_M_* of fwsim.h
+template <typename T>
+__device__ __forceinline__ void metrics_final(const DevCfg<T>& c, const State<T>& s, int64_t i, int n_commands,
+                                              T* out) {
+  const int64_t ld = s.ld;
+  const T nan = T(NAN);
+  const uint32_t n = ld_(s.metu, MU_N, ld, i);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const T e0 = ld_(s.met, MR_E0 + k, ld, i);
+    const uint32_t rs = ld_(s.metu, MU_RISE + 2 * k, ld, i), re = ld_(s.metu, MU_RISE + 2 * k + 1, ld, i);
+    out[FW_M_RISE_TIME + k] = (rs != M_NONE && re != M_NONE) ? T((double)re - (double)rs) : nan;
+    const T m = e0 > T(0) ? ld_(s.met, MR_EMIN + k, ld, i) : ld_(s.met, MR_EMAX + k, ld, i);
+    out[FW_M_OVERSHOOT + k] = sgn(m) == sgn(e0) ? nan : T(fabs(m / e0));
+    out[FW_M_TOTAL_ERROR + k] = ld_(s.met, MR_EABS + k, ld, i);
+    out[FW_M_AVG_ERROR + k] = fabs(e0) >= T(0.01) ? T(fabs(ld_(s.met, MR_ESUM + k, ld, i) / (T)n / e0)) : nan;
+    const int cnt = n < (uint32_t)FW_M_END_WINDOW ? (int)n : FW_M_END_WINDOW;
+    T acc = T(0);
+    for (int j = 0; j < cnt; j++) acc += ld_(s.met, MR_RING + 3 * j + k, ld, i);
+    out[FW_M_END_ERROR + k] = T(fabs(acc / (T)cnt));
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t st = ld_(s.metu, MU_SET + k, ld, i);
+    out[FW_M_SETTLING_TIME + k] = st != M_NONE ? (T)st : nan;
+    out[FW_M_SUCCESS + k] = st != M_NONE ? T(1) : T(0);
+    out[FW_M_SUCCESS_TIME_FRAC + k] = (T)((double)ld_(s.metu, MU_GC + k, ld, i) / (double)n);
+  }
+  out[FW_M_CONTROL_VARIATION] =
+      n_commands >= 2 ? ld_(s.met, MR_CV, ld, i) / (T(3) * c.dt * (T)(n_commands - 1)) : nan;
+}
+
+// ---------------------------------------------------------------------------
 // reset of one lane: PyFly.reset (pyfly.py:1262-1311) + FixedWingAircraft.reset
 // (fixed_wing.py:414-481) incl. sample_target (:654-746).  init: FW_NINIT values
 // (NaN = sample) or null; tin: 3 targets (NaN = sample) or null.
@@ -372,6 +523,10 @@ __global__ __launch_bounds__(BLOCK) void k_reset(const DevCfg<T>* __restrict__ c
   T y[NY], der[8], wind[3], tgt[3] = {T(0), T(0), T(0)};
   reset_lane(c, s, i, init, tin, y, der, wind, tgt);
   store_env_fresh(c, s, i, y, der, wind, tgt);
+  if (c.has_env && c.metrics) {
+    const T vr[3] = {der[0], der[1], der[3]};
+    metrics_init(c, s, i, tgt, vr);
+  }
   if (obs && c.has_env) {
     T seq[RING + 1][3];
     observe(c, y, der, tgt, 0, seq, seq, obs + i * c.n_obs, 1);
@@ -572,10 +727,21 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
   T reward;
   uint32_t g[4];
   load_row(s.goal, 4, ld, i, g);
+  // command history (control_variation): one constrained command per step, success or not
+  if (c.metrics && steps0 >= 1) {
+    T cv = ld_(s.met, MR_CV, ld, i);
+#pragma unroll
+    for (int q = 0; q < 3; q++) cv += fabs(cmd[q] - ld_(s.cmd, q, ld, i));
+    st_(s.met, MR_CV, ld, i, cv);
+  }
+#pragma unroll
+  for (int q = 0; q < 3; q++) st_(s.cmd, q, ld, i, cmd[q]);
   if (sterm == 0) {
+    const T vals[3] = {der[0], der[1], der[3]};
+    uint32_t gb = 0;
     if (c.streak_req > 0) {
-      const T vals[3] = {der[0], der[1], der[3]};
-      const uint32_t bit = goal_all(c, tgt, vals) ? 1u : 0u;
+      gb = goal_status_bits(c, tgt, vals);
+      const uint32_t bit = (gb >> 3) & 1u;
       g[3] = (g[3] << 1) | (g[2] >> 31);
       g[2] = (g[2] << 1) | (g[1] >> 31);
       g[1] = (g[1] << 1) | (g[0] >> 31);
@@ -597,6 +763,7 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
     }
     reward = reward_of(c, y, der, tgt, steps, seqA);
     next_target(c, steps_tgt, tgt);
+    if (c.metrics) metrics_step(c, s, i, tgt, vals, gb, g);
   } else {
     done = true;
     reward = c.step_fail_timesteps ? (T)(steps - c.steps_max) : c.step_fail_value;
@@ -622,6 +789,7 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
     e[3] = tgt[1];
     e[4] = tgt[2];
   }
+  if (done && c.metrics && s.met_out) metrics_final(c, s, i, steps, s.met_out + i * FW_NMETRIC);
   // wavefront-uniform skip of the reset path when no lane of the wave is done
   const bool do_reset = done && auto_reset;
   if (__ballot(do_reset)) {
@@ -629,6 +797,10 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
       T yr[NY], dr[8], wr[3], tr[3];
       reset_lane(c, s, i, (const T*)nullptr, (const T*)nullptr, yr, dr, wr, tr);
       store_env_fresh(c, s, i, yr, dr, wr, tr);
+      if (c.metrics) {
+        const T vr[3] = {dr[0], dr[1], dr[3]};
+        metrics_init(c, s, i, tr, vr);
+      }
       T seq0[RING + 1][3];
       observe(c, yr, dr, tr, 0, seq0, seq0, orow, 1);
       return;
@@ -668,8 +840,11 @@ struct fw_handle {
   const void* noise = nullptr;
   int64_t noise_len = 0;
   int spec = 0;  // 0 = generic DevCfg kernels, 1 = GymX8Cfg, 2 = PyflyX8Cfg (structure matched at upload)
+  int metrics = 0;          // streaming episode-metric state allocated (env->metrics at create)
+  void* met_out = nullptr;  // [N][FW_NMETRIC] done-episode records (fw_set_metrics_output)
   // offsets (bytes) of the SoA blocks inside base
   size_t o_y, o_der, o_wind, o_target, o_cmd, o_epret, o_act, o_cmdring, o_steps, o_goal, o_episode;
+  size_t o_met = 0, o_metu = 0;
 };
 
 namespace {
@@ -816,6 +991,9 @@ void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
     }
     d.streak_frac = (T)e.streak_frac;
     d.step_fail_value = (T)e.step_fail_value;
+    d.metrics = h->metrics && e.metrics;
+    d.rise_low = (T)e.rise_low;
+    d.rise_high = (T)e.rise_high;
     std::memcpy(d.obs, e.obs, sizeof(d.obs));
     std::memcpy(d.rew, e.rew, sizeof(d.rew));
   }
@@ -909,6 +1087,9 @@ State<T> state_of(const fw_handle* h) {
   s.key0 = (uint32_t)(h->seed & 0xFFFFFFFFu);
   s.key1 = (uint32_t)(h->seed >> 32);
   s.env_offset = (uint32_t)h->env_offset;
+  s.met = h->metrics ? (T*)(b + h->o_met) : nullptr;
+  s.metu = h->metrics ? (uint32_t*)(b + h->o_metu) : nullptr;
+  s.met_out = (T*)h->met_out;
   return s;
 }
 
@@ -947,6 +1128,7 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
   h->ld = (n_envs + 63) / 64 * 64;
   h->sim = *sim;
   h->has_env = env != nullptr;
+  h->metrics = env != nullptr && env->metrics != 0;
   if (env) {
     h->env = *env;
     int wa = 1, wc = 0;
@@ -979,6 +1161,10 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
   h->o_steps = off; off += row32;
   h->o_goal = off; off += 4 * row32;
   h->o_episode = off; off += row32;
+  if (h->metrics) {
+    h->o_met = off; off += (size_t)MT_ROWS * row;
+    h->o_metu = off; off += (size_t)MU_ROWS * row32;
+  }
   // rows are ld elements apart: the padding above is folded into ld for simplicity
   h->base_bytes = off;
   e = hipMalloc(&h->base, off);
@@ -1055,6 +1241,8 @@ int fw_update_config(fw_handle* h, const fw_sim_config* sim, const fw_env_config
       if (env->rew[r].kind == FW_REW_ACTION_DELTA) wa = std::max(wa, env->rew[r].window - 1);
     if (wa != h->act_window || wc != h->cmd_window || env->n_obs != h->env.n_obs)
       return set_err(FW_E_UNSUPPORTED, "config update may not change observation layout or window sizes");
+    if (env->metrics && !h->metrics)
+      return set_err(FW_E_UNSUPPORTED, "episode metrics must be enabled when the handle is created");
     h->env = *env;
   }
   h->sim = *sim;
@@ -1122,6 +1310,13 @@ int fw_env_step(fw_handle* h, const void* actions_dev, void* obs_dev, void* rewa
                    (float*)reward_dev, done_dev, term_dev, (float*)terminal_obs_dev, (float*)episode_dev, stats_dev,
                    auto_reset);
   return check_launch();
+}
+
+int fw_set_metrics_output(fw_handle* h, void* metrics_dev) {
+  if (!h) return set_err(FW_E_INVALID, "NULL handle");
+  if (metrics_dev && !h->metrics) return set_err(FW_E_INVALID, "handle was created without episode metrics");
+  h->met_out = metrics_dev;
+  return FW_OK;
 }
 
 static int block_info(const fw_handle* h, int32_t block, size_t* off, int* rows, size_t* esz) {

@@ -55,6 +55,11 @@ class Engine:
         self.stats = torch.zeros(n, dtype=torch.int32, device=dev)
         self.success = torch.zeros(n, dtype=torch.uint8, device=dev)
         self.cmd_out = torch.zeros(n, 3, dtype=dt, device=dev)
+        # episode-metric records of done envs (fixed_wing.py:1644-1736), when the config lists metrics
+        self.metrics = None
+        if self._env_cfg is not None and self._env_cfg.metrics:
+            self.metrics = torch.full((n, C.FW_NMETRIC), float("nan"), dtype=dt, device=dev)
+            _native.check(self.lib.fw_set_metrics_output(self.h, _ptr(self.metrics)), "fw_set_metrics_output")
         self._noise = None
         self.seed(0)
 

@@ -3,8 +3,8 @@
 One aircraft on the GPU, stepped with ``auto_reset=False`` so ``step`` after
 ``done`` behaves like the reference (the caller resets).  ``info`` carries
 ``termination`` ("steps", "success" or the violated variable) and ``target``
-like fixed_wing.py:519-628.  The episode metrics of ``cfg["metrics"]``
-(fixed_wing.py:1644-1736) are not reported by this facade.
+like fixed_wing.py:519-628, plus the episode metrics of ``cfg["metrics"]``
+(fixed_wing.py:1644-1736) on done.
 """
 import numpy as np
 import torch
@@ -13,7 +13,7 @@ from . import config as C
 from .engine import Engine
 from .pyfly import SimulatorView
 from .spaces import Box
-from .vec_env import termination_name
+from .vec_env import metric_info, termination_name
 
 
 class FixedWingAircraft:
@@ -74,6 +74,9 @@ class FixedWingAircraft:
         info = {}
         if d:
             info["termination"] = termination_name(term[0].item(), tuple(self.spec.sim.dynamics))
+            if self.engine.metrics is not None:
+                info.update(metric_info(self.engine.metrics[0].cpu().numpy(),
+                                        [m["name"] for m in self.cfg.get("metrics", [])]))
         info["target"] = self.target
         return obs[0].cpu().numpy().astype(np.float32), float(rew[0].item()), d, info
 

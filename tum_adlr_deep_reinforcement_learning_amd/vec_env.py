@@ -80,17 +80,36 @@ def termination_name(code, dynamics=("elevon_right", "elevon_left", "throttle"))
     return "solver"
 
 
+def metric_info(row, names):
+    """One FW_NMETRIC record -> the info entries get_metric produces (fixed_wing.py:1644-1736)."""
+    out = {}
+    for name in names:
+        col, keys = C.METRIC_LAYOUT[name]
+        vals = {}
+        for j, k in enumerate(keys):
+            v = float(row[col + j])
+            if name == "success":
+                v = bool(v)
+            elif name in ("settling_time", "rise_time") and np.isfinite(v):
+                v = int(round(v))
+            vals[k] = v
+        out[name] = vals
+    return out
+
+
 class _Infos(collections.abc.Sequence):
     """Per-env info dicts, materialised on first access (65536 dicts per step are
     the dominant host cost of the SB3 surface, and most callers touch few)."""
 
-    def __init__(self, n, done, term, tobs, episode, targets, t_elapsed, dynamics, with_target):
+    def __init__(self, n, done, term, tobs, episode, targets, t_elapsed, dynamics, with_target, metrics=None,
+                 metric_names=()):
         self._n = n
         self._done, self._term, self._tobs, self._ep = done, term, tobs, episode
         self._tgt = targets
         self._t = t_elapsed
         self._dyn = dynamics
         self._with_target = with_target
+        self._met, self._met_names = metrics, metric_names
         self._cache = {}
 
     def __len__(self):
@@ -109,6 +128,8 @@ class _Infos(collections.abc.Sequence):
                 d["termination"] = termination_name(self._term[i], self._dyn)
                 ep = self._ep[i]
                 d["episode"] = {"r": round(float(ep[0]), 6), "l": int(round(float(ep[1]))), "t": round(self._t, 6)}
+                if self._met is not None:
+                    d.update(metric_info(self._met[i], self._met_names))
                 if self._with_target:
                     d["target"] = {"roll": float(ep[2]), "pitch": float(ep[3]), "Va": float(ep[4])}
             elif self._with_target:
@@ -189,8 +210,9 @@ class FixedWingVecEnv(VecEnv):
         tobs = eng.terminal_obs.cpu().numpy().astype(np.float32) if anyd else None
         ep = eng.episode.cpu().numpy() if anyd else None
         tgt = eng.get_block(C.FW_BLK_TARGET).cpu().numpy() if self.info_target else None
+        met = eng.metrics.cpu().numpy() if (anyd and eng.metrics is not None) else None
         return _Infos(self.num_envs, done_np, term, tobs, ep, tgt, time.time() - self._t_start, self._dyn,
-                      self.info_target)
+                      self.info_target, met, [m["name"] for m in self.spec.cfg.get("metrics", [])])
 
     def _infos_lazy_device(self):
         """Device mode: infos are built only if the caller asks for them (triggers a sync)."""
