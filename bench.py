@@ -52,7 +52,13 @@ def algorithmic_bytes_per_env_step(spec, esz=4):
         if f["class"] == "action" and f["type"] == "delta":
             act_window = max(act_window, int(f["window_size"]) - 1)
     rd = (19 + 2 + 3 + 3 + 3 + act_window * 3 + 1) * esz + (1 + 1 + 4) * 4
-    wr = (19 + 8 + 3 + 3 + 1 + spec.n_obs + 1) * esz + (1 + 4 + 1) * 4 + 1
+    wr = (19 + 8 + 3 + 3 + 3 + 1 + spec.n_obs + 1) * esz + (1 + 4 + 1) * 4 + 1  # incl. last command
+    if spec.cfg.get("metrics") and spec.metrics_enabled:
+        # streaming episode metrics (csrc/fw_kernels.hip metrics_step): previous command, control
+        # variation, e0/sum/|sum|/min/max x3, previous ring error x3 (T); count, 3 goal registers x4,
+        # goal counts x4, settling x4, rise crossings x6 (u32)
+        rd += (3 + 1 + 15 + 3) * esz + (1 + 12 + 4 + 4 + 6) * 4
+        wr += (1 + 12 + 3) * esz + (1 + 12 + 4) * 4
     return rd, wr
 
 
@@ -150,6 +156,8 @@ def main():
     ap.add_argument("--turbulence", action="store_true", help="light Dryden turbulence + random steady wind")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-metrics", action="store_true",
+                    help="do not track the config's streaming episode metrics (fixed_wing.py:1644-1736)")
     ap.add_argument("--rollout-steps", type=int, default=0,
                     help="also run one PPO collect_rollouts of this horizon (2048 = BASELINE configs[2]/[3])")
     args = ap.parse_args()
@@ -164,6 +172,7 @@ def main():
 
     # pyfly_config.json defaults: random steady wind |w| <= 8 m/s; Dryden only with --turbulence
     spec = C.EnvSpec(sim_config_kw={"turbulence": bool(args.turbulence), "turbulence_intensity": "light"})
+    spec.metrics_enabled = not args.no_metrics
     n = args.envs
     eng = Engine(spec.sim, spec, n, device=dev, precision=args.precision)
     eng.seed(1234, env_offset=rank * n)
@@ -208,7 +217,8 @@ def main():
             with open(pmc) as f:
                 pm = json.load(f)
             if pm.get("envs") == n and pm.get("precision") == args.precision and \
-                    bool(pm.get("turbulence")) == bool(args.turbulence):
+                    bool(pm.get("turbulence")) == bool(args.turbulence) and \
+                    bool(pm.get("metrics", True)) == bool(spec.metrics_enabled):
                 traffic = pm.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
@@ -238,7 +248,8 @@ def main():
             "config": {"workload": "FixedWingAircraft.step x %d aircraft per GPU (attitude task, fixed_wing_config "
                                    "defaults, %s, RK45 rtol=1e-3 atol=1e-6, auto-reset)"
                                    % (n, "light Dryden + steady wind" if args.turbulence else
-                                      "steady wind, turbulence off"),
+                                      "steady wind, turbulence off")
+                                   + (", streaming episode metrics" if spec.metrics_enabled else ""),
                        "envs_per_gpu": n, "global_envs": n * world, "kernel": "k_env_step",
                        "parallelism": "env-dp%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

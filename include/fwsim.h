@@ -194,8 +194,8 @@ typedef struct fw_env_config {
   double rise_low, rise_high;         /* rise_time metric "low" / "high" (defaults 0.1, 0.9) */
 } fw_env_config;
 
-/* Episode-metric record written for every done env (row-major [N][FW_NMETRIC], handle
- * precision); NaN where the reference yields NaN.  Per-target entries are (roll, pitch, Va),
+/* Episode-metric record written for every done env (SoA [FW_NMETRIC][N] so the stores
+ * coalesce; handle precision); NaN where the reference yields NaN.  Per-target entries are (roll, pitch, Va),
  * goal entries (roll, pitch, Va, all).                                                      */
 #define FW_M_RISE_TIME 0           /* 3 */
 #define FW_M_SETTLING_TIME 3       /* 4 */
@@ -280,7 +280,7 @@ int fw_set_state(fw_handle* h, int32_t block, const void* src_dev, void* stream)
  * recomputes ranges on the host and pushes a new env/sim config).            */
 int fw_update_config(fw_handle* h, const fw_sim_config* sim, const fw_env_config* env);
 
-/* Register the device buffer [N][FW_NMETRIC] that fw_env_step fills for done envs (the episode
+/* Register the device buffer [FW_NMETRIC][N] that fw_env_step fills for done envs (the episode
  * metrics of FixedWingAircraft.get_metric, fixed_wing.py:1644-1736, which the reference puts in
  * info on done).  NULL stops the writes.  Requires env->metrics at create time. */
 int fw_set_metrics_output(fw_handle* h, void* metrics_dev);

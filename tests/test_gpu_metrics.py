@@ -32,7 +32,7 @@ def test_device_metrics_match_reference(case):
         if bool(done[0]):
             break
     assert s == len(acts) - 1, "episode length differs from the reference"
-    row = eng.metrics[0].cpu().numpy()
+    row = eng.metrics[:, 0].cpu().numpy()
     for name, (col, keys) in C.METRIC_LAYOUT.items():
         got, want = row[col:col + len(keys)], g("metric_" + name)
         if name in ("success", "settling_time", "rise_time"):

@@ -19,6 +19,7 @@ from tum_adlr_deep_reinforcement_learning_amd.engine import Engine  # noqa: E402
 n = int(os.environ.get("TAIL_N", "65536"))
 steps = int(os.environ.get("TAIL_STEPS", "300"))
 spec = C.EnvSpec(sim_config_kw={"turbulence": False})
+spec.metrics_enabled = os.environ.get("TAIL_METRICS", "1") == "1"
 eng = Engine(spec.sim, spec, n, device="cuda:0", precision=os.environ.get("TAIL_PREC", "float32"))
 eng.seed(1234)
 eng.reset()

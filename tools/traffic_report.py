@@ -48,7 +48,7 @@ def main(base):
     alg = sum(bench.algorithmic_bytes_per_env_step(spec, 4)) * 65536
     out = {
         "kernel": "k_env_step", "workload": "65536 aircraft fp32, turbulence off, U(-1,1) actions",
-        "envs": 65536, "precision": "float32", "turbulence": False,
+        "envs": 65536, "precision": "float32", "turbulence": False, "metrics": bool(spec.metrics_enabled),
         "fetch_size_kib_per_launch": ef, "write_size_kib_per_launch": ew, "launches": [nf, nw],
         "calibration": {"fetch_kib_k_calib_read": cf, "write_kib_k_calib_write": cw, "factor_read": f_read,
                         "factor_write": f_write, "pattern": "4 B/lane SoA rows, coalesced"},

@@ -75,12 +75,14 @@ struct State {
   uint32_t env_offset;
   T* met;             // [MT_ROWS][ld] streaming episode-metric sums (null: metrics off)
   uint32_t* metu;     // [MU_ROWS][ld] their counters / indices
-  T* met_out;         // [N][FW_NMETRIC] record of done envs (null: not requested)
+  T* met_out;         // [FW_NMETRIC][N] (SoA) record of done envs (null: not requested)
 };
 
 // streaming episode-metric state (fixed_wing.py:1644-1736 restated over running sums):
-// T rows
-constexpr int MR_E0 = 0, MR_ESUM = 3, MR_EABS = 6, MR_EMIN = 9, MR_EMAX = 12, MR_CV = 15, MR_RING = 16;
+// T rows: e0, sum, |sum|, min, max, previous error, sum of the last FW_M_END_WINDOW errors
+// (x3 targets), control variation, ring of the last FW_M_END_WINDOW errors
+constexpr int MR_E0 = 0, MR_ESUM = 3, MR_EABS = 6, MR_EMIN = 9, MR_EMAX = 12, MR_PREV = 15, MR_WSUM = 18, MR_CV = 21,
+              MR_RING = 22;
 constexpr int MT_ROWS = MR_RING + 3 * FW_M_END_WINDOW;
 // uint32 rows: error count, goal registers (roll/pitch/Va x 128 bit), goal counts (4),
 // settling index (4, ~0u = none), first crossings below the high / low rise limits (3 x 2)
@@ -283,6 +285,8 @@ __device__ __forceinline__ void metrics_init(const DevCfg<T>& c, const State<T>&
     st_(s.met, MR_EABS + k, ld, i, T(fabs(err)));
     st_(s.met, MR_EMIN + k, ld, i, err);
     st_(s.met, MR_EMAX + k, ld, i, err);
+    st_(s.met, MR_PREV + k, ld, i, err);
+    st_(s.met, MR_WSUM + k, ld, i, err);
     st_(s.met, MR_RING + k, ld, i, err);
   }
   st_(s.met, MR_CV, ld, i, T(0));
@@ -301,30 +305,63 @@ __device__ __forceinline__ void metrics_init(const DevCfg<T>& c, const State<T>&
   for (int r = 0; r < 6; r++) st_(s.metu, MU_RISE + r, ld, i, M_NONE);
 }
 
-// one successful step: errors w.r.t. the NEW targets (fixed_wing.py:575-579), goal statuses
-// `gb` w.r.t. the old ones (:534-537); gall = the updated "all" register
+// The per-step metric state of one aircraft, loaded with ONE batch of independent loads
+// (no load depends on another, none follows a store) and written back in one batch.
 template <typename T>
-__device__ __forceinline__ void metrics_step(const DevCfg<T>& c, const State<T>& s, int64_t i, const T* tgt,
-                                             const T* vals, uint32_t gb, const uint32_t gall[4]) {
-  const int64_t ld = s.ld;
-  const uint32_t n0 = ld_(s.metu, MU_N, ld, i), b = n0;  // index of the new history entry
-  const int slot = (int)(n0 % FW_M_END_WINDOW), pslot = (int)((n0 - 1) % FW_M_END_WINDOW);
+struct Met {
+  T row[MR_RING];          // e0 / sum / |sum| / min / max / prev / window sum (x3), cv
+  uint32_t u[MU_ROWS];     // count, goal registers, goal counts, settling, rise
+  T old[3];                // ring entries the next error overwrites (slot `slot`)
+  int slot;
+  // `slot` is known before the count is loaded: within an episode every step but a terminal
+  // failure appends an error, so the new entry's index is steps0 + 1
+  __device__ __forceinline__ void load(const State<T>& s, int64_t i, int steps0) {
+#pragma unroll
+    for (int r = 0; r < MR_RING; r++) row[r] = ld_(s.met, r, s.ld, i);
+#pragma unroll
+    for (int r = 0; r < MU_ROWS; r++) u[r] = ld_(s.metu, r, s.ld, i);
+    slot = (steps0 + 1) % FW_M_END_WINDOW;
+#pragma unroll
+    for (int k = 0; k < 3; k++) old[k] = ld_(s.met, MR_RING + 3 * slot + k, s.ld, i);
+  }
+  __device__ __forceinline__ void store(const State<T>& s, int64_t i) const {
+#pragma unroll
+    for (int r = 0; r < MR_RING; r++) st_(s.met, r, s.ld, i, row[r]);
+#pragma unroll
+    for (int r = 0; r < MU_ROWS; r++) st_(s.metu, r, s.ld, i, u[r]);
+  }
+};
+
+// one successful step: errors w.r.t. the NEW targets (fixed_wing.py:575-579), goal statuses
+// `gb` w.r.t. the old ones (:534-537); gall = the updated "all" register.  Writes the new
+// error into the end-error ring.
+template <typename T>
+__device__ __forceinline__ void metrics_step(const DevCfg<T>& c, const State<T>& s, int64_t i, Met<T>& M,
+                                             const T* tgt, const T* vals, uint32_t gb, const uint32_t gall[4]) {
+  const uint32_t n0 = M.u[MU_N], b = n0;  // index of the new history entry
+  const int slot = (int)(n0 % FW_M_END_WINDOW);
+  if (slot != M.slot) {  // stepping on after a failed (done) step without reset: re-read
+    M.slot = slot;
+#pragma unroll
+    for (int k = 0; k < 3; k++) M.old[k] = ld_(s.met, MR_RING + 3 * slot + k, s.ld, i);
+  }
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     const T err = target_error(c, k, tgt[k], vals[k]);
-    const T prev = ld_(s.met, MR_RING + 3 * pslot + k, ld, i);
-    const T e0 = ld_(s.met, MR_E0 + k, ld, i);
-    st_(s.met, MR_ESUM + k, ld, i, ld_(s.met, MR_ESUM + k, ld, i) + err);
-    st_(s.met, MR_EABS + k, ld, i, ld_(s.met, MR_EABS + k, ld, i) + T(fabs(err)));
-    st_(s.met, MR_EMIN + k, ld, i, fmin(ld_(s.met, MR_EMIN + k, ld, i), err));
-    st_(s.met, MR_EMAX + k, ld, i, fmax(ld_(s.met, MR_EMAX + k, ld, i), err));
-    st_(s.met, MR_RING + 3 * slot + k, ld, i, err);
+    const T prev = M.row[MR_PREV + k], e0 = M.row[MR_E0 + k];
+    M.row[MR_ESUM + k] += err;
+    M.row[MR_EABS + k] += T(fabs(err));
+    M.row[MR_EMIN + k] = fmin(M.row[MR_EMIN + k], err);
+    M.row[MR_EMAX + k] = fmax(M.row[MR_EMAX + k], err);
+    M.row[MR_PREV + k] = err;
+    M.row[MR_WSUM + k] += n0 >= (uint32_t)FW_M_END_WINDOW ? err - M.old[k] : err;
+    st_(s.met, MR_RING + 3 * slot + k, s.ld, i, err);
     // rise_time: earliest downward crossing of |error| through each limit
     const T lims[2] = {T(fabs(c.rise_high * e0)), T(fabs(c.rise_low * e0))};
 #pragma unroll
     for (int w = 0; w < 2; w++) {
-      const int row = MU_RISE + 2 * k + w;
-      if (ld_(s.metu, row, ld, i) == M_NONE && fabs(prev) >= lims[w] && fabs(err) < lims[w]) st_(s.metu, row, ld, i, b);
+      uint32_t& r = M.u[MU_RISE + 2 * k + w];
+      if (r == M_NONE && fabs(prev) >= lims[w] && fabs(err) < lims[w]) r = b;
     }
   }
   if (c.streak_req > 0) {
@@ -333,55 +370,51 @@ __device__ __forceinline__ void metrics_step(const DevCfg<T>& c, const State<T>&
       const uint32_t bit = (gb >> k) & 1u;
       uint32_t g[4];
       if (k < 3) {
+        uint32_t* R = M.u + MU_GB + 4 * k;
+        R[3] = (R[3] << 1) | (R[2] >> 31);
+        R[2] = (R[2] << 1) | (R[1] >> 31);
+        R[1] = (R[1] << 1) | (R[0] >> 31);
+        R[0] = (R[0] << 1) | bit;
 #pragma unroll
-        for (int w = 0; w < 4; w++) g[w] = ld_(s.metu, MU_GB + 4 * k + w, ld, i);
-        g[3] = (g[3] << 1) | (g[2] >> 31);
-        g[2] = (g[2] << 1) | (g[1] >> 31);
-        g[1] = (g[1] << 1) | (g[0] >> 31);
-        g[0] = (g[0] << 1) | bit;
-#pragma unroll
-        for (int w = 0; w < 4; w++) st_(s.metu, MU_GB + 4 * k + w, ld, i, g[w]);
+        for (int w = 0; w < 4; w++) g[w] = R[w];
       } else {
 #pragma unroll
         for (int w = 0; w < 4; w++) g[w] = gall[w];
       }
-      st_(s.metu, MU_GC + k, ld, i, ld_(s.metu, MU_GC + k, ld, i) + bit);
-      if (ld_(s.metu, MU_SET + k, ld, i) == M_NONE && settled(c, g, n0 + 1u)) st_(s.metu, MU_SET + k, ld, i, b);
+      M.u[MU_GC + k] += bit;
+      if (M.u[MU_SET + k] == M_NONE && settled(c, g, n0 + 1u)) M.u[MU_SET + k] = b;
     }
   }
-  st_(s.metu, MU_N, ld, i, n0 + 1u);
+  M.u[MU_N] = n0 + 1u;
 }
 
 // the record of a done episode (get_metric for every cfg metric), layout FW_M_* of fwsim.h
+// out: column of the SoA record [FW_NMETRIC][N] (element m at out[m * stride])
 template <typename T>
-__device__ __forceinline__ void metrics_final(const DevCfg<T>& c, const State<T>& s, int64_t i, int n_commands,
-                                              T* out) {
-  const int64_t ld = s.ld;
+__device__ __forceinline__ void metrics_final(const DevCfg<T>& c, const Met<T>& M, int n_commands, T* out,
+                                              int64_t stride) {
   const T nan = T(NAN);
-  const uint32_t n = ld_(s.metu, MU_N, ld, i);
+  const uint32_t n = M.u[MU_N];
+  const int cnt = n < (uint32_t)FW_M_END_WINDOW ? (int)n : FW_M_END_WINDOW;
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    const T e0 = ld_(s.met, MR_E0 + k, ld, i);
-    const uint32_t rs = ld_(s.metu, MU_RISE + 2 * k, ld, i), re = ld_(s.metu, MU_RISE + 2 * k + 1, ld, i);
-    out[FW_M_RISE_TIME + k] = (rs != M_NONE && re != M_NONE) ? T((double)re - (double)rs) : nan;
-    const T m = e0 > T(0) ? ld_(s.met, MR_EMIN + k, ld, i) : ld_(s.met, MR_EMAX + k, ld, i);
-    out[FW_M_OVERSHOOT + k] = sgn(m) == sgn(e0) ? nan : T(fabs(m / e0));
-    out[FW_M_TOTAL_ERROR + k] = ld_(s.met, MR_EABS + k, ld, i);
-    out[FW_M_AVG_ERROR + k] = fabs(e0) >= T(0.01) ? T(fabs(ld_(s.met, MR_ESUM + k, ld, i) / (T)n / e0)) : nan;
-    const int cnt = n < (uint32_t)FW_M_END_WINDOW ? (int)n : FW_M_END_WINDOW;
-    T acc = T(0);
-    for (int j = 0; j < cnt; j++) acc += ld_(s.met, MR_RING + 3 * j + k, ld, i);
-    out[FW_M_END_ERROR + k] = T(fabs(acc / (T)cnt));
+    const T e0 = M.row[MR_E0 + k];
+    const uint32_t rs = M.u[MU_RISE + 2 * k], re = M.u[MU_RISE + 2 * k + 1];
+    out[(FW_M_RISE_TIME + k) * stride] = (rs != M_NONE && re != M_NONE) ? T((double)re - (double)rs) : nan;
+    const T m = e0 > T(0) ? M.row[MR_EMIN + k] : M.row[MR_EMAX + k];
+    out[(FW_M_OVERSHOOT + k) * stride] = sgn(m) == sgn(e0) ? nan : T(fabs(m / e0));
+    out[(FW_M_TOTAL_ERROR + k) * stride] = M.row[MR_EABS + k];
+    out[(FW_M_AVG_ERROR + k) * stride] = fabs(e0) >= T(0.01) ? T(fabs(M.row[MR_ESUM + k] / (T)n / e0)) : nan;
+    out[(FW_M_END_ERROR + k) * stride] = T(fabs(M.row[MR_WSUM + k] / (T)cnt));
   }
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    const uint32_t st = ld_(s.metu, MU_SET + k, ld, i);
-    out[FW_M_SETTLING_TIME + k] = st != M_NONE ? (T)st : nan;
-    out[FW_M_SUCCESS + k] = st != M_NONE ? T(1) : T(0);
-    out[FW_M_SUCCESS_TIME_FRAC + k] = (T)((double)ld_(s.metu, MU_GC + k, ld, i) / (double)n);
+    const uint32_t st = M.u[MU_SET + k];
+    out[(FW_M_SETTLING_TIME + k) * stride] = st != M_NONE ? (T)st : nan;
+    out[(FW_M_SUCCESS + k) * stride] = st != M_NONE ? T(1) : T(0);
+    out[(FW_M_SUCCESS_TIME_FRAC + k) * stride] = (T)((double)M.u[MU_GC + k] / (double)n);
   }
-  out[FW_M_CONTROL_VARIATION] =
-      n_commands >= 2 ? ld_(s.met, MR_CV, ld, i) / (T(3) * c.dt * (T)(n_commands - 1)) : nan;
+  out[FW_M_CONTROL_VARIATION * stride] = n_commands >= 2 ? M.row[MR_CV] / (T(3) * c.dt * (T)(n_commands - 1)) : nan;
 }
 
 // ---------------------------------------------------------------------------
@@ -728,11 +761,14 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
   uint32_t g[4];
   load_row(s.goal, 4, ld, i, g);
   // command history (control_variation): one constrained command per step, success or not
-  if (c.metrics && steps0 >= 1) {
-    T cv = ld_(s.met, MR_CV, ld, i);
+  Met<T> M;
+  if (c.metrics) {
+    M.load(s, i, steps0);
+    T prev_cmd[3];
+    load_row(s.cmd, 3, ld, i, prev_cmd);
+    if (steps0 >= 1)
 #pragma unroll
-    for (int q = 0; q < 3; q++) cv += fabs(cmd[q] - ld_(s.cmd, q, ld, i));
-    st_(s.met, MR_CV, ld, i, cv);
+      for (int q = 0; q < 3; q++) M.row[MR_CV] += fabs(cmd[q] - prev_cmd[q]);
   }
 #pragma unroll
   for (int q = 0; q < 3; q++) st_(s.cmd, q, ld, i, cmd[q]);
@@ -763,7 +799,9 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
     }
     reward = reward_of(c, y, der, tgt, steps, seqA);
     next_target(c, steps_tgt, tgt);
-    if (c.metrics) metrics_step(c, s, i, tgt, vals, gb, g);
+#ifndef FW_MET_SKIP_STEP
+    if (c.metrics) metrics_step(c, s, i, M, tgt, vals, gb, g);
+#endif
   } else {
     done = true;
     reward = c.step_fail_timesteps ? (T)(steps - c.steps_max) : c.step_fail_value;
@@ -789,7 +827,14 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
     e[3] = tgt[1];
     e[4] = tgt[2];
   }
-  if (done && c.metrics && s.met_out) metrics_final(c, s, i, steps, s.met_out + i * FW_NMETRIC);
+  if (c.metrics) {
+#ifndef FW_MET_SKIP_STORE
+    M.store(s, i);
+#endif
+#ifndef FW_MET_SKIP_FINAL
+    if (done && s.met_out) metrics_final(c, M, steps, s.met_out + i, s.n);
+#endif
+  }
   // wavefront-uniform skip of the reset path when no lane of the wave is done
   const bool do_reset = done && auto_reset;
   if (__ballot(do_reset)) {
@@ -797,10 +842,12 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
       T yr[NY], dr[8], wr[3], tr[3];
       reset_lane(c, s, i, (const T*)nullptr, (const T*)nullptr, yr, dr, wr, tr);
       store_env_fresh(c, s, i, yr, dr, wr, tr);
+#ifndef FW_MET_SKIP_INIT
       if (c.metrics) {
         const T vr[3] = {dr[0], dr[1], dr[3]};
         metrics_init(c, s, i, tr, vr);
       }
+#endif
       T seq0[RING + 1][3];
       observe(c, yr, dr, tr, 0, seq0, seq0, orow, 1);
       return;
@@ -841,7 +888,7 @@ struct fw_handle {
   int64_t noise_len = 0;
   int spec = 0;  // 0 = generic DevCfg kernels, 1 = GymX8Cfg, 2 = PyflyX8Cfg (structure matched at upload)
   int metrics = 0;          // streaming episode-metric state allocated (env->metrics at create)
-  void* met_out = nullptr;  // [N][FW_NMETRIC] done-episode records (fw_set_metrics_output)
+  void* met_out = nullptr;  // [FW_NMETRIC][N] done-episode records (fw_set_metrics_output)
   // offsets (bytes) of the SoA blocks inside base
   size_t o_y, o_der, o_wind, o_target, o_cmd, o_epret, o_act, o_cmdring, o_steps, o_goal, o_episode;
   size_t o_met = 0, o_metu = 0;

@@ -58,7 +58,7 @@ class Engine:
         # episode-metric records of done envs (fixed_wing.py:1644-1736), when the config lists metrics
         self.metrics = None
         if self._env_cfg is not None and self._env_cfg.metrics:
-            self.metrics = torch.full((n, C.FW_NMETRIC), float("nan"), dtype=dt, device=dev)
+            self.metrics = torch.full((C.FW_NMETRIC, n), float("nan"), dtype=dt, device=dev)  # SoA
             _native.check(self.lib.fw_set_metrics_output(self.h, _ptr(self.metrics)), "fw_set_metrics_output")
         self._noise = None
         self.seed(0)

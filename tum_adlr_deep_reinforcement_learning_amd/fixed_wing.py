@@ -75,7 +75,7 @@ class FixedWingAircraft:
         if d:
             info["termination"] = termination_name(term[0].item(), tuple(self.spec.sim.dynamics))
             if self.engine.metrics is not None:
-                info.update(metric_info(self.engine.metrics[0].cpu().numpy(),
+                info.update(metric_info(self.engine.metrics[:, 0].cpu().numpy(),
                                         [m["name"] for m in self.cfg.get("metrics", [])]))
         info["target"] = self.target
         return obs[0].cpu().numpy().astype(np.float32), float(rew[0].item()), d, info

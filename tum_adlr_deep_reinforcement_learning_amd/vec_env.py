@@ -129,7 +129,7 @@ class _Infos(collections.abc.Sequence):
                 ep = self._ep[i]
                 d["episode"] = {"r": round(float(ep[0]), 6), "l": int(round(float(ep[1]))), "t": round(self._t, 6)}
                 if self._met is not None:
-                    d.update(metric_info(self._met[i], self._met_names))
+                    d.update(metric_info(self._met[:, i], self._met_names))
                 if self._with_target:
                     d["target"] = {"roll": float(ep[2]), "pitch": float(ep[3]), "Va": float(ep[4])}
             elif self._with_target:
