@@ -90,6 +90,22 @@ constexpr int MU_N = 0, MU_GB = 1, MU_GC = 13, MU_SET = 17, MU_RISE = 21;
 constexpr int MU_ROWS = MU_RISE + 6;
 constexpr uint32_t M_NONE = 0xFFFFFFFFu;
 
+// Debug build only (-DFW_TIMING, tools/phase_timing.py): lane 0 of every wave stamps the
+// 100 MHz real-time clock at phase boundaries into the episode_out buffer (8 x u64 per wave),
+// after draining all outstanding memory operations.
+#ifdef FW_TIMING
+#define FW_TSTAMP(k)                                                                                 \
+  do {                                                                                               \
+    __builtin_amdgcn_s_waitcnt(0);                                                                   \
+    if ((threadIdx.x & 63) == 0 && episode_out)                                                      \
+      ((unsigned long long*)episode_out)[(i >> 6) * 8 + (k)] = __builtin_amdgcn_s_memrealtime();     \
+  } while (0)
+#else
+#define FW_TSTAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 template <typename T>
 __device__ __forceinline__ T ld_(const T* p, int64_t row, int64_t ld, int64_t i) {
   return p[row * ld + i];
@@ -669,6 +685,7 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
   if (i >= s.n) return;
   const C& c = *reinterpret_cast<const C*>(cfgp);  // structural specialisation view (fw_device.hpp SpecCfg)
   const int64_t ld = s.ld;
+  FW_TSTAMP(0);
 
   T y[NY], der[8], wind[3], tgt[3], a[3];
   load_row(s.y, NY, ld, i, y);
@@ -691,6 +708,7 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
   // ---- PyFly.step ----
   T tl[3], ta[3];
   turbulence_at(c, s, i, episode, steps0, tl, ta);
+  FW_TSTAMP(1);
   int nfev = 0, nacc = 0;
   uint32_t dmask = 0;
 #if FW_LDS_STATE
@@ -708,6 +726,7 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
   load_row(s.target, 3, ld, i, tgt);
 #pragma unroll
   for (int q = 0; q < 3; q++) a[q] = actions[i * 3 + q];
+  FW_TSTAMP(2);
   if (sterm) {
 #pragma unroll
     for (int r = 0; r < 6; r++)
@@ -835,6 +854,7 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
     if (done && s.met_out) metrics_final(c, M, steps, s.met_out + i, s.n);
 #endif
   }
+  FW_TSTAMP(3);
   // wavefront-uniform skip of the reset path when no lane of the wave is done
   const bool do_reset = done && auto_reset;
   if (__ballot(do_reset)) {
@@ -850,10 +870,13 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
 #endif
       T seq0[RING + 1][3];
       observe(c, yr, dr, tr, 0, seq0, seq0, orow, 1);
+      FW_TSTAMP(5);
       return;
     }
   }
+#ifndef FW_SKIP_OBS
   observe(c, y, der, tgt, steps, seqA, seqC, orow, 1);
+#endif
 #pragma unroll
   for (int r = 0; r < NY; r++) st_(s.y, r, ld, i, y[r]);
 #pragma unroll
@@ -864,6 +887,7 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
   for (int w = 0; w < 4; w++) st_(s.goal, w, ld, i, g[w]);
   st_(s.ep_ret, 0, ld, i, ep_ret);
   s.steps[i] = (uint32_t)(steps & 0xFFFF) | ((uint32_t)(steps_tgt & 0xFFFF) << 16);
+  FW_TSTAMP(4);
 }
 
 }  // namespace
