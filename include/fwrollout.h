@@ -17,6 +17,7 @@
  *                     merged over ranks (the global batch of a sharded VecEnv)
  *   fw_vecnorm_apply  VecNormalize.step_wait's normalisation + return reset
  *                     stable_baselines3/common/vec_env/vec_normalize.py:106-131, 133-169
+ *   fw_replay_add     ReplayBuffer.add   stable_baselines3/common/buffers.py:222-235
  */
 #ifndef FWROLLOUT_H
 #define FWROLLOUT_H
@@ -66,6 +67,18 @@ int fw_vecnorm_apply(const float* obs, int64_t n, int32_t d, int64_t ldx, const 
                      int32_t norm_obs, double clip_obs, float* obs_out, int64_t ld_out, const float* rew,
                      int32_t norm_rew, double clip_rew, float* rew_out, const uint8_t* done, double* ret,
                      void* stream);
+
+/* ReplayBuffer.add (stable_baselines3/common/buffers.py:222-235) for n_envs transitions at once:
+ * one launch copies up to FW_MAX_COPY_SEGS device ranges (obs, next_obs, action, reward, done of
+ * the current step into their replay slots).  Ranges must not overlap; bytes % 4 == 0; 16-byte
+ * aligned ranges move as 16-byte vectors. */
+#define FW_MAX_COPY_SEGS 8
+typedef struct fw_copy_seg {
+  const void* src;
+  void* dst;
+  int64_t bytes;
+} fw_copy_seg;
+int fw_replay_add(const fw_copy_seg* segs, int32_t n_segs, void* stream);
 
 #ifdef __cplusplus
 }

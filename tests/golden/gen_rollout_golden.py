@@ -16,6 +16,7 @@ Usage:  python tests/golden/gen_rollout_golden.py
 Fixtures:
   rollout_gae.npz    RolloutBuffer.add x T + compute_returns_and_advantage, several (T, N, gamma, lambda)
   vecnormalize.npz   VecNormalize(reset + K step_wait) over a scripted VecEnv: normalised obs/rewards, rms states
+  replay.npz         ReplayBuffer add sequence (wrap-around) + _get_samples, optimize_memory_usage on/off
 """
 import os
 import sys
@@ -216,9 +217,43 @@ def gen_vecnormalize(VecEnv, VecNormalize, gym):
                         gamma=0.99, clip_obs=10.0, clip_reward=10.0, epsilon=1e-8)
 
 
+def gen_replay(gym):
+    """ReplayBuffer (n_envs = 1) add sequence that wraps around, then _get_samples on every slot,
+    with and without optimize_memory_usage (buffers.py:151-257)."""
+    from stable_baselines3.common.buffers import ReplayBuffer
+    rng = np.random.RandomState(77)
+    B, K = 7, 11
+    obs_space = gym.spaces.Box(-np.inf, np.inf, shape=(14,), dtype=np.float32)
+    act_space = gym.spaces.Box(-1.0, 1.0, shape=(3,), dtype=np.float32)
+    out = {}
+    adds = {"obs": rng.randn(K, 14).astype(np.float32), "next_obs": rng.randn(K, 14).astype(np.float32),
+            "action": rng.uniform(-1, 1, (K, 3)).astype(np.float32), "reward": rng.randn(K),
+            "done": (rng.rand(K) < 0.3)}
+    for k, v in adds.items():
+        out["add_" + k] = v
+    for opt in (False, True):
+        buf = ReplayBuffer(B, obs_space, act_space, device="cpu", n_envs=1, optimize_memory_usage=opt)
+        for t in range(K):
+            buf.add(adds["obs"][t][None], adds["next_obs"][t][None], adds["action"][t][None],
+                    np.array([adds["reward"][t]]), np.array([adds["done"][t]]))
+        inds = np.arange(B)
+        s = buf._get_samples(inds)
+        p = "opt%d__" % int(opt)
+        out[p + "pos"] = np.array(buf.pos)
+        out[p + "full"] = np.array(buf.full)
+        for name, t in zip(["observations", "actions", "next_observations", "dones", "rewards"], s):
+            out[p + name] = t.numpy()
+    np.savez_compressed(os.path.join(OUT, "replay.npz"), **out)
+
+
 if __name__ == "__main__":
     gym = _install_gym_stub()
     RolloutBuffer, RunningMeanStd, VecEnv, VecNormalize = _import_sb3()
-    gen_gae(RolloutBuffer, gym)
-    gen_vecnormalize(VecEnv, VecNormalize, gym)
-    print("wrote rollout_gae.npz, vecnormalize.npz")
+    which = sys.argv[1:] or ["gae", "vecnormalize", "replay"]
+    if "gae" in which:
+        gen_gae(RolloutBuffer, gym)
+    if "vecnormalize" in which:
+        gen_vecnormalize(VecEnv, VecNormalize, gym)
+    if "replay" in which:
+        gen_replay(gym)
+    print("wrote", which)

@@ -87,7 +87,12 @@ SIGNATURES = {
     "fw_rms_update": (_c.c_int, [_vp, _i32, _i32, _i32, _vp, _i32, _i32, _vp]),
     "fw_vecnorm_apply": (_c.c_int, [_vp, _i64, _i32, _i64, _vp, _c.c_double, _i32, _c.c_double, _vp, _i64, _vp, _i32,
                                     _c.c_double, _vp, _vp, _vp, _vp]),
+    "fw_replay_add": (_c.c_int, [_vp, _i32, _vp]),
 }
+
+
+class FwCopySeg(ctypes.Structure):  # include/fwrollout.h fw_copy_seg
+    _fields_ = [("src", _vp), ("dst", _vp), ("bytes", _i64)]
 
 
 def load(path=None):

@@ -12,6 +12,7 @@
 //                      moment records (the RCCL all-gather of a sharded batch).
 //   k_vecnorm_apply    VecNormalize.normalize_obs / normalize_reward + ret[news] = 0
 //                      (vec_normalize.py:106-131, 133-169).
+//   k_copy_segs        ReplayBuffer.add (buffers.py:222-235): all fields of one step, one launch.
 //
 // Floating point follows the reference's numpy promotions exactly where the reference
 // is deterministic (GAE: bit-exact), so contraction into FMA is disabled in this file.
@@ -272,6 +273,34 @@ __global__ __launch_bounds__(BLOCK) void k_vecnorm_apply(const float* __restrict
   if (done && retv && done[i]) retv[i] = 0.0;  // self.ret[news] = 0
 }
 
+// ---------------------------------------------------------------------------
+// ReplayBuffer.add: several independent device copies in one launch.  Each segment is
+// split into 16-byte vectors (when aligned) or dwords; the grid strides over the sum.
+// ---------------------------------------------------------------------------
+struct CopySegs {
+  const uint8_t* src[FW_MAX_COPY_SEGS];
+  uint8_t* dst[FW_MAX_COPY_SEGS];
+  int64_t units[FW_MAX_COPY_SEGS];   // number of 16-B (vec) or 4-B units
+  int64_t start[FW_MAX_COPY_SEGS + 1];
+  int vec[FW_MAX_COPY_SEGS];
+  int n;
+};
+
+__global__ __launch_bounds__(BLOCK) void k_copy_segs(CopySegs cs) {
+  const int64_t total = cs.start[cs.n];
+  for (int64_t u = (int64_t)blockIdx.x * BLOCK + threadIdx.x; u < total; u += (int64_t)gridDim.x * BLOCK) {
+    int k = 0;
+#pragma unroll
+    for (int j = 1; j < FW_MAX_COPY_SEGS; j++) k += (j < cs.n && u >= cs.start[j]) ? 1 : 0;
+    const int64_t off = u - cs.start[k];
+    if (cs.vec[k]) {
+      reinterpret_cast<uint4*>(cs.dst[k])[off] = reinterpret_cast<const uint4*>(cs.src[k])[off];
+    } else {
+      reinterpret_cast<uint32_t*>(cs.dst[k])[off] = reinterpret_cast<const uint32_t*>(cs.src[k])[off];
+    }
+  }
+}
+
 unsigned grid_for(int64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
 
 int moments_parts(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(MAX_PARTS, (n + BLOCK - 1) / BLOCK)); }
@@ -336,6 +365,30 @@ int fw_vecnorm_apply(const float* obs, int64_t n, int32_t d, int64_t ldx, const 
   if (rew_out && !rew) return fw::set_error(FW_E_INVALID, "fw_vecnorm_apply: rew_out without rew");
   hipLaunchKernelGGL(k_vecnorm_apply, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, obs, n, d, ldx, rms,
                      epsilon, norm_obs, clip_obs, obs_out, ld_out, rew, norm_rew, clip_rew, rew_out, done, ret);
+  FW_HIP(hipGetLastError());
+  return FW_OK;
+}
+
+int fw_replay_add(const fw_copy_seg* segs, int32_t n_segs, void* stream) {
+  if (!segs || n_segs < 1 || n_segs > FW_MAX_COPY_SEGS)
+    return fw::set_error(FW_E_INVALID, "fw_replay_add: 1..FW_MAX_COPY_SEGS segments");
+  CopySegs cs{};
+  cs.n = n_segs;
+  cs.start[0] = 0;
+  for (int k = 0; k < n_segs; k++) {
+    const fw_copy_seg& g = segs[k];
+    if (!g.src || !g.dst || g.bytes < 0 || g.bytes % 4) return fw::set_error(FW_E_INVALID, "fw_replay_add: bad segment");
+    const bool v = g.bytes % 16 == 0 && ((uintptr_t)g.src % 16) == 0 && ((uintptr_t)g.dst % 16) == 0;
+    cs.src[k] = (const uint8_t*)g.src;
+    cs.dst[k] = (uint8_t*)g.dst;
+    cs.vec[k] = v;
+    cs.units[k] = g.bytes / (v ? 16 : 4);
+    cs.start[k + 1] = cs.start[k] + cs.units[k];
+  }
+  const int64_t total = cs.start[n_segs];
+  if (total == 0) return FW_OK;
+  const unsigned grid = (unsigned)std::min<int64_t>((total + BLOCK - 1) / BLOCK, 8192);
+  hipLaunchKernelGGL(k_copy_segs, dim3(grid), dim3(BLOCK), 0, (hipStream_t)stream, cs);
   FW_HIP(hipGetLastError());
   return FW_OK;
 }

@@ -171,10 +171,23 @@ class VecNormalize:
         return self.step_wait()
 
     def normalize_obs(self, obs):
-        o = torch.as_tensor(obs, dtype=torch.float32, device=self.device).reshape(self.num_envs, -1).contiguous()
+        """vec_normalize.py:148-159 with the current statistics, any number of rows."""
+        o = torch.as_tensor(obs, dtype=torch.float32, device=self.device).reshape(-1, self.obs_dim).contiguous()
         out = torch.empty_like(o)
-        self._apply(o, None, None, obs_out=out)
+        d = self.obs_dim
+        _native.check(self.lib.fw_vecnorm_apply(_p(o), o.shape[0], d, d, _p(self.rms), float(self.epsilon),
+                                                int(self.norm_obs), float(self.clip_obs), _p(out), d, None, 0, 0.0,
+                                                None, None, None, self._s()), "fw_vecnorm_apply")
         return self._out(out)
+
+    def normalize_reward(self, reward):
+        """vec_normalize.py:161-169 with the current statistics (device tensors in, same shape out)."""
+        r = torch.as_tensor(reward, device=self.device)
+        if not self.norm_reward:
+            return r
+        d = self.obs_dim
+        scale = torch.sqrt(self.rms[2 * d + 2] + self.epsilon)
+        return torch.clamp(r.double() / scale, -self.clip_reward, self.clip_reward).to(r.dtype)
 
     def get_original_obs(self):
         return self._out(self.old_obs)
