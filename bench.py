@@ -63,11 +63,13 @@ def algorithmic_bytes_per_env_step(spec, esz=4):
 
 
 def device_ms_per_launch(launch, reps, dev):
-    """Average device duration of ``launch()`` (HIP events on the launching stream around each call).
+    """Average device duration of ``launch()``: one HIP event pair on the launching stream around
+    ``reps`` back-to-back launches, divided by ``reps``.
 
     The stream is first parked behind a spin kernel (torch.cuda._sleep) long enough for the host to
-    enqueue every launch, so host-side Python overhead between launches never shows up as device time
-    (the events then bracket only the kernel)."""
+    enqueue every launch, so host-side Python overhead between launches never shows up as device time;
+    no event sits between two launches (an event per launch serialises the queue and inflates each
+    launch by the marker's own cost).  Inter-launch dispatch gaps are included (conservative)."""
     stream = torch.cuda.current_stream(dev)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record(stream)
@@ -75,15 +77,15 @@ def device_ms_per_launch(launch, reps, dev):
     b.record(stream)
     torch.cuda.synchronize(dev)
     ms_per_cycle = max(a.elapsed_time(b), 1e-3) / float(1 << 20)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     host_ms = 2.0 + 0.2 * reps  # generous upper bound for enqueuing reps launches from Python
     torch.cuda._sleep(int(host_ms / ms_per_cycle))
-    for e0, e1 in evs:
-        e0.record(stream)
+    e0.record(stream)
+    for _ in range(reps):
         launch()
-        e1.record(stream)
+    e1.record(stream)
     torch.cuda.synchronize(dev)
-    return float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    return e0.elapsed_time(e1) / reps
 
 
 def cpu_baseline(seconds=12.0):
