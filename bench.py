@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from tum_adlr_deep_reinforcement_learning_amd import config as C  # noqa: E402
-from tum_adlr_deep_reinforcement_learning_amd.engine import Engine  # noqa: E402
+from tum_adlr_deep_reinforcement_learning_amd.engine import Engine, StepGraph  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md: 8.0 TB/s spec)
 
@@ -88,35 +88,53 @@ def device_ms_per_launch(launch, reps, dev):
     return e0.elapsed_time(e1) / reps
 
 
-def cpu_baseline(seconds=12.0):
-    """The CPU oracle (oracle/fw_oracle.c, fp64 C port of the reference step) on one host core."""
+def _cpu_worker(args):
+    """One host process of the CPU baseline: 64 oracle envs stepped with U(-1,1) actions for ``seconds``."""
+    seed, seconds = args
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle import oracle as O
     spec = C.EnvSpec(sim_config_kw={"turbulence": False})
     sc, ec = spec.sim.struct(), spec.struct()
-    rng = np.random.RandomState(0)
-    n_env = 64
+    rng = np.random.RandomState(seed)
     envs = []
-    for j in range(n_env):
+    for _ in range(64):
         e = O.OracleEnv(sc, ec, spec.n_obs)
         init = np.zeros(C.FW_NINIT)
         init[C.FW_I_ROLL], init[C.FW_I_PITCH] = rng.uniform(-1.9, 1.9), rng.uniform(-0.78, 0.78)
         init[C.FW_I_U] = rng.uniform(10, 23)
         init[C.FW_I_PD] = -50.0
-        e.reset(init, np.array([rng.uniform(-1, 1), rng.uniform(-0.4, 0.4), rng.uniform(15, 28)]))
-        envs.append((e, init))
+        tgt = np.array([rng.uniform(-1, 1), rng.uniform(-0.4, 0.4), rng.uniform(15, 28)])
+        e.reset(init, tgt)
+        envs.append((e, init, tgt))
     steps = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        for e, init in envs:
+        for e, init, tgt in envs:
             _, _, done, _, _ = e.step(rng.uniform(-1, 1, 3))
             steps += 1
             if done:
-                e.reset(init, np.array([0.1, 0.0, 20.0]))
-    dt = time.perf_counter() - t0
-    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": "%d env steps (64 envs x U(-1,1) actions, default task, turbulence off) of the fp64 C oracle "
-                      "on 1 host core in %.1f s" % (steps, dt)}
+                e.reset(init, tgt)
+    return steps, time.perf_counter() - t0
+
+
+def cpu_baseline(seconds=12.0, procs=None):
+    """The CPU oracle (oracle/fw_oracle.c, fp64 C port of the reference step) in one process per host
+    core, the way the reference runs its envs (SubprocVecEnv: one env process per core).  Must run
+    before this process touches the GPU (the workers are forked)."""
+    import multiprocessing as mp
+    if procs is None:
+        procs = max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16 cores
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import oracle as O
+    O.build()  # compile once in the parent (workers only load it)
+    with mp.get_context("fork").Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(1000 + k, seconds) for k in range(procs)])
+    steps = sum(r[0] for r in res)
+    dt = max(r[1] for r in res)
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": procs, "kind": "port",
+            "sample": "%d env steps (%d processes x 64 envs, U(-1,1) actions, default task, turbulence off, "
+                      "auto-reset) of the fp64 C oracle in %.1f s on %d host cores"
+                      % (steps, procs, dt, procs)}
 
 
 def rollout_leg(spec, n, T, dev, rank, world, precision):
@@ -210,13 +228,16 @@ def sac_fill_leg(n, K, dev, rank, world, precision):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=500)
-    ap.add_argument("--warmup", type=int, default=50)
+    # defaults time a steady-state window: over the first ~200 steps after the global reset no aircraft
+    # has tumbled into the stiff regimes whose RK45 steps need hundreds of RHS evaluations
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=1000)
     ap.add_argument("--envs", type=int, default=65536, help="aircraft per GPU")
     ap.add_argument("--precision", default="float32", choices=["float32", "float64"])
     ap.add_argument("--turbulence", action="store_true", help="light Dryden turbulence + random steady wind")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-procs", type=int, default=None, help="CPU baseline processes (default: min(16, cores))")
     ap.add_argument("--no-metrics", action="store_true",
                     help="do not track the config's streaming episode metrics (fixed_wing.py:1644-1736)")
     ap.add_argument("--rollout-steps", type=int, default=0,
@@ -229,6 +250,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # CPU baseline first: its worker processes are forked, which must happen before any HIP call
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds, args.cpu_procs)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -245,24 +270,37 @@ def main():
     gen.manual_seed(1 + rank)
     pool = torch.rand(16, n, 3, generator=gen, device=dev, dtype=eng.dtype) * 2 - 1
 
-    for s in range(args.warmup):
-        eng.env_step(pool[s % 16], stats=False)
+    # the K timed steps are issued as replays of a HIP graph of G captured launches (engine.StepGraph):
+    # one host call per G steps, so the box's host jitter never leaves the device idle between steps
+    G = 16
+    eng.env_step(pool[0], stats=False)  # first warm-up step, eager (kernel load outside the capture)
+    graph = StepGraph(eng, pool)
+
+    def run(k):
+        for _ in range(k // G):
+            graph.replay()
+        for s in range(k % G):
+            eng.env_step(pool[s], stats=False)
+
+    run(max(args.warmup - 1, 0))
     torch.cuda.synchronize(dev)
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        eng.env_step(pool[s % 16], stats=False)
+    ev0.record(stream)
+    run(args.steps)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # k_env_step device duration: events around each launch on its stream, host overhead excluded
-    it = iter(range(1 << 30))
-    kern_ms = device_ms_per_launch(lambda: eng.env_step(pool[next(it) % 16], stats=False),
-                                   min(max(args.steps, 10), 100), dev)
+    # k_env_step device duration per launch: HIP events on the launch stream around the timed steps
+    # themselves (graph replays keep the queue full, so this is kernel time plus dispatch gaps)
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
     el = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -296,9 +334,6 @@ def main():
         sac = sac_fill_leg(args.sac_envs // world, args.sac_fill_steps, dev, rank, world, args.precision)
 
     if rank == 0:
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(args.cpu_seconds)
         out = {
             "metric": "env-steps/sec at 64k parallel aircraft, 1/2/4/8 MI355X; % HBM roofline",
             "value": value,
@@ -316,7 +351,8 @@ def main():
                                    "defaults, %s, RK45 rtol=1e-3 atol=1e-6, auto-reset)"
                                    % (n, "light Dryden + steady wind" if args.turbulence else
                                       "steady wind, turbulence off")
-                                   + (", streaming episode metrics" if spec.metrics_enabled else ""),
+                                   + (", streaming episode metrics" if spec.metrics_enabled else "")
+                                   + ", timed after %d warm-up steps" % args.warmup,
                        "envs_per_gpu": n, "global_envs": n * world, "kernel": "k_env_step",
                        "parallelism": "env-dp%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

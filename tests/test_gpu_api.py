@@ -178,3 +178,34 @@ def test_pyfly_facade_matches_oracle():
     e = sim.state["energy_total"].value
     assert np.isfinite(e) and e > 0
     sim.engine.close()
+
+
+def test_step_graph_replay_matches_eager_steps():
+    """engine.StepGraph: K captured env steps replayed from a HIP graph leave exactly the state (and
+    last-step outputs) that K eager launches leave, including auto-resets inside the graph."""
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine, StepGraph
+    spec = C.EnvSpec(config_kw={"steps_max": 12}, sim_config_kw={"turbulence": False})
+    n, K = 4096, 8
+    engs = [Engine(spec.sim, spec, n, device="cuda:0", precision="float32") for _ in range(2)]
+    for e in engs:
+        e.seed(5)
+        e.reset()
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(3)
+    pool = torch.rand(K, n, 3, generator=g, device="cuda:0") * 2 - 1
+    for e in engs:
+        e.env_step(pool[0])
+    graph = StepGraph(engs[1], pool)
+    for r in range(3):  # 24 steps: crosses steps_max, so done/auto-reset happen inside the graph
+        for k in range(K):
+            engs[0].env_step(pool[k])
+        graph.replay()
+        pool.mul_(-1.0)  # refilled in place between replays: the graph reads the new values
+    torch.cuda.synchronize()
+    for blk in (C.FW_BLK_ODE, C.FW_BLK_DERIVED, C.FW_BLK_TARGET, C.FW_BLK_STEPS):
+        assert torch.equal(engs[0].get_block(blk), engs[1].get_block(blk)), blk
+    for name in ("obs", "reward", "done", "term", "terminal_obs", "episode"):
+        assert torch.equal(getattr(engs[0], name), getattr(engs[1], name)), name
+    assert int(engs[1].steps()[0].max()) <= 12
+    for e in engs:
+        e.close()

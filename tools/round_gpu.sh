@@ -21,6 +21,8 @@ run pytest_gpu 1000 python -m pytest tests -m gpu -q -rf -x
 if [ "${SKIP_PROF:-0}" = 0 ]; then
   bash tools/traffic.sh > "$OUT/traffic.log" 2>&1; rc=$?; echo "traffic rc=$rc"; tail -3 "$OUT/traffic.log"; [ $rc -le 1 ] || exit $rc
   cp gpurun_out/traffic/pmc_env_step.json "$OUT/" 2>/dev/null
-  run rocprof_trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -- python bench.py --steps 200 --warmup 20 --no-cpu-baseline
+  run rocprof_trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -- python bench.py --no-cpu-baseline
+  # the bench line's timed window = its last 1000 k_env_step dispatches
+  python tools/trace_window.py "$OUT/trace" 1000 k_env_step "$OUT/trace_window.json"
 fi
 run bench 600 python bench.py

@@ -146,6 +146,7 @@ class Engine:
                                            _ptr(self.episode) if episode else None,
                                            _ptr(self.stats) if stats else None, int(bool(auto_reset)),
                                            self.stream()), "fw_env_step")
+        self._stepped = True
         return self.obs, self.reward, self.done, self.term
 
     def observe(self):
@@ -173,3 +174,32 @@ class Engine:
     def steps(self):
         s = self.get_block(C.FW_BLK_STEPS)[0]
         return s & 0xFFFF, (s >> 16) & 0xFFFF
+
+
+class StepGraph:
+    """``K`` consecutive ``Engine.env_step`` launches captured into one HIP graph.
+
+    ``actions`` is a device tensor ``[K][n][3]`` of the engine's dtype; step ``k`` of every replay reads
+    ``actions[k]`` at replay time, so a caller (e.g. an off-policy warm-up that draws uniform actions
+    on the device, or a benchmark) refills it in place between replays.  One host call then issues K
+    kernels, so the device never idles behind Python between steps.  The outputs (``eng.obs``,
+    ``eng.reward``, ``eng.done``, ...) hold step K-1's values after a replay; the per-step values of the
+    earlier steps are not kept (use eager ``env_step`` when every step's outputs are consumed).
+    """
+
+    def __init__(self, eng, actions, auto_reset=True, terminal_obs=True, episode=True):
+        if actions.dim() != 3 or actions.shape[1:] != (eng.n, 3) or actions.dtype != eng.dtype \
+                or actions.device != eng.device or not actions.is_contiguous():
+            raise ValueError("actions must be a contiguous [K][n][3] %s tensor on %s" % (eng.dtype, eng.device))
+        self.eng, self.actions, self.k = eng, actions, actions.shape[0]
+        kw = dict(auto_reset=auto_reset, terminal_obs=terminal_obs, episode=episode)
+        if not getattr(eng, "_stepped", False):
+            raise RuntimeError("StepGraph: run one eager env_step first (loads the kernels outside the capture)")
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            for k in range(self.k):
+                eng.env_step(actions[k], **kw)
+
+    def replay(self):
+        self.graph.replay()
+        return self.eng.obs, self.eng.reward, self.eng.done, self.eng.term
