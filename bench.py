@@ -47,7 +47,7 @@ def algorithmic_bytes_per_env_step(spec, esz=4):
     act_window = 1
     for o in spec.cfg["observation"]["states"]:
         if o["type"] == "action" and spec.scale_actions:
-            act_window = max(act_window, int(o.get("window_size", 1)) - 1)
+            act_window = max(act_window, int(o.get("window_size", 1)))
     for f in spec.cfg["reward"]["factors"]:
         if f["class"] == "action" and f["type"] == "delta":
             act_window = max(act_window, int(f["window_size"]) - 1)

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FWSIM_ABI_VERSION 2
+#define FWSIM_ABI_VERSION 3
 
 /* ---- error codes ---------------------------------------------------------- */
 #define FW_OK 0
@@ -131,6 +131,8 @@ typedef struct fw_sim_config {
 #define FW_MAX_OBS 32
 #define FW_MAX_REW 8
 #define FW_MAX_WINDOW 16
+#define FW_MAX_OBS_LEN 16     /* observation.length (history rows) */
+#define FW_MAX_OBS_HIST 64    /* past observation rows kept per env: (length - 1) * step + 2 */
 
 /* observation entry kinds (fixed_wing.py:1149-1234) */
 #define FW_OBS_STATE 0          /* var = fw_var (roll..beta, omega, pos, vel, act states) */
@@ -192,6 +194,17 @@ typedef struct fw_env_config {
   int32_t metrics;
   int32_t pad2_;
   double rise_low, rise_high;         /* rise_time metric "low" / "high" (defaults 0.1, 0.9) */
+  /* observation.length / step / noise (get_observation, fixed_wing.py:1113-1262).  The
+   * observation of one env is obs_length rows of n_obs entries (row r = lag 1 + r * obs_step),
+   * i.e. [obs_length * n_obs] values; "vector" and "matrix" shapes share this memory layout.
+   * Rows older than the episode repeat its first row plus a per-row U(-1,1)*dt offset (the
+   * reference's init_noise).  obs_noise adds N(obs_noise_mean, obs_noise_std) to every value
+   * after normalisation.  Both draws come from the handle's Philox streams.                 */
+  int32_t obs_length;                 /* >= 1 (0 is read as 1) */
+  int32_t obs_step;                   /* >= 1 (0 is read as 1) */
+  int32_t obs_noise;                  /* 1: add observation noise */
+  int32_t pad3_;
+  double obs_noise_mean, obs_noise_std;
 } fw_env_config;
 
 /* Episode-metric record written for every done env (SoA [FW_NMETRIC][N] so the stores

@@ -49,3 +49,28 @@ def env_init(init_row, n_act_dyn=3):
         v[C.FW_I_ACT0 + 2 * j + 1] = 0.0
     v[C.FW_I_WIND_N:C.FW_I_WIND_D + 1] = init_row[15:18]
     return v
+
+
+OBS_HIST_CASES = {
+    # name -> config_kw (the config file itself is stored in the fixture: "" = default config)
+    "cnn_rand": None,
+    "cnn_fail_p": {"simulator": {"states": {6: {"constraint_min": -150, "constraint_max": 150}}}},
+    "cnn_short": {"steps_max": 40},
+    "vec3_rand": {"observation": {"length": 3, "step": 2, "shape": "vector"}},
+    "vec3_norm": {"observation": {"length": 3, "step": 2, "shape": "vector", "normalize": True}},
+}
+
+
+def obs_hist_spec(name, tmpdir):
+    """EnvSpec of an env_obs_hist.npz case (writes the stored reference config file to tmpdir)."""
+    import json
+    d = load("env_obs_hist.npz")
+    text = str(d[name + "__config_json"])
+    path = None
+    if text:
+        path = os.path.join(str(tmpdir), name + ".json")
+        with open(path, "w") as f:
+            f.write(text)
+    ckw = dict(OBS_HIST_CASES[name] or {})
+    ckw["steps_max"] = int(d[name + "__steps_max"])
+    return C.EnvSpec(config_path=path, config_kw=ckw, sim_config_kw={"turbulence": False}), d

@@ -20,8 +20,11 @@ Fixtures (all float64 unless noted):
   dryden.npz              Dryden FIR coefficients + raw filter outputs
   env_seq.npz             FixedWingAircraft reset/step sequences (obs, reward, done, term)
   env_pid_set.npz         PID replay of a synthetic 40-scenario evaluation set
+  env_metrics.npz         episode metrics + histories for metric scenarios
+  env_obs_hist.npz        observation-history episodes (observation.length > 1)
 """
 import hashlib
+import json
 import math
 import os
 import struct
@@ -554,8 +557,50 @@ def gen_metrics():
     np.savez_compressed(os.path.join(OUT, "env_metrics.npz"), **out)
 
 
+CNN_CFG = os.path.join(REF, "fixed-wing-gym/gym_fixed_wing/examples/models/cnn_controller/fixed_wing_config.json")
+
+
+def gen_obs_hist():
+    """Observation histories (observation.length > 1, fixed_wing.py:1133-1258): the reference's own
+    cnn_controller config (5 rows, matrix, relative targets) and the default config with 3 rows,
+    step 2, vector shape, with and without normalisation.  Rows older than the episode carry the
+    reference's init_noise (np_random.uniform(-1, 1) * dt, one draw per row); the tests check those
+    rows up to a row-constant offset."""
+    out = {}
+    rng = np.random.RandomState(123)
+    hist3 = {"observation": {"length": 3, "step": 2, "shape": "vector"}}
+    hist3n = {"observation": {"length": 3, "step": 2, "shape": "vector", "normalize": True}}
+    cases = [
+        # name, config path, config_kw, steps_max, n_steps, omega_deg, policy
+        ("cnn_rand", CNN_CFG, None, 2000, 200, 60.0, "rand"),
+        ("cnn_fail_p", CNN_CFG, {"simulator": {"states": {6: {"constraint_min": -150, "constraint_max": 150}}}}, 2000,
+         600, 60.0, "rand"),
+        ("cnn_short", CNN_CFG, None, 40, 60, 60.0, "rand"),
+        ("vec3_rand", GYM_CFG, hist3, 2000, 150, 60.0, "rand"),
+        ("vec3_norm", GYM_CFG, hist3n, 2000, 150, 60.0, "rand"),
+    ]
+    for name, path, ckw, smax, n, omd, pol in cases:
+        kw = {"steps_max": smax}
+        if ckw:
+            kw.update(ckw)
+        env = FixedWingAircraft(path, config_kw=kw, sim_config_kw={"turbulence": False})
+        env.seed(0)
+        ep = env_episode(env, rng, False, n, omega_deg=omd, policy=pol)
+        for k in ("init", "target0", "obs", "act", "rew", "done", "term"):
+            out[name + "__" + k] = ep[k]
+        out[name + "__steps_max"] = np.array(smax)
+        # the config file itself travels as data (the GPU box has no reference checkout); "" = default
+        out[name + "__config_json"] = np.array("" if path == GYM_CFG else json.dumps(json.load(open(path))))
+        out[name + "__config_kw"] = np.array(repr(ckw))
+        print("obs_hist %s: %d steps, obs %s, last term=%r" % (name, len(ep["rew"]), ep["obs"].shape[1:],
+                                                              ep["term"][-1]))
+    np.savez_compressed(os.path.join(OUT, "env_obs_hist.npz"), **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["single", "traj", "dryden", "env", "pidset", "metrics"]
+    which = sys.argv[1:] or ["single", "traj", "dryden", "env", "pidset", "metrics", "obshist"]
+    if "obshist" in which:
+        gen_obs_hist()
     if "single" in which:
         gen_single_step()
     if "traj" in which:

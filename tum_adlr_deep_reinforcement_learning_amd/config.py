@@ -57,6 +57,7 @@ FW_REW_STATE_ERROR, FW_REW_STATE_VALUE, FW_REW_ACTION_DELTA, FW_REW_ACTION_BOUND
 FW_FUN = {"linear": 0, "quadratic": 1, "exponential": 2}
 FW_TGT = {"constant": 0, "compensate": 1}
 FW_MAX_OBS, FW_MAX_REW, FW_MAX_WINDOW = 32, 8, 16
+FW_MAX_OBS_LEN, FW_MAX_OBS_HIST = 16, 64
 
 (FW_I_ROLL, FW_I_PITCH, FW_I_YAW, FW_I_P, FW_I_Q, FW_I_R, FW_I_PN, FW_I_PE, FW_I_PD, FW_I_U, FW_I_V, FW_I_W,
  FW_I_ACT0, FW_I_ACT0_DOT, FW_I_ACT1, FW_I_ACT1_DOT, FW_I_ACT2, FW_I_ACT2_DOT, FW_I_WIND_N, FW_I_WIND_E,
@@ -138,7 +139,10 @@ class FwEnvConfig(ctypes.Structure):
                 ("pad_", ctypes.c_int32),
                 ("rew", FwRewFactor * FW_MAX_REW),
                 ("metrics", ctypes.c_int32), ("pad2_", ctypes.c_int32),
-                ("rise_low", ctypes.c_double), ("rise_high", ctypes.c_double)]
+                ("rise_low", ctypes.c_double), ("rise_high", ctypes.c_double),
+                ("obs_length", ctypes.c_int32), ("obs_step", ctypes.c_int32),
+                ("obs_noise", ctypes.c_int32), ("pad3_", ctypes.c_int32),
+                ("obs_noise_mean", ctypes.c_double), ("obs_noise_std", ctypes.c_double)]
 
 
 # ---------------------------------------------------------------------------
@@ -440,13 +444,25 @@ class EnvSpec:
         self.sim = build_sim(sim_config_path, sim_parameter_path, skw)
         self.steps_max = int(cfg["steps_max"])
         obs_cfg = cfg["observation"]
-        if obs_cfg.get("length", 1) != 1:
-            raise NotImplementedError("observation.length > 1")
-        if obs_cfg.get("normalize", False) and any(o.get("mean") is None for o in obs_cfg["states"]):
+        # observation history (get_observation, fixed_wing.py:1133-1258): `length` rows, `step` apart
+        self.obs_length = int(obs_cfg.get("length", 1))
+        self.obs_step = int(obs_cfg.get("step", 1))
+        self.obs_shape_kind = obs_cfg.get("shape", "vector")
+        if self.obs_shape_kind not in ("vector", "matrix"):
+            raise ValueError("Unexpected observation shape {}".format(self.obs_shape_kind))
+        if not 1 <= self.obs_length <= FW_MAX_OBS_LEN or self.obs_step < 1:
+            raise NotImplementedError("observation.length %d / step %d" % (self.obs_length, self.obs_step))
+        if (self.obs_length - 1) * self.obs_step + 2 > FW_MAX_OBS_HIST:
+            raise NotImplementedError("observation history deeper than %d steps" % FW_MAX_OBS_HIST)
+        if obs_cfg.get("normalize", False) and any(o.get("mean") is None or o.get("var") is None
+                                                   for o in obs_cfg["states"] if o.get("norm", True)):
             raise NotImplementedError("observation normalisation without explicit mean/var")
+        # observation noise: val += np_random.normal(loc=mean, scale=var) (fixed_wing.py:1241-1242);
+        # a zero-mean, zero-scale draw adds exactly 0.0, so it is not drawn at all
         noise = obs_cfg.get("noise")
+        self.obs_noise = None
         if noise is not None and (noise.get("var", 0) != 0 or noise.get("mean", 0) != 0):
-            raise NotImplementedError("observation noise")
+            self.obs_noise = (float(noise.get("mean", 0)), float(noise.get("var", 0)))
         if cfg.get("integration_window", 0):
             raise NotImplementedError("integration_window")
         if cfg["reward"].get("form", "absolute") != "absolute":
@@ -540,6 +556,12 @@ class EnvSpec:
                 lo.append(low)
         self.obs_low = np.array(lo, dtype=np.float32)
         self.obs_high = np.array(hi, dtype=np.float32)
+        if self.obs_length > 1:  # fixed_wing.py:177-191: repeat per row (vector) or stack rows (matrix)
+            L = self.obs_length
+            if self.obs_shape_kind == "vector":
+                self.obs_low, self.obs_high = np.tile(self.obs_low, L), np.tile(self.obs_high, L)
+            else:
+                self.obs_low, self.obs_high = np.tile(self.obs_low, (L, 1)), np.tile(self.obs_high, (L, 1))
         alo, ahi, slo, shi = [], [], [], []
         for a in cfg["action"]["states"]:
             s_hi = self._state_bound(a["name"], "high")
@@ -555,8 +577,18 @@ class EnvSpec:
         self.action_scale_to_high = np.array(shi, dtype=np.float64)
 
     @property
-    def n_obs(self):
+    def n_obs_row(self):
+        """Entries of one observation row (the observation.states list)."""
         return len(self.cfg["observation"]["states"])
+
+    @property
+    def n_obs(self):
+        """Values of one env's observation: length rows x n_obs_row entries (flat on the device)."""
+        return self.obs_length * self.n_obs_row
+
+    @property
+    def obs_shape(self):
+        return tuple(self.obs_low.shape)
 
     def obs_names(self):
         out = []
@@ -637,6 +669,9 @@ class EnvSpec:
         rise = [m for m in cfg.get("metrics", []) if m["name"] == "rise_time"]
         e.rise_low = float(rise[0].get("low", 0.1)) if rise else 0.1
         e.rise_high = float(rise[0].get("high", 0.9)) if rise else 0.9
+        e.obs_length, e.obs_step = self.obs_length, self.obs_step
+        if self.obs_noise is not None:
+            e.obs_noise, (e.obs_noise_mean, e.obs_noise_std) = 1, self.obs_noise
         e.streak_req = int(t["success_streak_req"])
         if e.streak_req > 128:
             raise NotImplementedError("success_streak_req > 128")

@@ -99,6 +99,10 @@ struct DevCfg {
   int term_present[3];
   int metrics;                         // streaming episode metrics tracked (fw_env_config.metrics)
   T rise_low, rise_high;
+  int obs_len, obs_step, obs_hist;     // observation rows, their spacing, past rows kept (0: no history)
+  int obs_noise;                       // observation.noise drawn
+  int obs_general;                     // obs_len > 1 or obs_noise: observe_full instead of the plain row
+  T obs_noise_mean, obs_noise_std;
   fw_obs_entry obs[FW_MAX_OBS];
   fw_rew_factor rew[FW_MAX_REW];
 };
@@ -114,6 +118,7 @@ template <typename T, uint32_t CM, uint32_t CLM, uint32_t WM, uint32_t DM, int E
 struct SpecCfg : DevCfg<T> {
   static constexpr uint32_t cmask = CM, clipmask = CLM, wrapmask = WM, dotmask = DM;
   static constexpr int elevon = ELEVON, trig_alpha = TA, trig_beta = TB, euler_exact = EE;
+  static constexpr int obs_general = 0;  // specialisations serve plain length-1, noise-free observations
 };
 // fixed_wing_config.json (gym): omega +-720 deg/s and Va <= 70 constrained; Va, actuators,
 // elevator / aileron / throttle clipped; roll / yaw wrapped; elevon rate limits

@@ -76,6 +76,8 @@ struct State {
   T* met;             // [MT_ROWS][ld] streaming episode-metric sums (null: metrics off)
   uint32_t* metu;     // [MU_ROWS][ld] their counters / indices
   T* met_out;         // [FW_NMETRIC][N] (SoA) record of done envs (null: not requested)
+  T* obs_init;        // [n_obs][ld] raw observation row at the episode's reset (null: length-1 observations)
+  T* obs_ring;        // [obs_hist][n_obs][ld] raw rows of past steps, slot = step % obs_hist
 };
 
 // streaming episode-metric state (fixed_wing.py:1644-1736 restated over running sums):
@@ -168,10 +170,9 @@ __device__ __forceinline__ T state_value(int var, const T* y, const T* der) {
 // seqA / seqC: newest-first sequences of raw actions / constrained commands
 // (index 0 = latest), nseq = number of valid entries (= steps_count).
 template <typename T>
-__device__ __forceinline__ void observe(const DevCfg<T>& c, const T* y, const T* der, const T* tgt, int steps,
-                                        const T (*seqA)[3], const T (*seqC)[3], T* out, int64_t stride) {
-  for (int o = 0; o < c.n_obs; o++) {
-    const fw_obs_entry E = c.obs[o];
+__device__ __forceinline__ T obs_raw(const DevCfg<T>& c, const fw_obs_entry& E, const T* y, const T* der,
+                                     const T* tgt, int steps, const T (*seqA)[3], const T (*seqC)[3]) {
+  {
     T val;
     if (E.kind == FW_OBS_STATE) {
       val = state_value(E.var, y, der);
@@ -203,9 +204,94 @@ __device__ __forceinline__ void observe(const DevCfg<T>& c, const T* y, const T*
         val = (T)acc;
       }
     }
-    if (E.norm) val = (val - (T)E.mean) / (T)E.var_;
-    out[(int64_t)o * stride] = val;
+    return val;
   }
+}
+
+template <typename T>
+__device__ __forceinline__ T obs_norm(const fw_obs_entry& E, T val) {
+  return E.norm ? (val - (T)E.mean) / (T)E.var_ : val;
+}
+
+// length-1 observation without noise (the default task): one row straight from the state
+template <typename T>
+__device__ __forceinline__ void observe(const DevCfg<T>& c, const T* y, const T* der, const T* tgt, int steps,
+                                        const T (*seqA)[3], const T (*seqC)[3], T* out, int64_t stride) {
+  for (int o = 0; o < c.n_obs; o++) {
+    const fw_obs_entry E = c.obs[o];
+    out[(int64_t)o * stride] = obs_norm(E, obs_raw(c, E, y, der, tgt, steps, seqA, seqC));
+  }
+}
+
+// get_observation with history rows and/or noise (fixed_wing.py:1113-1262).  Row r is the
+// observation at lag i = 1 + r * step, built from the raw (un-normalised, noise-free) rows this
+// env stored at earlier steps: the reference reads state.history[-i], history["target"/"error"][-i]
+// and the action window ending i-1 steps ago, which are exactly the values its lag-1 row had at
+// step t-i+1.  On a failed step (ConstraintException) the state/target/error histories were not
+// appended, so those entries come from step t-i while the action window (appended before the
+// integration) still ends at step t-i+1.  Lags beyond the episode (i > steps_count) repeat the
+// episode's first row (actions: the actuator's current value) plus one U(-1,1)*dt offset per row
+// (init_noise).  Then normalisation, then N(mean, std) noise per value.
+constexpr int OBS_STEP = 0, OBS_FAIL = 1, OBS_RESET = 2, OBS_PEEK = 3;
+
+template <typename T>
+__device__ __forceinline__ void observe_full(const DevCfg<T>& c, const State<T>& s, int64_t i, uint32_t episode,
+                                          int mode, const T* y, const T* der, const T* tgt, int steps,
+                                          const T (*seqA)[3], const T (*seqC)[3], T* out) {
+  const int64_t ld = s.ld;
+  const int nr = c.n_obs;
+  const bool hist = c.obs_hist > 0;
+  const uint32_t ctr = s.env_offset + (uint32_t)i;
+  uint32_t rnd[4] = {0u, 0u, 0u, 0u};
+  T z[4] = {T(0), T(0), T(0), T(0)};
+  int e = 0;  // value index across rows (noise block = e / 4)
+  for (int r = 0; r < c.obs_len; r++) {
+    const int lag = 1 + r * c.obs_step;
+    const bool clamp = lag > steps;
+    T inoise = T(0);
+    if (clamp && c.obs_len > 1) {  // self.np_random.uniform(-1, 1) * dt
+      philox(s.key0, s.key1, ctr, episode, 3u, (uint32_t)steps * 16u + (uint32_t)r, rnd);
+      inoise = (T(2) * u01<T>(rnd[0]) - T(1)) * c.dt;
+    }
+    for (int o = 0; o < nr; o++, e++) {
+      const fw_obs_entry E = c.obs[o];
+      const bool act = E.kind == FW_OBS_ACTION_WINDOW;
+      T v;
+      if (!clamp && lag == 1) {
+        v = obs_raw(c, E, y, der, tgt, steps, seqA, seqC);
+      } else if (!clamp) {
+        const int at = (mode == OBS_FAIL && !act) ? steps - lag : steps - lag + 1;  // step whose row holds it
+        v = at <= 0 ? s.obs_init[(int64_t)o * ld + i] : s.obs_ring[((int64_t)(at % c.obs_hist) * nr + o) * ld + i];
+      } else if (act || steps == 0) {
+        v = obs_raw(c, E, y, der, tgt, 0, seqA, seqC);  // current values (steps_count - i < 0 branch)
+      } else {
+        v = s.obs_init[(int64_t)o * ld + i];
+      }
+      v = obs_norm(E, v + inoise);
+      if (c.obs_noise) {
+        if ((e & 3) == 0) {
+          philox(s.key0, s.key1, ctr, episode, 2u, (uint32_t)steps * 256u + (uint32_t)(e >> 2), rnd);
+          normal4<T>(rnd, z);
+        }
+        v += c.obs_noise_mean + c.obs_noise_std * z[e & 3];
+      }
+      if (out) out[e] = v;
+    }
+  }
+  if (hist && (mode == OBS_RESET || mode == OBS_STEP)) {  // this step's raw row for later lags
+    T* dst = mode == OBS_RESET ? s.obs_init : s.obs_ring + (int64_t)(steps % c.obs_hist) * nr * ld;
+    for (int o = 0; o < nr; o++) dst[(int64_t)o * ld + i] = obs_raw(c, c.obs[o], y, der, tgt, steps, seqA, seqC);
+  }
+}
+
+// dispatch: the plain row for the default task, the general path otherwise (compiled out of the
+// structural specialisations, whose obs_general is a constant 0)
+template <typename T, typename C>
+__device__ __forceinline__ void observe_env(const C& c, const State<T>& s, int64_t i, uint32_t episode, int mode,
+                                            const T* y, const T* der, const T* tgt, int steps, const T (*seqA)[3],
+                                            const T (*seqC)[3], T* out) {
+  if (c.obs_general) observe_full<T>(c, s, i, episode, mode, y, der, tgt, steps, seqA, seqC, out);
+  else observe<T>(c, y, der, tgt, steps, seqA, seqC, out, 1);
 }
 
 // get_reward (fixed_wing.py:941-1111), form "absolute"
@@ -576,9 +662,14 @@ __global__ __launch_bounds__(BLOCK) void k_reset(const DevCfg<T>* __restrict__ c
     const T vr[3] = {der[0], der[1], der[3]};
     metrics_init(c, s, i, tgt, vr);
   }
-  if (obs && c.has_env) {
+  if (c.has_env && (obs || c.obs_hist)) {  // the history needs the reset row even without an output
     T seq[RING + 1][3];
-    observe(c, y, der, tgt, 0, seq, seq, obs + i * c.n_obs, 1);
+#pragma unroll
+    for (int j = 0; j <= RING; j++)
+#pragma unroll
+      for (int a = 0; a < 3; a++) seq[j][a] = T(0);
+    observe_env(c, s, i, s.episode[i], OBS_RESET, y, der, tgt, 0, seq, seq,
+                obs ? obs + i * (int64_t)c.n_obs * c.obs_len : nullptr);
   }
 }
 
@@ -600,7 +691,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const DevCfg<T>* __restrict__
     for (int a = 0; a < 3; a++) seqA[j][a] = seqC[j][a] = T(0);
   // newest-first from the rings
 #pragma unroll
-  for (int j = 0; j < RING; j++) {
+  for (int j = 0; j <= RING; j++) {
     if (j < c.act_window && steps - 1 - j >= 0) {
       const int slot = (steps - 1 - j) % c.act_window;
 #pragma unroll
@@ -612,7 +703,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const DevCfg<T>* __restrict__
       for (int a = 0; a < 3; a++) seqC[j][a] = s.cmd_ring[((int64_t)slot * 3 + a) * ld + i];
     }
   }
-  observe(c, y, der, tgt, steps, seqA, seqC, obs + i * c.n_obs, 1);
+  observe_env(c, s, i, s.episode[i], OBS_PEEK, y, der, tgt, steps, seqA, seqC, obs + i * (int64_t)c.n_obs * c.obs_len);
 }
 
 // Re-reads the pre-step ODE state after the RK loop (sim_step_masked's reload hook): the
@@ -829,8 +920,10 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
   const T ep_ret = ld_(s.ep_ret, 0, ld, i) + reward;
 
   // ---- observation (also the terminal observation) ----
-  T* orow = obs_out + i * c.n_obs;
-  if (done && tobs_out) observe(c, y, der, tgt, steps, seqA, seqC, tobs_out + i * c.n_obs, 1);
+  const int64_t ow = (int64_t)c.n_obs * c.obs_len;  // values per observation (rows x entries)
+  const int omode = sterm ? OBS_FAIL : OBS_STEP;
+  T* orow = obs_out + i * ow;
+  if (done && tobs_out) observe_env(c, s, i, episode, omode, y, der, tgt, steps, seqA, seqC, tobs_out + i * ow);
 
   rew_out[i] = reward;
   done_out[i] = done ? 1 : 0;
@@ -869,13 +962,13 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
       }
 #endif
       T seq0[RING + 1][3];
-      observe(c, yr, dr, tr, 0, seq0, seq0, orow, 1);
+      observe_env(c, s, i, episode + 1u, OBS_RESET, yr, dr, tr, 0, seq0, seq0, orow);
       FW_TSTAMP(5);
       return;
     }
   }
 #ifndef FW_SKIP_OBS
-  observe(c, y, der, tgt, steps, seqA, seqC, orow, 1);
+  observe_env(c, s, i, episode, omode, y, der, tgt, steps, seqA, seqC, orow);
 #endif
 #pragma unroll
   for (int r = 0; r < NY; r++) st_(s.y, r, ld, i, y[r]);
@@ -916,6 +1009,8 @@ struct fw_handle {
   // offsets (bytes) of the SoA blocks inside base
   size_t o_y, o_der, o_wind, o_target, o_cmd, o_epret, o_act, o_cmdring, o_steps, o_goal, o_episode;
   size_t o_met = 0, o_metu = 0;
+  int obs_hist = 0;         // past raw observation rows kept per env ((length - 1) * step + 2, 0 = none)
+  size_t o_obs_init = 0, o_obs_ring = 0;
 };
 
 namespace {
@@ -1065,6 +1160,13 @@ void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
     d.metrics = h->metrics && e.metrics;
     d.rise_low = (T)e.rise_low;
     d.rise_high = (T)e.rise_high;
+    d.obs_len = e.obs_length > 1 ? e.obs_length : 1;
+    d.obs_step = e.obs_step > 1 ? e.obs_step : 1;
+    d.obs_hist = h->obs_hist;
+    d.obs_noise = e.obs_noise != 0;
+    d.obs_noise_mean = (T)e.obs_noise_mean;
+    d.obs_noise_std = (T)e.obs_noise_std;
+    d.obs_general = d.obs_len > 1 || d.obs_noise;
     std::memcpy(d.obs, e.obs, sizeof(d.obs));
     std::memcpy(d.rew, e.rew, sizeof(d.rew));
   }
@@ -1081,6 +1183,10 @@ int validate(const fw_sim_config* s, const fw_env_config* e) {
     if (e->n_rew < 0 || e->n_rew > FW_MAX_REW) return set_err(FW_E_INVALID, "n_rew out of range");
     if (e->steps_max > 65535) return set_err(FW_E_UNSUPPORTED, "steps_max > 65535");
     if (e->streak_req > 128) return set_err(FW_E_UNSUPPORTED, "success_streak_req > 128");
+    if (e->obs_length < 0 || e->obs_length > FW_MAX_OBS_LEN || e->obs_step < 0 ||
+        (e->obs_length > 1 && (e->obs_length - 1) * std::max(e->obs_step, 1) + 2 > FW_MAX_OBS_HIST))
+      return set_err(FW_E_UNSUPPORTED, "observation length / step out of range");
+    if (e->obs_noise && !(e->obs_noise_std >= 0)) return set_err(FW_E_INVALID, "observation noise scale < 0");
     for (int o = 0; o < e->n_obs; o++)
       if (e->obs[o].kind == FW_OBS_ACTION_WINDOW && (e->obs[o].window < 1 || e->obs[o].window > FW_MAX_WINDOW))
         return set_err(FW_E_UNSUPPORTED, "action window out of range");
@@ -1098,7 +1204,7 @@ template <typename S, typename T>
 bool same_structure(const DevCfg<T>& d) {
   return d.cmask == S::cmask && d.clipmask == S::clipmask && d.wrapmask == S::wrapmask && d.dotmask == S::dotmask &&
          d.elevon == S::elevon && d.trig_alpha == S::trig_alpha && d.trig_beta == S::trig_beta &&
-         d.euler_exact == S::euler_exact;
+         d.euler_exact == S::euler_exact && d.obs_general == S::obs_general;
 }
 
 template <typename T>
@@ -1161,6 +1267,8 @@ State<T> state_of(const fw_handle* h) {
   s.met = h->metrics ? (T*)(b + h->o_met) : nullptr;
   s.metu = h->metrics ? (uint32_t*)(b + h->o_metu) : nullptr;
   s.met_out = (T*)h->met_out;
+  s.obs_init = h->obs_hist ? (T*)(b + h->o_obs_init) : nullptr;
+  s.obs_ring = h->obs_hist ? (T*)(b + h->o_obs_ring) : nullptr;
   return s;
 }
 
@@ -1205,8 +1313,8 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
     int wa = 1, wc = 0;
     for (int o = 0; o < env->n_obs; o++)
       if (env->obs[o].kind == FW_OBS_ACTION_WINDOW) {
-        if (env->scale_actions) wa = std::max(wa, env->obs[o].window - 1);
-        else wc = std::max(wc, env->obs[o].window - 1);
+        if (env->scale_actions) wa = std::max(wa, env->obs[o].window);  // window entries: fw_observe re-reads the newest too
+        else wc = std::max(wc, env->obs[o].window);
       }
     for (int r = 0; r < env->n_rew; r++)
       if (env->rew[r].kind == FW_REW_ACTION_DELTA) wa = std::max(wa, env->rew[r].window - 1);
@@ -1235,6 +1343,12 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
   if (h->metrics) {
     h->o_met = off; off += (size_t)MT_ROWS * row;
     h->o_metu = off; off += (size_t)MU_ROWS * row32;
+  }
+  if (env && env->obs_length > 1) {  // observation history: first row of the episode + ring of past rows
+    const int step = env->obs_step > 1 ? env->obs_step : 1;
+    h->obs_hist = (env->obs_length - 1) * step + 2;
+    h->o_obs_init = off; off += (size_t)env->n_obs * row;
+    h->o_obs_ring = off; off += (size_t)h->obs_hist * env->n_obs * row;
   }
   // rows are ld elements apart: the padding above is folded into ld for simplicity
   h->base_bytes = off;
@@ -1274,7 +1388,7 @@ int fw_num_envs(const fw_handle* h, int64_t* n) {
 
 int fw_num_obs(const fw_handle* h, int32_t* n) {
   if (!h || !n) return set_err(FW_E_INVALID, "NULL argument");
-  *n = h->has_env ? h->env.n_obs : 0;
+  *n = h->has_env ? h->env.n_obs * std::max(h->env.obs_length, 1) : 0;
   return FW_OK;
 }
 
@@ -1305,12 +1419,14 @@ int fw_update_config(fw_handle* h, const fw_sim_config* sim, const fw_env_config
     int wa = 1, wc = 0;
     for (int o = 0; o < env->n_obs; o++)
       if (env->obs[o].kind == FW_OBS_ACTION_WINDOW) {
-        if (env->scale_actions) wa = std::max(wa, env->obs[o].window - 1);
-        else wc = std::max(wc, env->obs[o].window - 1);
+        if (env->scale_actions) wa = std::max(wa, env->obs[o].window);  // window entries: fw_observe re-reads the newest too
+        else wc = std::max(wc, env->obs[o].window);
       }
     for (int r = 0; r < env->n_rew; r++)
       if (env->rew[r].kind == FW_REW_ACTION_DELTA) wa = std::max(wa, env->rew[r].window - 1);
-    if (wa != h->act_window || wc != h->cmd_window || env->n_obs != h->env.n_obs)
+    if (wa != h->act_window || wc != h->cmd_window || env->n_obs != h->env.n_obs ||
+        std::max(env->obs_length, 1) != std::max(h->env.obs_length, 1) ||
+        std::max(env->obs_step, 1) != std::max(h->env.obs_step, 1))
       return set_err(FW_E_UNSUPPORTED, "config update may not change observation layout or window sizes");
     if (env->metrics && !h->metrics)
       return set_err(FW_E_UNSUPPORTED, "episode metrics must be enabled when the handle is created");

@@ -63,7 +63,7 @@ class FixedWingAircraft:
             for k, v in target.items():
                 tgt[C.TARGET_INDEX[k], 0] = v
         obs = self.engine.reset(init=init, target=tgt)
-        return obs[0].cpu().numpy().astype(np.float32)
+        return obs[0].cpu().numpy().astype(np.float32).reshape(self.spec.obs_shape)
 
     def step(self, action):
         a = np.asarray(action, dtype=np.float64).reshape(1, 3)
@@ -78,7 +78,7 @@ class FixedWingAircraft:
                 info.update(metric_info(self.engine.metrics[:, 0].cpu().numpy(),
                                         [m["name"] for m in self.cfg.get("metrics", [])]))
         info["target"] = self.target
-        return obs[0].cpu().numpy().astype(np.float32), float(rew[0].item()), d, info
+        return obs[0].cpu().numpy().astype(np.float32).reshape(self.spec.obs_shape), float(rew[0].item()), d, info
 
     def render(self, mode="plot", **kw):
         raise NotImplementedError("rendering is host-side plotting; out of scope for the device engine")

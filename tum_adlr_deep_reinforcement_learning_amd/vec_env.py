@@ -198,16 +198,21 @@ class FixedWingVecEnv(VecEnv):
         obs, rew, done, term = eng.env_step(self._actions, auto_reset=True)
         self._actions = None
         if self.return_tensors:
-            return obs, rew, done.bool(), self._infos_lazy_device()
+            return self._shaped(obs), rew, done.bool(), self._infos_lazy_device()
         done_np = done.cpu().numpy().astype(bool)
         infos = self._infos(done_np)
-        return obs.cpu().numpy().astype(np.float32), rew.cpu().numpy().astype(np.float32), done_np, infos
+        return self._shaped(obs.cpu().numpy().astype(np.float32)), rew.cpu().numpy().astype(np.float32), done_np, infos
+
+    def _shaped(self, o):
+        """[N][length * n_row] device layout -> [N, *observation_space.shape] ("matrix" observations)."""
+        shape = self.observation_space.shape
+        return o if len(shape) == 1 else o.reshape((o.shape[0],) + tuple(shape))
 
     def _infos(self, done_np):
         eng = self.engine
         term = eng.term.cpu().numpy()
         anyd = bool(done_np.any())
-        tobs = eng.terminal_obs.cpu().numpy().astype(np.float32) if anyd else None
+        tobs = self._shaped(eng.terminal_obs.cpu().numpy().astype(np.float32)) if anyd else None
         ep = eng.episode.cpu().numpy() if anyd else None
         tgt = eng.get_block(C.FW_BLK_TARGET).cpu().numpy() if self.info_target else None
         met = eng.metrics.cpu().numpy() if (anyd and eng.metrics is not None) else None
@@ -303,8 +308,8 @@ class FixedWingVecEnv(VecEnv):
                 raise NotImplementedError("turbulence_noise for a subset of the envs")
             self.engine.set_noise(turbulence_noise)
         obs = self.engine.reset(mask=mask, init=init, target=tgt)
-        o = obs.cpu().numpy().astype(np.float32)
+        o = self._shaped(obs.cpu().numpy().astype(np.float32))
         return [o[i] for i in idx]
 
     def _out(self, t):
-        return t if self.return_tensors else t.cpu().numpy().astype(np.float32)
+        return self._shaped(t if self.return_tensors else t.cpu().numpy().astype(np.float32))
