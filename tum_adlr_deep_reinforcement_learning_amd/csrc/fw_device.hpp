@@ -43,6 +43,9 @@ constexpr int MAX_NFEV = 6000;
 #ifndef FW_ER_LDS
 #define FW_ER_LDS 1  // DOPRI error sum in LDS: frees 20 VGPRs of the RK loop (measured -3%)
 #endif
+#ifndef FW_P_LDS
+#define FW_P_LDS 0  // bitmask: RK stage accumulators P3/P4/P5/YB held in LDS instead of VGPRs (fp32)
+#endif
 #ifndef FW_RELAUNDER
 #define FW_RELAUNDER 0  // 1: re-issue config scalar loads per RHS (helped the generic kernel; -4.5% slower on the specialised one)
 #endif  // RHS evaluations per step before the step is declared a solver failure
@@ -515,6 +518,12 @@ template <typename T>
 using V2 = T __attribute__((ext_vector_type(2)));
 constexpr int NP = (NY + 1) / 2;
 
+// LDS slots (pairs per lane) the integrator needs: y, f, error sum, stage accumulators
+template <typename T>
+constexpr int lds_slots() {
+  return 2 + FW_ER_LDS + ((sizeof(T) == 4 && FW_P_LDS) ? 4 : 0);
+}
+
 template <typename T, typename C>
 FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy, V2<T>* __restrict__ sf, int stride,
                int& nfev, int& nacc, V2<T>* __restrict__ se = nullptr) {
@@ -539,11 +548,24 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
 #if FW_ER_LDS
   // error accumulator in this lane's third LDS slot (registers go to the live stage vectors)
 #define ERV(p) se[(p) * stride]
-  V P3[NP], P4[NP], P5[NP], YB[NP], ys[NP], K[NP];
+  V ys[NP], K[NP];
 #else
-  V P3[NP], P4[NP], P5[NP], YB[NP], ER[NP], ys[NP], K[NP];
+  V ER[NP], ys[NP], K[NP];
 #define ERV(p) ER[p]
 #endif
+  // stage accumulators P3, P4, P5, YB (k = 0..3): VGPRs, or (fp32, bit k of FW_P_LDS) four more
+  // LDS slots of this lane after the error sum (the kernels size their LDS with lds_slots<T>())
+  constexpr unsigned PL = sizeof(T) == 4 ? (unsigned)FW_P_LDS : 0u;
+  V* const sp = (se ? se : sf) + NP * stride;
+  V Preg[4][NP];
+  auto PA = [&](int k, int p) -> V& {
+    if ((PL >> k) & 1u) return sp[(k * NP + p) * stride];
+    return Preg[k][p];
+  };
+#define P3 (0)
+#define P4 (1)
+#define P5 (2)
+#define YB (3)
 #pragma unroll
   for (int p = 0; p < NP; p++) {
     V v;
@@ -635,49 +657,49 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
       for (int p = 0; p < NP; p++) {
         const V f = F(p);
         ys[p] = YR(p) + (f * T(A20) + K[p] * T(A21)) * ht;
-        P3[p] = f * T(A30) + K[p] * T(A31);
-        P4[p] = f * T(A40) + K[p] * T(A41);
-        P5[p] = f * T(A50) + K[p] * T(A51);
-        YB[p] = f * T(B0);
+        PA(P3, p) = f * T(A30) + K[p] * T(A31);
+        PA(P4, p) = f * T(A40) + K[p] * T(A41);
+        PA(P5, p) = f * T(A50) + K[p] * T(A51);
+        PA(YB, p) = f * T(B0);
         ERV(p) = f * T(E0);
       }
       stage = 3;
     } else if (stage == 3) {  // K = K2
 #pragma unroll
       for (int p = 0; p < NP; p++) {
-        P3[p] += K[p] * T(A32);
-        P4[p] += K[p] * T(A42);
-        P5[p] += K[p] * T(A52);
-        YB[p] += K[p] * T(B2);
+        PA(P3, p) += K[p] * T(A32);
+        PA(P4, p) += K[p] * T(A42);
+        PA(P5, p) += K[p] * T(A52);
+        PA(YB, p) += K[p] * T(B2);
         ERV(p) += K[p] * T(E2);
-        ys[p] = YR(p) + P3[p] * ht;
+        ys[p] = YR(p) + PA(P3, p) * ht;
       }
       stage = 4;
     } else if (stage == 4) {  // K = K3
 #pragma unroll
       for (int p = 0; p < NP; p++) {
-        P4[p] += K[p] * T(A43);
-        P5[p] += K[p] * T(A53);
-        YB[p] += K[p] * T(B3);
+        PA(P4, p) += K[p] * T(A43);
+        PA(P5, p) += K[p] * T(A53);
+        PA(YB, p) += K[p] * T(B3);
         ERV(p) += K[p] * T(E3);
-        ys[p] = YR(p) + P4[p] * ht;
+        ys[p] = YR(p) + PA(P4, p) * ht;
       }
       stage = 5;
     } else if (stage == 5) {  // K = K4
 #pragma unroll
       for (int p = 0; p < NP; p++) {
-        P5[p] += K[p] * T(A54);
-        YB[p] += K[p] * T(B4);
+        PA(P5, p) += K[p] * T(A54);
+        PA(YB, p) += K[p] * T(B4);
         ERV(p) += K[p] * T(E4);
-        ys[p] = YR(p) + P5[p] * ht;
+        ys[p] = YR(p) + PA(P5, p) * ht;
       }
       stage = 6;
     } else if (stage == 6) {  // K = K5; ys <- y_new
 #pragma unroll
       for (int p = 0; p < NP; p++) {
-        YB[p] += K[p] * T(B5);
+        PA(YB, p) += K[p] * T(B5);
         ERV(p) += K[p] * T(E5);
-        ys[p] = YR(p) + ht * YB[p];
+        ys[p] = YR(p) + ht * PA(YB, p);
       }
       stage = 7;
     } else {  // K = f(t_new, y_new): error norm + step control (rk.py:138-173)
@@ -746,6 +768,10 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
 #undef F
 #undef ERV
 #undef YR
+#undef P3
+#undef P4
+#undef P5
+#undef YB
   return result;
 }
 

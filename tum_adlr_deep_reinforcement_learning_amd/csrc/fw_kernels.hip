@@ -742,7 +742,7 @@ __global__ __launch_bounds__(BLOCK) void k_sim_step(const DevCfg<T>* __restrict_
   turbulence_at(c, s, i, s.episode[i], k, tl, ta);
   int nfev = 0, nacc = 0;
   uint32_t dmask = 0;
-  __shared__ V2<T> lds[(2 + FW_ER_LDS) * NP * BLOCK];  // y, f (+ error sum) of the block's aircraft (pairs)
+  __shared__ V2<T> lds[lds_slots<T>() * NP * BLOCK];  // y, f (+ error sum) of the block's aircraft (pairs)
   const int term = sim_step_masked(c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
                                    lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i});
   if (term) {  // uncommitted derived values keep their previous (history[-1]) value
@@ -803,7 +803,7 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
   int nfev = 0, nacc = 0;
   uint32_t dmask = 0;
 #if FW_LDS_STATE
-  __shared__ V2<T> lds[(2 + FW_ER_LDS) * NP * BLOCK];  // y, f (+ error sum) of the block's aircraft (pairs)
+  __shared__ V2<T> lds[lds_slots<T>() * NP * BLOCK];  // y, f (+ error sum) of the block's aircraft (pairs)
   const int sterm = sim_step_masked(c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
                                     lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i});
 #else
