@@ -22,6 +22,7 @@ Fixtures (all float64 unless noted):
   env_pid_set.npz         PID replay of a synthetic 40-scenario evaluation set
   env_metrics.npz         episode metrics + histories for metric scenarios
   env_obs_hist.npz        observation-history episodes (observation.length > 1)
+  pyfly_envelope.npz      the reference's own sensitivity to a 1e-7 initial perturbation (fp32 gate)
 """
 import hashlib
 import json
@@ -358,6 +359,124 @@ def gen_traj():
     np.savez_compressed(os.path.join(OUT, "pyfly_traj.npz"), **out)
 
 
+TRAJ_CASES = [("pid_off", False, 0, None), ("pid_on", True, 0, None), ("rand_off", False, 1, None),
+              ("rand_on", True, 2, None), ("rand_fail", True, 3, 45.0)]
+
+
+def _replay_open_loop(name, turb_on, seed, olim, cmds, L, perturb, post=None):
+    """Replay a pyfly_traj case open-loop from its recorded commands; perturb(st, cmd, k) edits inputs."""
+    rng = np.random.RandomState(seed)
+    sim = pf.PyFly(PYFLY_CFG, PYFLY_PARAM, config_kw={"turbulence": turb_on, "turbulence_sim_length": L})
+    if olim is not None:
+        for n in ["omega_p", "omega_q", "omega_r"]:
+            sim.state[n].constraint_min = np.radians(-olim)
+            sim.state[n].constraint_max = np.radians(olim)
+    sim.seed(seed)
+    st = random_state(rng, omega_deg=60.0 if olim is None else 0.5 * olim, dots=False)
+    st["roll"], st["pitch"] = -0.5, 0.15
+    wind = random_wind(rng) if turb_on else [0.0, 0.0, 0.0]
+    n_chunks = (len(cmds) + L - 1) // L + 1
+    noise = rng.standard_normal((4, L * n_chunks)) if turb_on else np.zeros((4, L * n_chunks))
+    perturb(st, None, -1)
+    st["wind"] = wind
+    sim.reset(state=st, turbulence_noise=noise if turb_on else None)
+    ys, fail = [ode_vector(sim)], len(cmds)
+    for s in range(len(cmds)):
+        cmd = [float(c) for c in cmds[s]]
+        perturb(None, cmd, s)
+        ok, _ = sim.step(cmd)
+        if not ok:
+            fail = s
+            break
+        if post is not None:
+            post(sim, s)
+        ys.append(ode_vector(sim))
+    return np.array(ys), fail
+
+
+def gen_envelope(eps=1e-7, n_pert=3):
+    """The reference's own sensitivity (SURVEY.md 8 d, gate 3), per step and ODE component, as the
+    maximum absolute deviation from the pyfly_traj.npz trajectory when the trajectory is replayed
+    open-loop (its recorded commands) with perturbed inputs:
+      dev_eps   initial state entries scaled by (1 +- eps), n_pert random sign patterns
+      dev_fp32  initial state and every step's commands rounded to float32 (what an fp32 engine is
+                handed), the arithmetic still fp64
+      dev_rtol  initial state scaled by (1 +- rtol = 1e-3): one solver-tolerance-sized kick, the size
+                of the state change an RK45 accept/reject decision that goes the other way makes
+      dev_state32  fp32 inputs and the ODE state rounded to float32 after every step (nearest; and
+                nearest +- 1 ulp at random for the other patterns)
+    plus the perturbed runs' termination steps (fail_*)."""
+    d = np.load(os.path.join(OUT, "pyfly_traj.npz"))
+    out = {}
+    for name, turb_on, seed, olim in TRAJ_CASES:
+        g = lambda k: d[name + "__" + k]  # noqa: E731
+        cmds, y_ref, L = g("cmd"), g("y"), int(g("L"))
+
+        def dev_of(perturb_factory, reps):
+            dev = np.zeros_like(y_ref)
+            fails = []
+            for k in range(reps):
+                yp, f = _replay_open_loop(name, turb_on, seed, olim, cmds, L, perturb_factory(k))
+                n = min(len(yp), len(y_ref))
+                dev[:n] = np.maximum(dev[:n], np.abs(yp[:n] - y_ref[:n]))
+                fails.append(f)
+            return dev, np.array(fails)
+
+        def scaled(e):
+            def factory(k):
+                prng = np.random.RandomState(1000 * (1 + int(e == 1e-3)) + k)
+
+                def pert(st, cmd, kk):
+                    if st is not None:
+                        for key in ENV_STATE_KEYS:
+                            st[key] = st[key] * (1.0 + e * prng.choice([-1.0, 1.0]))
+                return pert
+            return factory
+
+        def to32_factory(k):
+            def to32(st, cmd, kk):
+                if st is not None:
+                    for key in ENV_STATE_KEYS:
+                        st[key] = float(np.float32(st[key]))
+                if cmd is not None:
+                    cmd[:] = [float(np.float32(c)) for c in cmd]
+            return to32
+
+        def state32(k):
+            # the ODE state stored in float32 after every step (round to nearest, plus for k > 0 a
+            # random +-1 ulp): an fp32 engine's per-step rounding, with fp64 arithmetic in between
+            prng = np.random.RandomState(3000 + k)
+
+            def post(sim, s):
+                y = ode_vector(sim).astype(np.float32)
+                if k > 0:
+                    y = np.nextafter(y, np.where(prng.rand(len(y)) < 0.5, -np.inf, np.inf).astype(np.float32))
+                sim._set_states_from_ode_solution(y.astype(np.float64), save=False)
+            return post
+
+        def dev_state32(reps):
+            dev = np.zeros_like(y_ref)
+            fails = []
+            for k in range(reps):
+                yp, f = _replay_open_loop(name, turb_on, seed, olim, cmds, L, to32_factory(k), post=state32(k))
+                n = min(len(yp), len(y_ref))
+                dev[:n] = np.maximum(dev[:n], np.abs(yp[:n] - y_ref[:n]))
+                fails.append(f)
+            return dev, np.array(fails)
+
+        for tag, fac, reps in (("eps", scaled(eps), n_pert), ("fp32", to32_factory, 1), ("rtol", scaled(1e-3), n_pert),
+                               ("state32", None, n_pert)):
+            dev, fails = dev_state32(reps) if tag == "state32" else dev_of(fac, reps)
+            out[name + "__dev_" + tag] = dev
+            out[name + "__fail_" + tag] = fails
+            rms = np.sqrt(np.mean(y_ref ** 2, axis=0)) + 1e-3
+            e = np.max(dev / rms, axis=1)
+            print("%s %s: scaled deviation at 100 %.2e, 500 %.2e, max %.2e, fails %s"
+                  % (name, tag, e[min(100, len(e) - 1)], e[min(500, len(e) - 1)], e.max(), fails))
+    out["eps"] = np.array(eps)
+    np.savez_compressed(os.path.join(OUT, "pyfly_envelope.npz"), **out)
+
+
 # ---------------------------------------------------------------------------
 # C. Dryden
 # ---------------------------------------------------------------------------
@@ -598,13 +717,17 @@ def gen_obs_hist():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["single", "traj", "dryden", "env", "pidset", "metrics", "obshist"]
+    which = sys.argv[1:] or ["single", "traj", "envelope", "dryden", "env", "pidset", "metrics", "obshist"]
+    if "envelope" in which and "traj" not in which:
+        gen_envelope()
     if "obshist" in which:
         gen_obs_hist()
     if "single" in which:
         gen_single_step()
     if "traj" in which:
         gen_traj()
+        if "envelope" in which:
+            gen_envelope()
     if "dryden" in which:
         gen_dryden()
     if "env" in which:

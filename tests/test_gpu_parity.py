@@ -6,6 +6,11 @@ Tolerances (relative metric |d| / (|ref| + 1e-3)):
   fp64 kernel, free-running 1000 steps ........... <= 1e-7 (+ step-count parity)
   fp32 kernel, teacher-forced single step ........ median <= 1e-6, >= 97 % of cases <= 1e-4
                                                     (the rest are RK45 accept/reject flips)
+  fp32 kernel, free-running 1000 steps ........... within 5x the reference's own deviation under
+                                                    per-step float32 state storage (+ rtol kick after
+                                                    the first accept/reject flip), same termination +-1
+  PID evaluation set (40 scenarios) .............. fp64: lengths exact (all but <= 1), rewards <= 1e-6;
+                                                    fp32: >= 69 % exact, >= 92 % within 4 steps
   env sequences fp64 ............................. obs/reward <= 1e-6 abs, identical done/termination
 """
 import numpy as np
@@ -277,3 +282,127 @@ def test_generic_and_specialised_kernels_agree(precision, monkeypatch):
             close = ((o1 - o2).abs() <= 1e-4 * (1 + o2.abs())).all(1) & ((r1 - r2).abs() <= 1e-4 * (1 + r2.abs()))
             assert close.float().mean() >= 0.99
             assert (d1 == d2).float().mean() >= 0.99
+
+
+def _free_run(name, precision):
+    """Free-running PyFly.step replay of a pyfly_traj.npz case: per-step |y - y_ref| per component, the
+    step of the first RK45 accept/reject divergence from the reference (nfev differs), fail steps."""
+    d = F.load("pyfly_traj.npz")
+    g = lambda k: d[name + "__" + k]  # noqa: E731
+    turb = bool(g("turb_on"))
+    spec = C.build_sim(config_kw={"turbulence": turb, "turbulence_sim_length": int(g("L"))})
+    for v in ("omega_p", "omega_q", "omega_r"):
+        spec.vars[v].constraint_min = -np.radians(float(g("omega_lim_deg")))
+        spec.vars[v].constraint_max = np.radians(float(g("omega_lim_deg")))
+    eng = _engine(spec, None, 1, precision)
+    eng.set_block(C.FW_BLK_ODE, g("y")[0][:, None])
+    der = np.zeros((8, 1))
+    der[:6, 0] = g("derived")[0][:6]
+    eng.set_block(C.FW_BLK_DERIVED, der)
+    eng.set_block(C.FW_BLK_WIND, g("wind")[:, None])
+    eng.set_block(C.FW_BLK_STEPS, np.zeros(1, np.int32))
+    if turb:
+        eng.set_noise(g("noise")[None])
+    cmds = torch.tensor(g("cmd"), dtype=eng.dtype, device="cuda:0")
+    dev = np.zeros_like(g("y"))
+    fail, first_flip = len(cmds), len(cmds)
+    for s in range(len(cmds)):
+        succ, term = eng.sim_step(cmds[s:s + 1], stats=True)
+        if int(eng.stats[0] & 0xFFFF) != int(g("nfev")[s]) and first_flip == len(cmds):
+            first_flip = s
+        if int(term[0]) != 0:
+            fail = s
+            break
+        dev[s + 1] = np.abs(eng.get_block(C.FW_BLK_ODE)[:, 0].double().cpu().numpy() - g("y")[s + 1])
+    eng.close()
+    ref_fail = len(cmds) if bool(g("success")[-1]) else len(cmds) - 1
+    rms = np.sqrt(np.mean(g("y") ** 2, axis=0)) + 1e-3  # per-component signal scale
+    return dev / rms, rms, fail, ref_fail, first_flip
+
+
+@pytest.mark.parametrize("name", ["pid_off", "pid_on", "rand_off", "rand_on", "rand_fail"])
+def test_free_running_trajectory_fp32_within_reference_envelope(name):
+    """SURVEY.md 8(d) gate 3, measured against the reference's OWN sensitivity (pyfly_envelope.npz: the
+    reference replaying the same 1000 commands from perturbed inputs).  Error metric per step: max over
+    ODE components of |y - y_ref| / rms(y_ref component), a component's error relative to its signal
+    scale (|y| + 1e-3 explodes at the zero crossings of the actuator rates).
+
+    Gate: termination step identical +-1, and at every step the error stays inside the band the
+    reference itself spans (running maxima) under either
+      * its ODE state STORED in float32 after every step (fp64 arithmetic in between; x5), or
+      * one solver-tolerance kick (initial state x (1 +- rtol = 1e-3)) -- the size of the state change
+        an RK45 accept/reject decision, or a stage crossing an actuator clip boundary, makes when fp32
+        rounding puts it on the other side.
+    Measured (round 1): max error / band 0.01-0.30; the first accept/reject divergence from the fp64
+    reference comes after 68-1000 steps.  A one-off relative 1e-7 perturbation of the initial state
+    (the survey's first proposal, also in the fixture as dev_eps) is exceeded 5-85x: fp32 re-rounds the
+    state every step and the dynamics amplify each rounding, which that yardstick does not model."""
+    E = F.load("pyfly_envelope.npz")
+    e, rms_ref, fail, ref_fail, flip = _free_run(name, "float32")
+    assert abs(fail - ref_fail) <= 1, (fail, ref_fail)
+    n = min(fail, ref_fail) + 1
+    err = e[:n].max(axis=1)
+    env32 = np.maximum.accumulate((E[name + "__dev_state32"][:n] / rms_ref).max(axis=1))
+    env_rtol = np.maximum.accumulate((E[name + "__dev_rtol"][:n] / rms_ref).max(axis=1))
+    band = np.maximum(np.maximum(5.0 * env32, env_rtol), 1e-5)
+    print("%s: first accept/reject flip at step %d; max err %.2e, max err/band %.2f"
+          % (name, flip, err.max(), (err / band).max()))
+    assert np.all(err <= band), int((err / band).argmax())
+
+
+def _pid_batch(precision):
+    """The 40-scenario PID evaluation set (env_pid_set.npz) as one batch of envs on the device."""
+    from _pid import PID
+    d = F.load("env_pid_set.npz")
+    ckw = {"steps_max": 1500, "action": {"scale_space": False},
+           "target": {"on_success": "done", "success_streak_fraction": 1, "success_streak_req": 100,
+                      "states": {0: {"bound": 5}, 1: {"bound": 5}, 2: {"bound": 2}}}}
+    spec = C.EnvSpec(config_kw=ckw, sim_config_kw={"turbulence": False})
+    n = len(d["length"])
+    init = np.full((C.FW_NINIT, n), np.nan)
+    init[:12] = d["init"].T
+    init[C.FW_I_ACT0:C.FW_I_ACT2_DOT + 1] = 0.0
+    init[C.FW_I_WIND_N:] = 0.0
+    eng = _engine(spec.sim, spec, n, precision)
+    obs = eng.reset(init=init, target=d["target"].T).double().cpu().numpy()
+    pids = [PID(*d["target"][i]) for i in range(n)]
+    length = np.zeros(n, int)
+    rew = np.zeros((n, 1500))
+    alive = np.ones(n, bool)
+    for s in range(1500):
+        a = np.stack([pids[i].action(obs[i]) for i in range(n)])
+        o, r, dn, _ = eng.env_step(torch.tensor(a, dtype=eng.dtype, device="cuda:0"), auto_reset=False)
+        o, r, dn = o.double().cpu().numpy(), r.double().cpu().numpy(), dn.cpu().numpy().astype(bool)
+        for i in np.nonzero(alive)[0]:
+            pids[i].set_reference(*o[i, 6:9])
+            rew[i, s] = r[i]
+            length[i] += 1
+            if dn[i]:
+                alive[i] = False
+        obs = o
+        if not alive.any():
+            break
+    eng.close()
+    return d, length, rew
+
+
+def test_pid_evaluation_set_fp64_episode_lengths_and_rewards():
+    """SURVEY.md 8(d) gate 4, fp64: the device reproduces the reference's PID replay of the evaluation
+    set (episode lengths exact on all but at most one scenario, per-step rewards within 1e-6 + 1e-6/step)."""
+    d, length, rew = _pid_batch("float64")
+    exact = int((length == d["length"]).sum())
+    assert exact >= len(length) - 1, (exact, length, d["length"])
+    for i in np.nonzero(length == d["length"])[0]:
+        L = length[i]
+        tol = 1e-6 + 1e-6 * np.arange(L)
+        assert np.all(np.abs(rew[i, :L] - d["reward"][i, :L]) <= tol), i
+
+
+def test_pid_evaluation_set_fp32_episode_lengths():
+    """SURVEY.md 8(d) gate 4, fp32: within the loose bound the reference itself shows against its stored
+    eval_res_PID_none.npy (>= 69% exact episode lengths, >= 92% within 4 steps)."""
+    d, length, _ = _pid_batch("float32")
+    exact = (length == d["length"]).mean()
+    near = (np.abs(length - d["length"]) <= 4).mean()
+    print("fp32 PID set: exact %.3f, within 4 steps %.3f" % (exact, near))
+    assert exact >= 0.69 and near >= 0.92, (exact, near, length, d["length"])
