@@ -173,9 +173,19 @@ def test_env_sequences_fp64(name):
 
 def test_env_matches_oracle_fp64_batch():
     """64 envs, random actions incl. out-of-range, 400 steps: fp64 kernel == oracle step by step."""
+    _batch_vs_oracle(64, 400, 5)
+
+
+@pytest.mark.parametrize("n", [1, 63, 257])
+def test_env_matches_oracle_fp64_ragged_batches(n):
+    """Batch sizes that fill neither a wave (64) nor a block (256): the lanes past N are masked and
+    every live lane still equals the oracle (SubprocVecEnv accepts any env count)."""
+    _batch_vs_oracle(n, 150, 11 + n)
+
+
+def _batch_vs_oracle(n, steps, seed):
     spec = C.EnvSpec(config_kw={"steps_max": 250}, sim_config_kw={"turbulence": False})
-    n = 64
-    rng = np.random.RandomState(5)
+    rng = np.random.RandomState(seed)
     init = np.full((C.FW_NINIT, n), np.nan)
     d2r = np.radians
     init[C.FW_I_ROLL] = rng.uniform(d2r(-110), d2r(110), n)
@@ -197,7 +207,7 @@ def test_env_matches_oracle_fp64_batch():
     for j in range(n):
         np.testing.assert_allclose(envs[j].reset(init[:, j], tgt[:, j]), obs[j], rtol=1e-12, atol=1e-12)
     alive = np.ones(n, bool)
-    for s in range(400):
+    for s in range(steps):
         a = rng.uniform(-1.3, 1.3, (n, 3))
         o, r, dn, tm = eng.env_step(torch.tensor(a, device="cuda:0"), auto_reset=False)
         o, r, dn, tm = o.cpu().numpy(), r.cpu().numpy(), dn.cpu().numpy(), tm.cpu().numpy()
@@ -213,10 +223,11 @@ def test_env_matches_oracle_fp64_batch():
             break
 
 
-def test_full_size_properties_fp32():
-    """65536 envs, 300 steps of U(-1,1) actions with auto-reset: finite, bounded, deterministic, shard-invariant."""
+@pytest.mark.parametrize("n", [65536, 262144 + 37])
+def test_full_size_properties_fp32(n):
+    """65536 envs (configs[2]) and a ragged batch above the largest config (262144 + 37), 300 steps of
+    U(-1,1) actions with auto-reset: finite, bounded, deterministic, shard-invariant."""
     spec = C.EnvSpec(sim_config_kw={"turbulence": False})
-    n = 65536
 
     def run(seed, offset=0, count=n, steps=300):
         eng = _engine(spec.sim, spec, count, "float32")
