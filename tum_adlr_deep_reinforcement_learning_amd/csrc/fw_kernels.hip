@@ -5,7 +5,7 @@
 // multiple of 64, so lane i of a wave touches element i of each row: every
 // global access below is a coalesced dword (or dwordx2 for fp64) per lane.
 //
-// Kernels (one lane = one aircraft, 256-thread blocks, the RK45 state and
+// Kernels (one lane = one aircraft, one-wave blocks, the RK45 state and
 // stage vectors staged in LDS, no MFMA -- the work is elementwise ODE
 // integration):
 //   k_env_step   FixedWingAircraft.step + PyFly.step + masked auto-reset (hot path)
@@ -46,7 +46,10 @@ int set_err(int code, const std::string& msg) { return fw::set_error(code, msg);
     if (e_ != hipSuccess) return set_err(FW_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
   } while (0)
 
-constexpr int BLOCK = 256;
+#ifndef FW_BLOCK
+#define FW_BLOCK 64  // threads per block: one wave (measured 1-2% faster than 256, profiles/r01_ab_block.log)
+#endif
+constexpr int BLOCK = FW_BLOCK;
 #ifndef FW_LDS_STATE
 #define FW_LDS_STATE 1  // 0 = y/f in VGPRs (measured: 512 VGPRs + spills, slower)
 #endif
