@@ -3,14 +3,23 @@
 
 One "step" = one FixedWingAircraft.step (PyFly.step with scipy-RK45 step
 control + env epilogue + masked auto-reset) for every aircraft of the batch,
-i.e. one launch of k_env_step over N = --envs aircraft per GPU.  Actions are
-uniform random in [-1, 1]^3, pre-generated on the device (a pool of 16 batches
-cycled), so the timed region contains only the hot path.
+i.e. one launch of k_env_step per GPU.  Actions are uniform random in [-1, 1]^3,
+pre-generated on the device (a pool of 16 batches cycled), so the timed region
+contains only the hot path.
 
-Workload (BASELINE.json configs[2]): 65536 parallel aircraft per GPU,
-attitude-tracking task (fixed_wing_config.json defaults), fp32, turbulence off.
-Multi-GPU: one process per GPU (torchrun), each rank owns its own 65536 envs
-(weak scaling, disjoint Philox streams), no collective on the data path.
+Workload (BASELINE.json metric / configs[2]-[3]): 65536 aircraft in TOTAL
+(``--envs``), attitude-tracking task (fixed_wing_config.json defaults), fp32,
+turbulence off.  With ``--gpus N`` the 65536 aircraft are split over N GPUs
+(8192 per GPU at N = 8: strong scaling, configs[3]); one process per GPU, each
+rank owns a contiguous env range with disjoint Philox streams, no collective on
+the data path.  ``python bench.py --gpus N`` launches the N ranks itself (before
+any GPU call) unless it already runs under torchrun, where WORLD_SIZE must equal N.
+
+Steady state: after the global reset the population first runs ``--prep`` (1000)
+untimed steps, so the timed window always sees the steady-state mix of
+mid-episode, tumbling (straggler) and freshly reset aircraft whatever
+``--warmup`` is; the first 96 steps after the reset are timed separately and
+reported as ``early_regime``.
 
 Prints ONE JSON line (rank 0).
 """
@@ -225,56 +234,58 @@ def sac_fill_leg(n, K, dev, rank, world, precision):
     return out
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    # defaults time a steady-state window: over the first ~200 steps after the global reset no aircraft
-    # has tumbled into the stiff regimes whose RK45 steps need hundreds of RHS evaluations
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=1000)
-    ap.add_argument("--envs", type=int, default=65536, help="aircraft per GPU")
-    ap.add_argument("--precision", default="float32", choices=["float32", "float64"])
-    ap.add_argument("--turbulence", action="store_true", help="light Dryden turbulence + random steady wind")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-procs", type=int, default=None, help="CPU baseline processes (default: min(16, cores))")
-    ap.add_argument("--no-metrics", action="store_true",
-                    help="do not track the config's streaming episode metrics (fixed_wing.py:1644-1736)")
-    ap.add_argument("--rollout-steps", type=int, default=0,
-                    help="also run one PPO collect_rollouts of this horizon (2048 = BASELINE configs[2]/[3])")
-    ap.add_argument("--sac-fill-steps", type=int, default=0,
-                    help="also run a SAC replay-buffer fill of this many steps (BASELINE configs[4])")
-    ap.add_argument("--sac-envs", type=int, default=262144, help="global envs of the SAC fill leg")
-    args = ap.parse_args()
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2.0  # wave64 VALU instructions/s: 1024 SIMDs, one per 2 cycles at 2.4 GHz
+REFERENCE_CPU = {"value": 814.0, "unit": "env-steps/s", "cores": 8, "kind": "reference",
+                 "sample": "reference VecNormalize(SubprocVecEnv([FixedWingAircraft] x 8)), default task, turbulence "
+                           "off, U(-1,1) actions, 300 steps per env; measured in the survey container (8 vCPU Xeon, "
+                           "SURVEY.md 6 / BASELINE.md 2) -- the reference is not shipped to the GPU box"}
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # CPU baseline first: its worker processes are forked, which must happen before any HIP call
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds, args.cpu_procs)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
 
-    # pyfly_config.json defaults: random steady wind |w| <= 8 m/s; Dryden only with --turbulence
-    spec = C.EnvSpec(sim_config_kw={"turbulence": bool(args.turbulence), "turbulence_intensity": "light"})
-    spec.metrics_enabled = not args.no_metrics
-    n = args.envs
+def _self_launch(args):
+    """--gpus N outside torchrun: start N ranks as child processes (nothing here has touched the GPU)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
+def _pmc_record(n, args, spec):
+    """profiles/pmc_env_step.json when it was measured on this very workload (else None)."""
+    pmc = os.path.join(ROOT, "profiles", "pmc_env_step.json")
+    try:
+        with open(pmc) as f:
+            pm = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if pm.get("envs") == n and pm.get("precision") == args.precision and \
+            bool(pm.get("turbulence")) == bool(args.turbulence) and \
+            bool(pm.get("metrics", True)) == bool(spec.metrics_enabled) and pm.get("regime") == "steady":
+        return pm
+    return None
+
+
+def timed_env_steps(n, args, spec, dev, rank, world, env_offset, early=True):
+    """Steady-state timing of ``args.steps`` env steps of ``n`` aircraft on this rank.
+
+    Returns (elapsed_s, kernel_ms, early_ms) with elapsed/kernel_ms max-reduced over ranks."""
     eng = Engine(spec.sim, spec, n, device=dev, precision=args.precision)
-    eng.seed(1234, env_offset=rank * n)
+    eng.seed(1234, env_offset=env_offset)
     eng.reset()
     gen = torch.Generator(device=dev)
     gen.manual_seed(1 + rank)
     pool = torch.rand(16, n, 3, generator=gen, device=dev, dtype=eng.dtype) * 2 - 1
-
-    # the K timed steps are issued as replays of a HIP graph of G captured launches (engine.StepGraph):
-    # one host call per G steps, so the box's host jitter never leaves the device idle between steps
+    # the steps are issued as replays of a HIP graph of G captured launches (engine.StepGraph): one host
+    # call per G steps, so the box's host jitter never leaves the device idle between steps
     G = 16
-    eng.env_step(pool[0], stats=False)  # first warm-up step, eager (kernel load outside the capture)
+    eng.env_step(pool[0], stats=False)  # first step eager (kernel load outside the capture)
     graph = StepGraph(eng, pool)
+    done_steps = 1
 
     def run(k):
         for _ in range(k // G):
@@ -282,13 +293,23 @@ def main():
         for s in range(k % G):
             eng.env_step(pool[s], stats=False)
 
-    run(max(args.warmup - 1, 0))
+    stream = torch.cuda.current_stream(dev)
+    early_ms = None
+    if early:  # early-episode regime: the first 96 steps after the global reset (no stragglers yet)
+        torch.cuda.synchronize(dev)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        run(96)
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        early_ms = a.elapsed_time(b) / 96
+        done_steps += 96
+    run(max(args.prep - done_steps, 0))  # steady-state population
+    run(args.warmup)
     torch.cuda.synchronize(dev)
-
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    stream = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
@@ -301,36 +322,90 @@ def main():
     # k_env_step device duration per launch: HIP events on the launch stream around the timed steps
     # themselves (graph replays keep the queue full, so this is kernel time plus dispatch gaps)
     kern_ms = ev0.elapsed_time(ev1) / args.steps
-    el = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    el = torch.tensor([elapsed, kern_ms, early_ms or 0.0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms = float(el[0]), float(el[1])
+    eng.close()
+    del graph
+    return float(el[0]), float(el[1]), (float(el[2]) if early else None)
 
-    total_steps = n * world * args.steps
-    value = total_steps / elapsed
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--prep", type=int, default=1000,
+                    help="untimed steps after the global reset that build the steady-state population")
+    ap.add_argument("--envs", type=int, default=65536, help="aircraft in total, split over the GPUs")
+    ap.add_argument("--precision", default="float32", choices=["float32", "float64"])
+    ap.add_argument("--turbulence", action="store_true", help="light Dryden turbulence + random steady wind")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-procs", type=int, default=None, help="CPU baseline processes (default: min(16, cores))")
+    ap.add_argument("--no-metrics", action="store_true",
+                    help="do not track the config's streaming episode metrics (fixed_wing.py:1644-1736)")
+    ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling line (65536 aircraft per GPU)")
+    ap.add_argument("--rollout-steps", type=int, default=0,
+                    help="also run one PPO collect_rollouts of this horizon (2048 = BASELINE configs[2]/[3])")
+    ap.add_argument("--sac-fill-steps", type=int, default=0,
+                    help="also run a SAC replay-buffer fill of this many steps (BASELINE configs[4])")
+    ap.add_argument("--sac-envs", type=int, default=262144, help="global envs of the SAC fill leg")
+    args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_self_launch(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.envs % world:
+        print("bench.py: --envs %d does not split evenly over %d GPUs" % (args.envs, world), file=sys.stderr)
+        sys.exit(2)
+    # CPU baseline first: its worker processes are forked, which must happen before any HIP call
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds, args.cpu_procs)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    # pyfly_config.json defaults: random steady wind |w| <= 8 m/s; Dryden only with --turbulence
+    spec = C.EnvSpec(sim_config_kw={"turbulence": bool(args.turbulence), "turbulence_intensity": "light"})
+    spec.metrics_enabled = not args.no_metrics
+    n = args.envs // world  # strong scaling: the global batch is split over the GPUs
+    elapsed, kern_ms, early_ms = timed_env_steps(n, args, spec, dev, rank, world, rank * n)
+    value = args.envs * args.steps / elapsed
+
+    weak = None
+    if world > 1 and not args.no_weak:  # secondary: 65536 aircraft per GPU
+        nw = 65536
+        w_el, w_k, _ = timed_env_steps(nw, args, spec, dev, rank, world, rank * nw, early=False)
+        weak = {"envs_per_gpu": nw, "global_envs": nw * world, "value": nw * world * args.steps / w_el,
+                "ms_per_step": w_el / args.steps * 1e3, "kernel_ms": w_k}
+
     esz = 4 if args.precision == "float32" else 8
     rd, wr = algorithmic_bytes_per_env_step(spec, esz)
     achieved = (rd + wr) * n / (kern_ms * 1e-3) / 1e9  # GB/s per GPU, dominant kernel
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_env_step.json")
-    if os.path.exists(pmc):
-        try:
-            with open(pmc) as f:
-                pm = json.load(f)
-            if pm.get("envs") == n and pm.get("precision") == args.precision and \
-                    bool(pm.get("turbulence")) == bool(args.turbulence) and \
-                    bool(pm.get("metrics", True)) == bool(spec.metrics_enabled):
-                traffic = pm.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    pm = _pmc_record(n, args, spec)
+    traffic = pm.get("hbm_bytes_per_launch") if pm else None
+    roof_valu = None
+    if pm and pm.get("valu_insts_per_launch"):
+        valu_rate = pm["valu_insts_per_launch"] / (kern_ms * 1e-3)
+        roof_valu = {"bound": "valu", "achieved": valu_rate / 1e9, "peak": VALU_ISSUE_PEAK / 1e9,
+                     "unit": "Ginst/s (wave64 VALU issue)", "frac": valu_rate / VALU_ISSUE_PEAK,
+                     "valu_insts_per_launch": pm["valu_insts_per_launch"],
+                     "valu_insts_per_wave": pm["valu_insts_per_launch"] * 64.0 / n,
+                     "source": "profiles/pmc_env_step.json (SQ_INSTS_VALU, steady-state dispatches)"}
 
     rollout = None
     if args.rollout_steps > 0:
-        eng.close()
         rollout = rollout_leg(spec, n, args.rollout_steps, dev, rank, world, args.precision)
     sac = None
     if args.sac_fill_steps > 0:
-        eng.close()
         sac = sac_fill_leg(args.sac_envs // world, args.sac_fill_steps, dev, rank, world, args.precision)
 
     if rank == 0:
@@ -343,23 +418,30 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32" if args.precision == "float32" else "f64",
-            "data": "synthetic (seeded Philox initial states, U(-1,1) actions pre-generated on device)",
-            "config": {"workload": "FixedWingAircraft.step x %d aircraft per GPU (attitude task, fixed_wing_config "
-                                   "defaults, %s, RK45 rtol=1e-3 atol=1e-6, auto-reset)"
-                                   % (n, "light Dryden + steady wind" if args.turbulence else
+            "data": "synthetic: seeded Philox initial states, U(-1,1) actions pre-generated on device; timed in the "
+                    "steady state (%d untimed steps after the global reset, then %d warm-up steps)"
+                    % (args.prep, args.warmup),
+            "config": {"workload": "FixedWingAircraft.step x %d aircraft in total, %d per GPU (attitude task, "
+                                   "fixed_wing_config defaults, %s, RK45 rtol=1e-3 atol=1e-6, auto-reset)"
+                                   % (args.envs, n, "light Dryden + steady wind" if args.turbulence else
                                       "steady wind, turbulence off")
-                                   + (", streaming episode metrics" if spec.metrics_enabled else "")
-                                   + ", timed after %d warm-up steps" % args.warmup,
-                       "envs_per_gpu": n, "global_envs": n * world, "kernel": "k_env_step",
+                                   + (", streaming episode metrics" if spec.metrics_enabled else ""),
+                       "global_envs": args.envs, "envs_per_gpu": n, "kernel": "k_env_step",
                        "parallelism": "env-dp%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "algorithmic_bytes_per_env_step": rd + wr, "kernel_ms": kern_ms},
+                         "algorithmic_bytes_per_env_step": rd + wr, "kernel_ms": kern_ms,
+                         "binding_limit": "valu issue + RK45 straggler latency (see roofline_valu, DESIGN.md 3)"},
+            "roofline_valu": roof_valu,
+            "early_regime": {"steps": 96, "kernel_ms": early_ms, "env_steps_per_s_per_gpu": n / (early_ms * 1e-3)},
             "cpu_baseline": cpu,
+            "cpu_baseline_reference": REFERENCE_CPU,
         }
+        if weak is not None:
+            out["weak_scaling"] = weak
         if rollout is not None:
             out["rollout"] = rollout
         if sac is not None:

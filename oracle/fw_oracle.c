@@ -280,14 +280,27 @@ static double rms(const double* x) {
 }
 
 /* Integrate y from 0 to dt (solve_ivp defaults).  Returns termination code
- * (0 = ok).  On success y_out holds sol.y[:, -1].  Counts accepted steps.    */
+ * (0 = ok, > 0 = constraint, -1 = solver failure).  y_out holds sol.y[:, -1]:
+ * the final state, or on a solver failure the last ACCEPTED sub-step (y0 if
+ * none) -- solve_ivp appends only accepted steps to sol.y (ivp.py:654-672) and
+ * pyfly.py:1393-1396 saves sol.y[:, -1] whatever sol.status is.  Solver
+ * failure = TOO_SMALL_STEP (rk.py:128-129; also taken on a NaN step size, where
+ * scipy itself would loop for ever) or the max_nfev RHS-evaluation budget
+ * (this build's guard; 0 = 6000).  Counts accepted steps.                     */
 static int rk45(ctx* X, const double* y0, double* y_out, int* naccept) {
   const fw_sim_config* c = X->c;
   double rtol = c->rtol, atol = c->atol, t_bound = c->dt;
+  const int budget = c->max_nfev > 0 ? c->max_nfev : 6000;
   double f[NY], y[NY];
   int t_;
   memcpy(y, y0, sizeof(y));
-  if ((t_ = rhs(X, 1, y, f))) return t_; /* RungeKutta.__init__ rk.py:95 */
+  *naccept = 0;
+#define RHS_(first, yy, ff)                          \
+  do {                                               \
+    if ((t_ = rhs(X, (first), (yy), (ff)))) return t_; \
+    if (X->nfev >= budget) goto solver_failed;       \
+  } while (0)
+  RHS_(1, y, f); /* RungeKutta.__init__ rk.py:95 */
   /* select_initial_step common.py:68-134 */
   double sc[NY], tmp[NY];
   double interval = fabs(t_bound - 0.0);
@@ -300,7 +313,7 @@ static int rk45(ctx* X, const double* y0, double* y_out, int* naccept) {
   if (h0 > interval) h0 = interval;
   double y1[NY], f1[NY];
   for (int i = 0; i < NY; i++) y1[i] = y[i] + h0 * f[i];
-  if ((t_ = rhs(X, 0, y1, f1))) return t_;
+  RHS_(0, y1, f1);
   for (int i = 0; i < NY; i++) tmp[i] = (f1[i] - f[i]) / sc[i];
   double d2 = rms(tmp) / h0;
   double h1;
@@ -316,7 +329,6 @@ static int rk45(ctx* X, const double* y0, double* y_out, int* naccept) {
 
   double t = 0.0;
   double K[7][NY];
-  *naccept = 0;
   /* solve_ivp loop ivp.py:654-662 + OdeSolver.step base.py:175-206 */
   while (!(t - t_bound >= 0)) {
     /* RungeKutta._step_impl rk.py:111-173 */
@@ -325,7 +337,7 @@ static int rk45(ctx* X, const double* y0, double* y_out, int* naccept) {
     int rejected = 0, accepted = 0;
     double t_new = t, ynew[NY];
     while (!accepted) {
-      if (h_abs < min_step) return -1; /* TOO_SMALL_STEP -> solver failed (y stays) */
+      if (!(h_abs >= min_step)) goto solver_failed; /* TOO_SMALL_STEP (rk.py:128-129) */
       double h = h_abs;
       t_new = t + h;
       if (t_new - t_bound > 0) t_new = t_bound;
@@ -340,14 +352,14 @@ static int rk45(ctx* X, const double* y0, double* y_out, int* naccept) {
           for (int j = 0; j < s; j++) acc += K[j][i] * RK_A[s][j];
           ys[i] = y[i] + acc * h;
         }
-        if ((t_ = rhs(X, 0, ys, K[s]))) return t_;
+        RHS_(0, ys, K[s]);
       }
       for (int i = 0; i < NY; i++) {
         double acc = 0;
         for (int j = 0; j < 6; j++) acc += K[j][i] * RK_B[j];
         ynew[i] = y[i] + h * acc;
       }
-      if ((t_ = rhs(X, 0, ynew, K[6]))) return t_;
+      RHS_(0, ynew, K[6]);
       double err[NY];
       for (int i = 0; i < NY; i++) {
         double acc = 0;
@@ -373,6 +385,10 @@ static int rk45(ctx* X, const double* y0, double* y_out, int* naccept) {
   }
   memcpy(y_out, y, sizeof(y));
   return 0;
+solver_failed:
+  memcpy(y_out, y, sizeof(y));
+  return -1;
+#undef RHS_
 }
 
 /* ------------------------------------------------------------------------- */
@@ -443,11 +459,10 @@ int orc_sim_step(const fw_sim_config* c, double* y, double* der, double* hist, c
   *naccept = 0;
   if (t) { *nfev = 0; return t; }
   double y1[NY];
+  memcpy(y1, y, sizeof(y1));
   t = rk45(&X, y, y1, naccept);
   *nfev = X.nfev;
-  if (t < 0) { /* solver failure: reference saves sol.y[:, -1] == last accepted; not reached in practice */
-    return 0;
-  }
+  if (t < 0) t = 0; /* solver failure: sol.y[:, -1] (last accepted) is saved as usual (pyfly.py:1393-1396) */
   if (t) return t;
 
   /* _set_states_from_ode_solution(save=True) pyfly.py:1852-1881 -- commits in

@@ -23,6 +23,9 @@ Fixtures (all float64 unless noted):
   env_metrics.npz         episode metrics + histories for metric scenarios
   env_obs_hist.npz        observation-history episodes (observation.length > 1)
   pyfly_envelope.npz      the reference's own sensitivity to a 1e-7 initial perturbation (fp32 gate)
+  pyfly_solver_fail.npz   PyFly.step when the RK45 integration fails (sol.y[:, -1] committed)
+  pyfly_energy.npz        energy states along PID / constraint-terminated trajectories
+  env_curriculum.npz      set_curriculum_level ranges/constraints/targets and sampled resets
 """
 import hashlib
 import json
@@ -716,8 +719,191 @@ def gen_obs_hist():
     np.savez_compressed(os.path.join(OUT, "env_obs_hist.npz"), **out)
 
 
+
+# ---------------------------------------------------------------------------
+# I. solver failure: sol.y[:, -1] committed (pyfly.py:1393-1396)
+# ---------------------------------------------------------------------------
+
+
+class _Budget(Exception):
+    pass
+
+
+def _budget_rk45(budget):
+    """scipy's own RK45 that declares a step failure once ``budget`` RHS evaluations are spent.
+
+    Stands in for a TOO_SMALL_STEP failure, which no reference configuration can reach (pyfly
+    calls solve_ivp with the default tolerances on a continuous RHS).  Only the step method
+    changes: solve_ivp's loop (ivp.py), its sol.y bookkeeping (accepted steps only) and pyfly's
+    save of sol.y[:, -1] after the call are the reference's own code.  The budget is checked
+    after each evaluation, a constraint raise inside that evaluation taking precedence -- the
+    max_nfev rule of fw_sim_config."""
+    from scipy.integrate import RK45
+
+    class BudgetRK45(RK45):
+        def __init__(self, fun, t0, y0, t_bound, **kw):
+            self._spent = 0
+
+            def counted(t, y):
+                out = fun(t, y)
+                self._spent += 1
+                if self._spent >= budget:
+                    raise _Budget()
+                return out
+            try:
+                super().__init__(counted, t0, y0, t_bound, **kw)
+                self._init_failed = False
+            except _Budget:  # f0 or the initial-step probe hit the budget: no step at all
+                self._init_failed = True
+                self.t, self.y, self.t_old, self.status = t0, np.array(y0, float), None, "running"
+                self.h_abs, self.f, self.direction, self.n, self.nfev = 0.0, None, 1.0, len(y0), budget
+                self.njev, self.nlu = 0, 0
+                self.t_bound = t_bound
+
+        def _step_impl(self):
+            if self._init_failed:
+                return False, "budget"
+            try:
+                return super()._step_impl()
+            except _Budget:
+                return False, "budget"
+
+    return BudgetRK45
+
+
+def gen_solver_fail():
+    rows = {k: [] for k in ["y0", "wind", "cmd_in", "budget", "y1", "success", "term", "nfev", "naccept",
+                            "status", "derived1", "der0"]}
+    rng = np.random.RandomState(777)
+    orig = scipy.integrate.solve_ivp
+    budgets = [2, 8, 14, 20, 26, 32, 44]
+    for i in range(112):
+        budget = budgets[i % len(budgets)]
+        sim = pf.PyFly(PYFLY_CFG, PYFLY_PARAM, config_kw={"turbulence": False})
+        for n in ["omega_p", "omega_q", "omega_r"]:
+            sim.state[n].constraint_min, sim.state[n].constraint_max = np.radians(-720.0), np.radians(720.0)
+        sim.seed(4000 + i)
+        st = random_state(rng, omega_deg=120.0)
+        wind = random_wind(rng) if i % 3 else [0.0, 0.0, 0.0]
+        st["wind"] = wind
+        sim.reset(state=st)
+        cnt = _count_rhs(sim)
+        cmd = [rng.uniform(np.radians(-40), np.radians(45)), rng.uniform(np.radians(-40), np.radians(40)),
+               rng.uniform(-0.2, 1.2)]
+        y0, der0, cmd_in = ode_vector(sim), derived(sim), list(cmd)
+        status = {}
+
+        def patched(*a, **k):
+            sol = orig(*a, method=_budget_rk45(budget), **k)
+            status["s"] = sol.status
+            status["na"] = len(sol.t) - 1
+            return sol
+        scipy.integrate.solve_ivp = patched
+        try:
+            ok, info = sim.step(cmd)
+        finally:
+            scipy.integrate.solve_ivp = orig
+        rows["y0"].append(y0)
+        rows["der0"].append(der0)
+        rows["wind"].append(np.array(wind, dtype=np.float64))
+        rows["cmd_in"].append(np.array(cmd_in))
+        rows["budget"].append(budget)
+        rows["y1"].append(ode_vector(sim))
+        rows["success"].append(ok)
+        rows["term"].append(info.get("termination", ""))
+        rows["nfev"].append(cnt["n"])
+        rows["naccept"].append(status.get("na", -1))
+        rows["status"].append(status.get("s", 99))
+        rows["derived1"].append(derived(sim))
+    out = {k: np.array(v) for k, v in rows.items()}
+    np.savez_compressed(os.path.join(OUT, "pyfly_solver_fail.npz"), **out)
+    print("solver failure: %d cases, %d failed integrations (status -1), %d constraint terminations" % (
+        len(out["y0"]), int((out["status"] == -1).sum()), int((~out["success"]).sum())))
+
+
+# ---------------------------------------------------------------------------
+# J. energy states (EnergyVariable, pyfly.py:430-450; updated after successful steps :1408-1411)
+# ---------------------------------------------------------------------------
+
+ENERGY_NAMES = ["energy_total", "energy_potential", "energy_kinetic_rotational", "energy_kinetic_translational"]
+
+
+def gen_energy():
+    out = {}
+    for name, seed, olim, n_steps in [("pid", 0, None, 300), ("rand_fail", 3, 45.0, 1000)]:
+        rng = np.random.RandomState(seed)
+        sim = pf.PyFly(PYFLY_CFG, PYFLY_PARAM, config_kw={"turbulence": False})
+        if olim is not None:
+            for n in ["omega_p", "omega_q", "omega_r"]:
+                sim.state[n].constraint_min, sim.state[n].constraint_max = np.radians(-olim), np.radians(olim)
+        sim.seed(seed)
+        st = random_state(rng, omega_deg=60.0 if olim is None else 0.5 * olim, dots=False)
+        st["wind"] = random_wind(rng)
+        sim.reset(state=st)
+        pid = {"dt": sim.dt, "va": 22.0, "phi": 0.2, "theta": 0.0, "iv": 0.0, "ir": 0.0, "ip": 0.0}
+        y, der, en, cmds, succ = [ode_vector(sim)], [derived(sim)], [[sim.state[e].value for e in ENERGY_NAMES]], [], []
+        for s in range(n_steps):
+            if name == "pid":
+                cmd = pid_action(pid, sim)
+            else:
+                cmd = [rng.uniform(np.radians(-30), np.radians(35)), rng.uniform(np.radians(-32.5), np.radians(32.5)),
+                       rng.uniform(0, 1)]
+            cmds.append(list(cmd))
+            ok, info = sim.step(cmd)
+            succ.append(ok)
+            y.append(ode_vector(sim))
+            der.append(derived(sim))
+            en.append([sim.state[e].value for e in ENERGY_NAMES])
+            if not ok:
+                break
+        for k, v in dict(y=np.array(y), derived=np.array(der), energy=np.array(en), cmd=np.array(cmds),
+                         success=np.array(succ), wind=np.array(st["wind"]), omega_lim_deg=np.array(olim or 180.0)).items():
+            out[name + "__" + k] = v
+        print("energy %s: %d steps, last success %s" % (name, len(succ), succ[-1]))
+    out["names"] = np.array(ENERGY_NAMES)
+    np.savez_compressed(os.path.join(OUT, "pyfly_energy.npz"), **out)
+
+
+# ---------------------------------------------------------------------------
+# K. curriculum levels (FixedWingAircraft.set_curriculum_level, fixed_wing.py:334-412)
+# ---------------------------------------------------------------------------
+
+
+def gen_curriculum():
+    out = {}
+    levels = [0.0, 0.25, 0.5, 0.75, 1.0]
+    props = ["init_min", "init_max", "value_min", "value_max", "constraint_min", "constraint_max"]
+    env = make_env(False)
+    names = [s_["name"] for s_ in env.cfg["simulator"]["states"]]
+    out["state_names"] = np.array(names)
+    for li, lvl in enumerate(levels):
+        env.set_curriculum_level(lvl)
+        tab = np.array([[np.nan if getattr(env.simulator.state[n], p, None) is None else
+                         float(getattr(env.simulator.state[n], p)) for p in props] for n in names])
+        out["L%d__states" % li] = tab
+        tp = env._target_props_init["states"]
+        out["L%d__targets" % li] = np.array([[np.nan if tp[t].get(k) is None else float(tp[t][k])
+                                             for k in ("low", "high", "delta", "bound")]
+                                            for t in ("roll", "pitch", "Va")])
+        out["L%d__target_rad" % li] = np.array([bool(tp[t].get("convert_to_radians", False))
+                                               for t in ("roll", "pitch", "Va")])
+        # sampled episodes: initial state and first target of reset() (gym np_random; distribution only)
+        env.seed(100 + li)
+        init, tgt = [], []
+        for _ in range(300):
+            env.reset()
+            init.append([env.simulator.state[n].value for n in ("roll", "pitch", "Va", "velocity_u")])
+            tgt.append([env.target["roll"], env.target["pitch"], env.target["Va"]])
+        out["L%d__init" % li] = np.array(init)
+        out["L%d__target" % li] = np.array(tgt)
+    out["levels"] = np.array(levels)
+    out["props"] = np.array(props)
+    np.savez_compressed(os.path.join(OUT, "env_curriculum.npz"), **out)
+    print("curriculum: %d levels, %d simulator states" % (len(levels), len(names)))
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["single", "traj", "envelope", "dryden", "env", "pidset", "metrics", "obshist"]
+    which = sys.argv[1:] or ["single", "traj", "envelope", "dryden", "env", "pidset", "metrics", "obshist",
+                             "solverfail", "energy", "curriculum"]
     if "envelope" in which and "traj" not in which:
         gen_envelope()
     if "obshist" in which:
@@ -736,3 +922,9 @@ if __name__ == "__main__":
         gen_pid_set()
     if "metrics" in which:
         gen_metrics()
+    if "solverfail" in which:
+        gen_solver_fail()
+    if "energy" in which:
+        gen_energy()
+    if "curriculum" in which:
+        gen_curriculum()

@@ -106,3 +106,38 @@ def test_shard_range_partitions():
             parts = [shard_range(total, r, w) for r in range(w)]
             assert sum(c for _, c in parts) == total
             assert all(parts[i][0] + parts[i][1] == parts[i + 1][0] for i in range(w - 1))
+
+
+def _uneven_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _, cnt = shard_range(5, rank, world)  # odd env count: 3 + 2
+        buf = RolloutBuffer(T, Box(-np.inf, np.inf, (D,)), Box(-1, 1, (A,)), device="cpu", n_envs=cnt)
+        try:
+            buf.all_gather()
+            q.put((rank, "no error"))
+        except ValueError as e:
+            q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_uneven_shards_raise_on_gather():
+    """An odd env count splits 3 + 2: stepping works, but the rollout all-gather (equal-size
+    all_gather_into_tensor) must refuse loudly on every rank instead of hanging in RCCL."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_uneven_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, msg in res:
+        assert "uneven env shards [3, 2]" in msg, (rank, msg)

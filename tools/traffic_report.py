@@ -19,14 +19,19 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_launch(d, kernel, counter):
+def per_launch(d, kernel, counter, last=None):
+    """Mean per-dispatch value of ``counter`` for ``kernel``; ``last``: only the last N dispatches (the
+    bench's timed window, in dispatch order)."""
     vals = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
-                vals.append(float(r["Counter_Value"]))
+                vals.append((int(r.get("Dispatch_Id") or len(vals)), float(r["Counter_Value"])))
     if not vals:
         raise SystemExit("no %s samples for %s under %s" % (counter, kernel, d))
+    vals = [v for _, v in sorted(vals)]
+    if last:
+        vals = vals[-last:]
     return sum(vals) / len(vals), len(vals)
 
 
@@ -37,8 +42,14 @@ def main(base):
     cw, _ = per_launch(os.path.join(base, "calib_write"), "k_calib_write", "WRITE_SIZE")
     f_read = calib["read_bytes_k_calib_read"] / (cf * 1024.0)
     f_write = calib["write_bytes_k_calib_write"] / (cw * 1024.0)
-    ef, nf = per_launch(os.path.join(base, "env_fetch"), "k_env_step", "FETCH_SIZE")
-    ew, nw = per_launch(os.path.join(base, "env_write"), "k_env_step", "WRITE_SIZE")
+    last = int(os.environ.get("PMC_LAST", "200"))  # the bench's timed (steady-state) dispatches
+    ef, nf = per_launch(os.path.join(base, "env_fetch"), "k_env_step", "FETCH_SIZE", last)
+    ew, nw = per_launch(os.path.join(base, "env_write"), "k_env_step", "WRITE_SIZE", last)
+    valu = {}
+    if os.path.isdir(os.path.join(base, "env_valu")):
+        for ctr in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY",
+                    "SQ_ACTIVE_INST_VALU"):
+            valu[ctr] = per_launch(os.path.join(base, "env_valu"), "k_env_step", ctr, last)[0]
     read_b = ef * 1024.0 * f_read
     write_b = ew * 1024.0 * f_write
     sys.path.insert(0, ROOT)
@@ -49,6 +60,8 @@ def main(base):
     out = {
         "kernel": "k_env_step", "workload": "65536 aircraft fp32, turbulence off, U(-1,1) actions",
         "envs": 65536, "precision": "float32", "turbulence": False, "metrics": bool(spec.metrics_enabled),
+        "regime": "steady", "dispatches": "last %d k_env_step dispatches of the bench (its timed window)" % last,
+        "valu_insts_per_launch": valu.get("SQ_INSTS_VALU"), "sq_counters_per_launch": valu or None,
         "fetch_size_kib_per_launch": ef, "write_size_kib_per_launch": ew, "launches": [nf, nw],
         "calibration": {"fetch_kib_k_calib_read": cf, "write_kib_k_calib_write": cw, "factor_read": f_read,
                         "factor_write": f_write, "pattern": "4 B/lane SoA rows, coalesced"},

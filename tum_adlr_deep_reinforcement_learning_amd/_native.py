@@ -4,7 +4,9 @@ The library is built in-tree (``tum_adlr_deep_reinforcement_learning_amd/lib/lib
 with hipcc for ``--offload-arch=gfx950``.  There is no CPU fallback: if the
 library is missing the product path raises.
 """
+import contextlib
 import ctypes
+import fcntl
 import os
 import subprocess
 
@@ -41,19 +43,38 @@ def needs_build():
 EXTRA_FLAGS = ["-fno-slp-vectorize"]  # packed-f32 pairing costs register moves here
 
 
-def build(force=False, verbose=False, out=None, extra=None):
-    """Compile csrc/*.hip into lib/libfwsim.so (seconds; cross-compiles without a GPU)."""
-    out = out or LIB_PATH
-    if out == LIB_PATH and not force and not needs_build():
-        return LIB_PATH
+@contextlib.contextmanager
+def _build_lock(out):
+    """Exclusive lock next to the library: concurrent ranks (torchrun) build once, the others wait."""
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    tmp = out + ".tmp"
-    flags = EXTRA_FLAGS if extra is None else extra
-    cmd = [_hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared"] + flags + ["-o", tmp] + UNITS
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.check_call(cmd)
-    os.replace(tmp, out)
+    with open(out + ".lock", "w") as f:
+        fcntl.flock(f, fcntl.LOCK_EX)
+        try:
+            yield
+        finally:
+            fcntl.flock(f, fcntl.LOCK_UN)
+
+
+def build(force=False, verbose=False, out=None, extra=None):
+    """Compile csrc/*.hip into lib/libfwsim.so (seconds; cross-compiles without a GPU).
+
+    Holds a file lock around the staleness check and the compile, and writes through a
+    per-process temporary file, so parallel callers never see a partial library."""
+    out = out or LIB_PATH
+    with _build_lock(out):
+        if out == LIB_PATH and not force and not needs_build():
+            return LIB_PATH
+        tmp = "%s.%d.tmp" % (out, os.getpid())
+        flags = EXTRA_FLAGS if extra is None else extra
+        cmd = [_hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared"] + flags + ["-o", tmp] + UNITS
+        if verbose:
+            print(" ".join(cmd))
+        try:
+            subprocess.check_call(cmd)
+            os.replace(tmp, out)
+        finally:
+            if os.path.exists(tmp):
+                os.remove(tmp)
     return out
 
 

@@ -103,7 +103,7 @@ class FwSimConfig(ctypes.Structure):
                 ("lim", FwLimits * FW_NVAR),
                 ("act", FwActuator * 3),
                 ("elevon", ctypes.c_int32), ("disabled_inputs", ctypes.c_int32),
-                ("wind_random", ctypes.c_int32), ("pad0_", ctypes.c_int32),
+                ("wind_random", ctypes.c_int32), ("max_nfev", ctypes.c_int32),
                 ("wind_mag_min", ctypes.c_double), ("wind_mag_max", ctypes.c_double),
                 ("wind_init_min", ctypes.c_double * 3), ("wind_init_max", ctypes.c_double * 3),
                 ("turbulence", ctypes.c_int32), ("turb_len", ctypes.c_int32),
@@ -342,6 +342,9 @@ class SimSpec:
     def __init__(self, cfg, params):
         self.cfg = cfg
         self.params = params
+        # RHS-evaluation budget of one RK45 step (fw_sim_config.max_nfev; 0 = the library default 6000).
+        # scipy has none; exhausting it is handled like solve_ivp's TOO_SMALL_STEP failure.
+        self.max_nfev = 0
         self.vars = {}
         for v in cfg["variables"]:
             self.vars[v["name"]] = VarSpec(**v)
@@ -384,6 +387,7 @@ class SimSpec:
         cfg = self.cfg
         c.dt, c.rho, c.g = float(cfg["dt"]), float(cfg["rho"]), float(cfg["g"])
         c.rtol, c.atol = 1e-3, 1e-6
+        c.max_nfev = int(self.max_nfev)
         for i, n in enumerate(PARAM_NAMES):
             c.param[i] = float(self.params[n])
         slot = {}

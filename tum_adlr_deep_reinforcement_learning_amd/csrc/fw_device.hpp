@@ -36,7 +36,8 @@ int set_error(int code, const std::string& msg);
 
 constexpr int NY = FW_NY;
 constexpr double PI_D = 3.141592653589793;
-constexpr int MAX_NFEV = 6000;
+constexpr int MAX_NFEV = 6000;  // default RHS-evaluation budget per step (fw_sim_config.max_nfev)
+constexpr uint32_t DM_SOLVER_FAIL = 1u << 31;  // sim_step_masked dmask bit: RK45 failed, last accepted sub-step kept
 #ifndef FW_Y_PREFETCH
 #define FW_Y_PREFETCH 0
 #endif
@@ -81,6 +82,7 @@ struct DevCfg {
   uint32_t cmask, clipmask, wrapmask;  // per fw_var: has constraint / has clip / wraps
   uint32_t dotmask;                    // per actuator: dot_max finite
   int elevon, disabled_inputs, turbulence, turb_len, wind_random;
+  int max_nfev;                        // RHS-evaluation budget of one step
   int trig_alpha, trig_beta;           // alpha/beta limited -> use trig of the clipped angle
   int euler_exact;                     // roll/pitch/yaw limited -> Euler-angle rotation post step
   T wind_mag_min, wind_mag_max, wind_init_min[3], wind_init_max[3];
@@ -615,10 +617,10 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
           result = term;
           active = false;
         }
-        // hard bound on work per step so that no input can keep a wave spinning:
-        // scipy's own TOO_SMALL_STEP exit needs < 2100 evaluations from any h <= dt
-        if (nfev >= MAX_NFEV) {
-          result = -1;
+        // hard bound on work per step so that no input can keep a wave spinning (scipy has
+        // none; ends the step like its TOO_SMALL_STEP failure, reported in the stats)
+        else if (nfev >= c.max_nfev) {
+          result = -2;
           active = false;
         }
       }
@@ -831,7 +833,10 @@ FW_HD void dryden(const DevCfg<T>& c, int k, const T* un1, const T* u0, T* tl, T
 //   cmd[3]    raw commands in, constrained out
 //   dmask     bit r set <=> der[r] was (re)computed.  On failure the stored state
 //             holds the committed part of the save (history[-1] semantics); the
-//             caller keeps its previous der[r] for the clear bits.
+//             caller keeps its previous der[r] for the clear bits.  Bit 31
+//             (DM_SOLVER_FAIL): the integration failed (TOO_SMALL_STEP, NaN step
+//             or the max_nfev budget) and, like solve_ivp's sol.y[:, -1], the last
+//             accepted sub-step went through the normal save (pyfly.py:1393-1396).
 // Returns termination code (0 = success).
 // ---------------------------------------------------------------------------
 struct KeepY {  // default: y stays live in registers across the integration
@@ -864,7 +869,10 @@ FW_HD int sim_step_masked(const C& c, T* y, T* der, T* cmd, const T* wind, const
   for (int i = 0; i < NY; i++) y1[i] = y[i];
   term = rk45(c, X, y1, sy, sf, stride, nfev, nacc, FW_ER_LDS ? sf + NP * stride : nullptr);
   reload(y);
-  if (term < 0) return 0;  // solver failure: reference keeps sol.y[:, -1]; never observed
+  if (term < 0) {  // solver failure: y1 = the last accepted sub-step (rk45 wrote Y back), saved as usual
+    dmask = DM_SOLVER_FAIL;
+    term = 0;
+  }
   if (term) return term;
 
   // ---- _set_states_from_ode_solution(save=True) (pyfly.py:1852-1881) ----

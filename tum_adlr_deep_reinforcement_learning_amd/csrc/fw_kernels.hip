@@ -765,7 +765,7 @@ __global__ __launch_bounds__(BLOCK) void k_sim_step(const DevCfg<T>* __restrict_
     for (int a = 0; a < 3; a++) cmd_out[i * 3 + a] = cmd[a];
   if (success) success[i] = term == 0;
   if (term_out) term_out[i] = term;
-  if (stats) stats[i] = nfev | (nacc << 16);
+  if (stats) stats[i] = (int32_t)((uint32_t)nfev | ((uint32_t)nacc << 16) | (dmask & DM_SOLVER_FAIL));
 }
 
 template <typename T, typename C>
@@ -931,7 +931,7 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
   rew_out[i] = reward;
   done_out[i] = done ? 1 : 0;
   if (term_out) term_out[i] = term;
-  if (stats) stats[i] = nfev | (nacc << 16);
+  if (stats) stats[i] = (int32_t)((uint32_t)nfev | ((uint32_t)nacc << 16) | (dmask & DM_SOLVER_FAIL));
 
   // Monitor episode record + the episode's final target (info["target"] of the done step)
   if (done && episode_out) {
@@ -1115,6 +1115,7 @@ void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
   d.turbulence = s.turbulence;
   d.turb_len = s.turb_len > 0 ? s.turb_len : 1;
   d.wind_random = s.wind_random;
+  d.max_nfev = s.max_nfev > 0 ? s.max_nfev : MAX_NFEV;
   d.wind_mag_min = (T)s.wind_mag_min;
   d.wind_mag_max = (T)s.wind_mag_max;
   for (int k = 0; k < 3; k++) {

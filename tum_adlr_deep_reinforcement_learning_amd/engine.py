@@ -175,6 +175,11 @@ class Engine:
         s = self.get_block(C.FW_BLK_STEPS)[0]
         return s & 0xFFFF, (s >> 16) & 0xFFFF
 
+    @staticmethod
+    def decode_stats(stats):
+        """fw_sim_step / fw_env_step stats -> (nfev, n_accepted, solver_failed) tensors."""
+        return stats & 0xFFFF, (stats >> 16) & 0x7FFF, (stats < 0)
+
 
 class StepGraph:
     """``K`` consecutive ``Engine.env_step`` launches captured into one HIP graph.

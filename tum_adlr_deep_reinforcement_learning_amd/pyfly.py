@@ -20,6 +20,26 @@ _ODE_ROWS = {"omega_p": 4, "omega_q": 5, "omega_r": 6, "position_n": 7, "positio
 _DER_ROWS = {"roll": 0, "pitch": 1, "yaw": 2, "Va": 3, "alpha": 4, "beta": 5, "elevator": 6, "aileron": 7}
 
 
+def energy_value(name, y, der, params, g):
+    """EnergyVariable.calculate_value (pyfly.py:430-450) from a stored state: ODE state ``y`` [19],
+    derived states ``der`` [8] (der[3] = Va), aircraft ``params`` (x8_param.mat names), gravity ``g``.
+
+    The reference refreshes the energies only after a successful step (pyfly.py:1408-1411) and at
+    reset.  Reading them from the device's stored state gives the same values after a failed step
+    too: a failure leaves omega, position and Va at their pre-step values (stage conditioning fails
+    before the save; at the save only the Euler-angle conditions can still fail, and they come
+    before those variables are committed -- fw_device.hpp sim_step_masked)."""
+    m, val = params["mass"], 0.0
+    if name in ("energy_potential", "energy_total"):
+        val += m * g * (-y[9])
+    if name in ("energy_kinetic_rotational", "energy_kinetic", "energy_total"):
+        for J, w in zip(("Jx", "Jy", "Jz"), y[4:7]):
+            val += 0.5 * params[J] * w ** 2
+    if name in ("energy_kinetic_translational", "energy_kinetic", "energy_total"):
+        val += 0.5 * m * der[3] ** 2
+    return val
+
+
 class _VarView:
     """Read-only stand-in for pyfly's ``Variable`` (``.value``, ``.name``)."""
 
@@ -74,17 +94,7 @@ class SimulatorView:
         raise KeyError(name)
 
     def _energy(self, name):
-        """EnergyVariable.calculate_value (pyfly.py:430-450), host-side from the device state."""
-        y, d = self._block(C.FW_BLK_ODE), self._block(C.FW_BLK_DERIVED)
-        m, val = self._p["mass"], 0.0
-        if name in ("energy_potential", "energy_total"):
-            val += m * self._g * (-y[9])
-        if name in ("energy_kinetic_rotational", "energy_kinetic", "energy_total"):
-            for J, w in zip(("Jx", "Jy", "Jz"), y[4:7]):
-                val += 0.5 * self._p[J] * w ** 2
-        if name in ("energy_kinetic_translational", "energy_kinetic", "energy_total"):
-            val += 0.5 * m * d[3] ** 2
-        return val
+        return energy_value(name, self._block(C.FW_BLK_ODE), self._block(C.FW_BLK_DERIVED), self._p, self._g)
 
     def get_states_vector(self, states, attribute="value"):
         return [self.state[s].value for s in states]

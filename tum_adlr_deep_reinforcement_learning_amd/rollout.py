@@ -110,16 +110,24 @@ class RolloutBuffer:
             self.full = True
 
     def compute_returns_and_advantage(self, last_values, dones):
-        """buffers.py:304-333 on the device (fw_gae)."""
+        """buffers.py:304-333 on the device (fw_gae) over the rows stored so far (``size()``): the
+        bootstrap value enters at the last stored row, as the reference's loop over buffer_size does
+        when the buffer is full."""
         lv = torch.as_tensor(last_values).to(self.device).reshape(-1)
         ld = torch.as_tensor(np.asarray(dones) if not isinstance(dones, torch.Tensor) else dones).to(self.device)
-        gae(self.rewards, self.values.contiguous() if not self.values.is_contiguous() else self.values, self.dones,
-            lv, ld, self.gamma, self.gae_lambda, self.advantages, self.returns)
+        n = self.size() or self.buffer_size
+        gae(self.rewards[:n], self.values[:n], self.dones[:n], lv, ld, self.gamma, self.gae_lambda,
+            self.advantages[:n], self.returns[:n])
 
     # ------------------------------------------------------------- sharding
     def all_gather(self, group=None):
         """Gather every rank's slab (one all_gather_into_tensor) -> GatheredRollout over W*N envs.
-        Env g = rank * N + e, i.e. the global env order of the sharded VecEnv."""
+        Env g = rank * N + e, i.e. the global env order of the sharded VecEnv.  Every rank must hold
+        the same number of envs (all_gather_into_tensor needs equal slabs): an uneven split raises."""
+        counts = all_gather_flat(torch.tensor([self.n_envs], dtype=torch.int64, device=self.device), group)
+        if counts.numel() > 1 and bool((counts != self.n_envs).any()):
+            raise ValueError("RolloutBuffer.all_gather: uneven env shards %s; split the envs evenly over the ranks"
+                             % counts.flatten().tolist())
         return GatheredRollout(list(all_gather_flat(self.slab, group)), self)
 
     def get(self, batch_size=None, generator=None):

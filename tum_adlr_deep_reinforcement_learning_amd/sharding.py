@@ -23,7 +23,10 @@ def world():
 
 
 def shard_range(n_total, rank, world_size):
-    """Contiguous split of ``n_total`` envs: (env_offset, count) of ``rank`` (first ranks get the remainder)."""
+    """Contiguous split of ``n_total`` envs: (env_offset, count) of ``rank`` (first ranks get the remainder).
+
+    An uneven split is fine for stepping; the rollout all-gather needs equal shards and raises on one
+    (RolloutBuffer.all_gather)."""
     base, rem = divmod(int(n_total), int(world_size))
     count = base + (1 if rank < rem else 0)
     offset = rank * base + min(rank, rem)
