@@ -210,7 +210,7 @@ def sac_fill_leg(n, K, dev, rank, world, precision):
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    col.collect(K)
+    col.collect(K, chunk=100)  # warm-up actions do not depend on obs: fused open-loop rollouts
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -330,6 +330,41 @@ def timed_env_steps(n, args, spec, dev, rank, world, env_offset, early=True):
     return float(el[0]), float(el[1]), (float(el[2]) if early else None)
 
 
+def open_loop_leg(n, args, spec, dev, rank, world, env_offset, K=256, launches=4):
+    """The same workload through the open-loop rollout kernel (fw_env_rollout: K steps per launch,
+    actions pre-generated): the rate of a SAC / TD3 warm-up fill or a scripted-command evaluation, where
+    the actions do not depend on the observations.  Steady state as above (prep steps first)."""
+    eng = Engine(spec.sim, spec, n, device=dev, precision=args.precision)
+    eng.seed(1234, env_offset=env_offset)
+    eng.reset()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1 + rank)
+    acts = (torch.rand(K, n, 3, generator=gen, device=dev, dtype=eng.dtype) * 2 - 1).contiguous()
+    for _ in range(max(args.prep // K, 1)):  # steady-state population
+        eng.env_rollout(acts)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(launches):
+        eng.env_rollout(acts)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0, e0.elapsed_time(e1)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    eng.close()
+    steps = K * launches
+    return {"kernel": "k_env_rollout", "steps_per_launch": K, "steps": steps, "envs_per_gpu": n,
+            "global_envs": n * world, "value": n * world * steps / float(el[0]), "unit": "env-steps/s",
+            "ms_per_step": float(el[0]) / steps * 1e3, "kernel_ms_per_step": float(el[1]) / steps}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -346,6 +381,7 @@ def main():
     ap.add_argument("--no-metrics", action="store_true",
                     help="do not track the config's streaming episode metrics (fixed_wing.py:1644-1736)")
     ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling line (65536 aircraft per GPU)")
+    ap.add_argument("--no-open-loop", action="store_true", help="skip the open-loop rollout line (fw_env_rollout)")
     ap.add_argument("--rollout-steps", type=int, default=0,
                     help="also run one PPO collect_rollouts of this horizon (2048 = BASELINE configs[2]/[3])")
     ap.add_argument("--sac-fill-steps", type=int, default=0,
@@ -386,6 +422,8 @@ def main():
         w_el, w_k, _ = timed_env_steps(nw, args, spec, dev, rank, world, rank * nw, early=False)
         weak = {"envs_per_gpu": nw, "global_envs": nw * world, "value": nw * world * args.steps / w_el,
                 "ms_per_step": w_el / args.steps * 1e3, "kernel_ms": w_k}
+
+    open_loop = None if args.no_open_loop else open_loop_leg(n, args, spec, dev, rank, world, rank * n)
 
     esz = 4 if args.precision == "float32" else 8
     rd, wr = algorithmic_bytes_per_env_step(spec, esz)
@@ -440,6 +478,8 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_reference": REFERENCE_CPU,
         }
+        if open_loop is not None:
+            out["open_loop_rollout"] = open_loop
         if weak is not None:
             out["weak_scaling"] = weak
         if rollout is not None:

@@ -288,6 +288,18 @@ int fw_env_step(fw_handle* h, const void* actions_dev, void* obs_dev, void* rewa
                 int32_t* term_dev, void* terminal_obs_dev, void* episode_dev, int32_t* stats_dev,
                 int32_t auto_reset, void* stream);
 
+/* Open-loop rollout: n_steps consecutive fw_env_step calls in ONE launch, for actions known in
+ * advance (SAC / TD3 warm-up with uniform actions, off_policy_algorithm.py:354-472 collect_rollouts
+ * before learning_starts; scripted command sequences).  Same per-step semantics and results as
+ * n_steps fw_env_step launches, bit for bit; each wave advances through the steps on its own instead of
+ * every step waiting for the slowest aircraft of the batch.  actions_dev [K][N][3]; per-step outputs
+ * stacked: obs_dev [K][N][n_obs], reward_dev [K][N], done_dev uint8[K][N], and (each may be NULL)
+ * term_dev int32[K][N], terminal_obs_dev [K][N][n_obs], episode_dev [K][N][5], stats_dev int32[K][N].
+ * The metrics record (fw_set_metrics_output) holds each env's last episode that ended in the launch. */
+int fw_env_rollout(fw_handle* h, int32_t n_steps, const void* actions_dev, void* obs_dev, void* reward_dev,
+                   uint8_t* done_dev, int32_t* term_dev, void* terminal_obs_dev, void* episode_dev, int32_t* stats_dev,
+                   int32_t auto_reset, void* stream);
+
 /* Observation of the current state (FixedWingAircraft.get_observation). */
 int fw_observe(fw_handle* h, void* obs_dev, void* stream);
 

@@ -96,6 +96,7 @@ SIGNATURES = {
     "fw_reset": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "fw_sim_step": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "fw_env_step": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
+    "fw_env_rollout": (_c.c_int, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
     "fw_observe": (_c.c_int, [_vp, _vp, _vp]),
     "fw_get_state": (_c.c_int, [_vp, _i32, _vp, _vp]),
     "fw_set_state": (_c.c_int, [_vp, _i32, _vp, _vp]),

@@ -9,6 +9,7 @@
 // stage vectors staged in LDS, no MFMA -- the work is elementwise ODE
 // integration):
 //   k_env_step   FixedWingAircraft.step + PyFly.step + masked auto-reset (hot path)
+//   k_env_rollout K such steps per launch with actions given in advance (open loop)
 //   k_sim_step   PyFly.step only
 //   k_reset      masked reset (sampled with Philox or injected values)
 //   k_observe    get_observation of the current state
@@ -768,16 +769,15 @@ __global__ __launch_bounds__(BLOCK) void k_sim_step(const DevCfg<T>* __restrict_
   if (stats) stats[i] = (int32_t)((uint32_t)nfev | ((uint32_t)nacc << 16) | (dmask & DM_SOLVER_FAIL));
 }
 
+// FixedWingAircraft.step of aircraft i (the body of k_env_step and of one k_env_rollout step).
+// lds: this block's RK45 slots (lds_slots<T>() * NP * BLOCK pairs).
 template <typename T, typename C>
-__global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
-                                                    const T* __restrict__ actions, T* __restrict__ obs_out,
-                                                    T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
-                                                    int32_t* __restrict__ term_out, T* __restrict__ tobs_out,
-                                                    T* __restrict__ episode_out, int32_t* __restrict__ stats,
-                                                    int auto_reset) {
-  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-  if (i >= s.n) return;
-  const C& c = *reinterpret_cast<const C*>(cfgp);  // structural specialisation view (fw_device.hpp SpecCfg)
+__device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, const int64_t i, V2<T>* lds,
+                                              const T* __restrict__ actions, T* __restrict__ obs_out,
+                                              T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
+                                              int32_t* __restrict__ term_out, T* __restrict__ tobs_out,
+                                              T* __restrict__ episode_out, int32_t* __restrict__ stats,
+                                              int auto_reset) {
   const int64_t ld = s.ld;
   FW_TSTAMP(0);
 
@@ -806,7 +806,6 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
   int nfev = 0, nacc = 0;
   uint32_t dmask = 0;
 #if FW_LDS_STATE
-  __shared__ V2<T> lds[lds_slots<T>() * NP * BLOCK];  // y, f (+ error sum) of the block's aircraft (pairs)
   const int sterm = sim_step_masked(c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
                                     lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i});
 #else
@@ -984,6 +983,44 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
   st_(s.ep_ret, 0, ld, i, ep_ret);
   s.steps[i] = (uint32_t)(steps & 0xFFFF) | ((uint32_t)(steps_tgt & 0xFFFF) << 16);
   FW_TSTAMP(4);
+}
+
+template <typename T, typename C>
+__global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
+                                                    const T* __restrict__ actions, T* __restrict__ obs_out,
+                                                    T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
+                                                    int32_t* __restrict__ term_out, T* __restrict__ tobs_out,
+                                                    T* __restrict__ episode_out, int32_t* __restrict__ stats,
+                                                    int auto_reset) {
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= s.n) return;
+  const C& c = *reinterpret_cast<const C*>(cfgp);  // structural specialisation view (fw_device.hpp SpecCfg)
+  __shared__ V2<T> lds[lds_slots<T>() * NP * BLOCK];  // y, f (+ error sum) of the block's aircraft (pairs)
+  env_step_lane(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out, stats, auto_reset);
+}
+
+// Open-loop rollout: n_steps consecutive FixedWingAircraft.step calls per aircraft in ONE launch, actions
+// given in advance ([K][N][3]; outputs per step [K][N][...]).  Identical per-step code to k_env_step, so
+// the results equal K k_env_step launches bit for bit; what changes is synchronisation: a wave moves on
+// to its next step as soon as its own aircraft are done, instead of every step waiting for the slowest
+// aircraft of the whole batch (the RK45 straggler tail).
+template <typename T, typename C>
+__global__ __launch_bounds__(BLOCK) void k_env_rollout(const DevCfg<T>* __restrict__ cfgp, State<T> s, int n_steps,
+                                                       const T* __restrict__ actions, T* __restrict__ obs_out,
+                                                       T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
+                                                       int32_t* __restrict__ term_out, T* __restrict__ tobs_out,
+                                                       T* __restrict__ episode_out, int32_t* __restrict__ stats,
+                                                       int auto_reset) {
+  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= s.n) return;
+  const C& c = *reinterpret_cast<const C*>(cfgp);
+  __shared__ V2<T> lds[lds_slots<T>() * NP * BLOCK];
+  const int64_t n = s.n, ow = (int64_t)c.n_obs * c.obs_len;
+  for (int k = 0; k < n_steps; k++) {
+    env_step_lane(c, s, i, lds, actions + k * n * 3, obs_out + k * n * ow, rew_out + k * n, done_out + k * n,
+                  term_out ? term_out + k * n : nullptr, tobs_out ? tobs_out + k * n * ow : nullptr,
+                  episode_out ? episode_out + k * n * 5 : nullptr, stats ? stats + k * n : nullptr, auto_reset);
+  }
 }
 
 }  // namespace
@@ -1500,6 +1537,25 @@ int fw_env_step(fw_handle* h, const void* actions_dev, void* obs_dev, void* rewa
     FW_LAUNCH_SPEC(k_env_step, float, h, st, state_of<float>(h), (const float*)actions_dev, (float*)obs_dev,
                    (float*)reward_dev, done_dev, term_dev, (float*)terminal_obs_dev, (float*)episode_dev, stats_dev,
                    auto_reset);
+  return check_launch();
+}
+
+int fw_env_rollout(fw_handle* h, int32_t n_steps, const void* actions_dev, void* obs_dev, void* reward_dev,
+                   uint8_t* done_dev, int32_t* term_dev, void* terminal_obs_dev, void* episode_dev, int32_t* stats_dev,
+                   int32_t auto_reset, void* stream) {
+  if (!h || !actions_dev || !obs_dev || !reward_dev || !done_dev) return set_err(FW_E_INVALID, "NULL argument");
+  if (!h->has_env) return set_err(FW_E_INVALID, "handle has no env config");
+  if (n_steps < 1) return set_err(FW_E_INVALID, "n_steps must be >= 1");
+  FW_HIP(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  if (h->precision == FW_F64)
+    FW_LAUNCH_SPEC(k_env_rollout, double, h, st, state_of<double>(h), n_steps, (const double*)actions_dev,
+                   (double*)obs_dev, (double*)reward_dev, done_dev, term_dev, (double*)terminal_obs_dev,
+                   (double*)episode_dev, stats_dev, auto_reset);
+  else
+    FW_LAUNCH_SPEC(k_env_rollout, float, h, st, state_of<float>(h), n_steps, (const float*)actions_dev,
+                   (float*)obs_dev, (float*)reward_dev, done_dev, term_dev, (float*)terminal_obs_dev,
+                   (float*)episode_dev, stats_dev, auto_reset);
   return check_launch();
 }
 

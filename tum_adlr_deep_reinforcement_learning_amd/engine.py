@@ -149,6 +149,38 @@ class Engine:
         self._stepped = True
         return self.obs, self.reward, self.done, self.term
 
+    def env_rollout(self, actions, auto_reset=True, stats=False, terminal_obs=True, episode=True):
+        """K consecutive ``env_step`` calls in ONE launch (fw_env_rollout) for actions known in advance.
+
+        ``actions``: device tensor [K][n][3].  Returns (obs [K][n][n_obs], reward [K][n], done [K][n],
+        term [K][n]); ``self.rollout_terminal_obs`` [K][n][n_obs], ``self.rollout_episode`` [K][n][5] and
+        ``self.rollout_stats`` [K][n] hold the other per-step outputs.  The buffers are reused by the next
+        call with the same K.  Bitwise the same as K ``env_step`` calls."""
+        if actions.dim() != 3 or actions.shape[1:] != (self.n, 3):
+            raise ValueError("actions must be [K][%d][3]" % self.n)
+        act = actions if (actions.dtype == self.dtype and actions.device == self.device and actions.is_contiguous()) \
+            else actions.to(device=self.device, dtype=self.dtype).contiguous()
+        K = int(act.shape[0])
+        if getattr(self, "_roll_k", None) != K:
+            dev, dt, n = self.device, self.dtype, self.n
+            w = max(self.n_obs, 1)
+            self._roll_k = K
+            self.rollout_obs = torch.zeros(K, n, w, dtype=dt, device=dev)
+            self.rollout_terminal_obs = torch.zeros(K, n, w, dtype=dt, device=dev)
+            self.rollout_reward = torch.zeros(K, n, dtype=dt, device=dev)
+            self.rollout_done = torch.zeros(K, n, dtype=torch.uint8, device=dev)
+            self.rollout_term = torch.zeros(K, n, dtype=torch.int32, device=dev)
+            self.rollout_episode = torch.zeros(K, n, 5, dtype=dt, device=dev)
+            self.rollout_stats = torch.zeros(K, n, dtype=torch.int32, device=dev)
+        _native.check(self.lib.fw_env_rollout(self.h, K, _ptr(act), _ptr(self.rollout_obs), _ptr(self.rollout_reward),
+                                              _ptr(self.rollout_done), _ptr(self.rollout_term),
+                                              _ptr(self.rollout_terminal_obs) if terminal_obs else None,
+                                              _ptr(self.rollout_episode) if episode else None,
+                                              _ptr(self.rollout_stats) if stats else None, int(bool(auto_reset)),
+                                              self.stream()), "fw_env_rollout")
+        self._stepped = True
+        return self.rollout_obs, self.rollout_reward, self.rollout_done, self.rollout_term
+
     def observe(self):
         _native.check(self.lib.fw_observe(self.h, _ptr(self.obs), self.stream()), "fw_observe")
         return self.obs

@@ -138,14 +138,37 @@ class OffPolicyCollector:
     def unscale_action(self, a):
         return self.low + (0.5 * (a + 1.0) * (self.high - self.low))
 
+    def _warmup(self, k):
+        """True if the next ``k`` steps all draw uniform warm-up actions (no policy in the loop)."""
+        return self.actor is None or self.num_timesteps + k * self.env.num_envs <= self.learning_starts
+
     @torch.no_grad()
-    def collect(self, n_steps):
+    def collect(self, n_steps, chunk=0):
+        """``n_steps`` steps of all envs.  ``chunk`` > 1: warm-up steps (uniform actions, which do not depend
+        on the observations) run ``chunk`` at a time through the fused open-loop rollout
+        (FixedWingVecEnv.rollout) -- same actions, transitions and buffer contents as stepping one by one."""
         env, buf = self.env, self.buffer
         n = env.num_envs
         if self.last_obs is None:
             self.last_obs = env.reset().clone()
             self.last_original_obs = (env.get_original_obs() if self._vecnorm else self.last_obs).clone()
-        for _ in range(n_steps):
+        done_steps = 0
+        if chunk > 1 and not self._vecnorm and hasattr(env, "rollout"):
+            while n_steps - done_steps >= chunk and self._warmup(chunk):
+                scaled = []
+                for _ in range(chunk):  # the per-step draws of the loop below, in the same order
+                    u = torch.rand(n, self.low.numel(), device=buf.device, generator=self.gen)
+                    scaled.append(self.scale_action(self.low + u * (self.high - self.low)))
+                scaled = torch.stack(scaled)
+                obs, reward, done, _ = env.rollout(self.unscale_action(scaled))
+                for k in range(chunk):
+                    buf.add(self.last_original_obs, obs[k], scaled[k], reward[k], done[k])
+                    self.last_original_obs = obs[k]
+                self.num_timesteps += n * chunk
+                self.last_obs = obs[chunk - 1].clone()
+                self.last_original_obs = self.last_obs
+                done_steps += chunk
+        for _ in range(n_steps - done_steps):
             if self.num_timesteps < self.learning_starts or self.actor is None:
                 u = torch.rand(n, self.low.numel(), device=buf.device, generator=self.gen)
                 unscaled = self.low + u * (self.high - self.low)

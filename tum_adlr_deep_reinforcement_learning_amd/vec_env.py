@@ -203,6 +203,18 @@ class FixedWingVecEnv(VecEnv):
         infos = self._infos(done_np)
         return self._shaped(obs.cpu().numpy().astype(np.float32)), rew.cpu().numpy().astype(np.float32), done_np, infos
 
+    def rollout(self, actions):
+        """``K`` consecutive ``step`` calls for actions known in advance ([K][N][3] device tensor), in one
+        fused launch (Engine.env_rollout): the SAC / TD3 warm-up with uniform actions, scripted command
+        sequences.  Auto-reset as in ``step``.  Returns device tensors (obs [K, N, *obs_shape], reward
+        [K][N], done [K][N] bool, termination code [K][N]); terminal observations and Monitor records of
+        the done steps are in ``engine.rollout_terminal_obs`` / ``engine.rollout_episode``."""
+        a = torch.as_tensor(actions).to(device=self.device, dtype=self.engine.dtype)
+        obs, rew, done, term = self.engine.env_rollout(a.reshape(a.shape[0], self.num_envs, -1).contiguous())
+        shape = self.observation_space.shape
+        o = obs if len(shape) == 1 else obs.reshape(obs.shape[:2] + tuple(shape))
+        return o, rew, done.bool(), term
+
     def _shaped(self, o):
         """[N][length * n_row] device layout -> [N, *observation_space.shape] ("matrix" observations)."""
         shape = self.observation_space.shape
