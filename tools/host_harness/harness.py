@@ -1,4 +1,14 @@
-"""Build + load the CPU harness of the device physics (TEST ONLY)."""
+"""Host (CPU) build of the device physics, for debugging only -- not a test and not the product.
+
+fw_device.hpp's functions are __host__ __device__; this harness compiles them for the CPU (libm in
+place of the hardware rcp/exp/atan2 approximations) so a single aircraft step can be replayed and
+instrumented in fp32 or fp64 without a GPU.  Used e.g. to show that the fp32 single-step deviations
+of tests/test_gpu_r02.py::test_single_step_fp32_all_components_gate2 come from the fp32 algorithm
+(initial-step probe cancellation), not from the device.  Usage (from the repo root):
+
+    import sys; sys.path.insert(0, "tools/host_harness"); import harness as H
+    H.sim_step(0 /*fp32*/ or 1, cfg, y, der, wind, turb, cmd)
+"""
 import ctypes
 import os
 import subprocess

@@ -349,6 +349,10 @@ FW_HD void airspeed_vec_euler(T phi, T th, T psi, const T* w, const T* tl, const
 // ---------------------------------------------------------------------------
 template <typename T, typename C>
 FW_HD int rhs(const C& c0, const StepCtx<T>& X, bool first, const T* y, T* dy) {
+#ifdef FW_RHS_TRIVIAL  // ISA accounting experiment only (tools/isa_loop.sh -DFW_RHS_TRIVIAL)
+  for (int i = 0; i < NY; i++) dy[i] = y[i] * X.sp[0];
+  return 0;
+#endif
   const C& c = relaunder(c0);
   int term = 0;
   T om[3] = {y[4], y[5], y[6]};

@@ -51,6 +51,9 @@ int set_err(int code, const std::string& msg) { return fw::set_error(code, msg);
 #define FW_BLOCK 64  // threads per block: one wave (measured 1-2% faster than 256, profiles/r01_ab_block.log)
 #endif
 constexpr int BLOCK = FW_BLOCK;
+#ifndef FW_MIN_WAVES
+#define FW_MIN_WAVES 1  // __launch_bounds__ minimum waves per SIMD of the env-step kernels (VGPR budget 512 / this)
+#endif
 #ifndef FW_LDS_STATE
 #define FW_LDS_STATE 1  // 0 = y/f in VGPRs (measured: 512 VGPRs + spills, slower)
 #endif
@@ -986,7 +989,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
 }
 
 template <typename T, typename C>
-__global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
+__global__ __launch_bounds__(BLOCK, FW_MIN_WAVES) void k_env_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
                                                     const T* __restrict__ actions, T* __restrict__ obs_out,
                                                     T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
                                                     int32_t* __restrict__ term_out, T* __restrict__ tobs_out,
@@ -999,13 +1002,32 @@ __global__ __launch_bounds__(BLOCK) void k_env_step(const DevCfg<T>* __restrict_
   env_step_lane(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out, stats, auto_reset);
 }
 
+// One env step of k_env_rollout.  Inlined (default), the step loop's kernel spills ~230 VGPRs
+// (values live across the RK loop into the epilogue); behind a call boundary it does not, but the call
+// costs more than the spills (tools/ab_bench.sh, profiles/r02_ab_rollout.log).
+#ifndef FW_ROLLOUT_CALL
+#define FW_ROLLOUT_CALL 0  // 1: the step behind a call (no spills, but measured 5% slower: profiles/r02_ab_rollout.log)
+#endif
+#if FW_ROLLOUT_CALL
+#define FW_ROLLOUT_INLINE __noinline__
+#else
+#define FW_ROLLOUT_INLINE __forceinline__
+#endif
+template <typename T, typename C>
+__device__ FW_ROLLOUT_INLINE void env_step_call(const C& c, const State<T>& s, const int64_t i, V2<T>* lds,
+                                           const T* actions, T* obs_out, T* rew_out, uint8_t* done_out,
+                                           int32_t* term_out, T* tobs_out, T* episode_out, int32_t* stats,
+                                           int auto_reset) {
+  env_step_lane(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out, stats, auto_reset);
+}
+
 // Open-loop rollout: n_steps consecutive FixedWingAircraft.step calls per aircraft in ONE launch, actions
 // given in advance ([K][N][3]; outputs per step [K][N][...]).  Identical per-step code to k_env_step, so
 // the results equal K k_env_step launches bit for bit; what changes is synchronisation: a wave moves on
 // to its next step as soon as its own aircraft are done, instead of every step waiting for the slowest
 // aircraft of the whole batch (the RK45 straggler tail).
 template <typename T, typename C>
-__global__ __launch_bounds__(BLOCK) void k_env_rollout(const DevCfg<T>* __restrict__ cfgp, State<T> s, int n_steps,
+__global__ __launch_bounds__(BLOCK, FW_MIN_WAVES) void k_env_rollout(const DevCfg<T>* __restrict__ cfgp, State<T> s, int n_steps,
                                                        const T* __restrict__ actions, T* __restrict__ obs_out,
                                                        T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
                                                        int32_t* __restrict__ term_out, T* __restrict__ tobs_out,
@@ -1013,11 +1035,11 @@ __global__ __launch_bounds__(BLOCK) void k_env_rollout(const DevCfg<T>* __restri
                                                        int auto_reset) {
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (i >= s.n) return;
-  const C& c = *reinterpret_cast<const C*>(cfgp);
   __shared__ V2<T> lds[lds_slots<T>() * NP * BLOCK];
-  const int64_t n = s.n, ow = (int64_t)c.n_obs * c.obs_len;
+  const int64_t n = s.n, ow = (int64_t)cfgp->n_obs * cfgp->obs_len;
   for (int k = 0; k < n_steps; k++) {
-    env_step_lane(c, s, i, lds, actions + k * n * 3, obs_out + k * n * ow, rew_out + k * n, done_out + k * n,
+    const C& c = *reinterpret_cast<const C*>(cfgp);
+    env_step_call(c, s, i, lds, actions + k * n * 3, obs_out + k * n * ow, rew_out + k * n, done_out + k * n,
                   term_out ? term_out + k * n : nullptr, tobs_out ? tobs_out + k * n * ow : nullptr,
                   episode_out ? episode_out + k * n * 5 : nullptr, stats ? stats + k * n : nullptr, auto_reset);
   }
