@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FWSIM_ABI_VERSION 3
+#define FWSIM_ABI_VERSION 4
 
 /* ---- error codes ---------------------------------------------------------- */
 #define FW_OK 0
@@ -169,6 +169,20 @@ typedef struct fw_rew_factor {
 #define FW_TGT_CONSTANT 0
 #define FW_TGT_COMPENSATE 1
 
+/* simulator parameter randomisation (FixedWingAircraft.sample_simulator_parameters,
+ * fixed_wing.py:748-813: the env config's "simulator": {"model": {...}} block), one entry per
+ * randomised parameter, redrawn for an aircraft at each of its resets.                        */
+#define FW_DIST_GAUSSIAN 0
+#define FW_DIST_UNIFORM 1
+typedef struct fw_rand_param {
+  int32_t param;    /* fw_param index */
+  int32_t dist;     /* FW_DIST_GAUSSIAN: N(original, var), then clipped to original -+ clip;
+                       FW_DIST_UNIFORM: U(original - var, original + var)                 */
+  double original;  /* the parameter's value before sampling ("original", else the config value) */
+  double var;       /* absolute (a "relative" var_type is multiplied by |original| by the host) */
+  double clip;      /* absolute, may be negative (relative clip * original, as the reference); NaN = none */
+} fw_rand_param;
+
 typedef struct fw_env_config {
   int32_t steps_max;
   int32_t n_obs;
@@ -208,6 +222,12 @@ typedef struct fw_env_config {
   int32_t obs_noise;                  /* 1: add observation noise */
   int32_t pad3_;
   double obs_noise_mean, obs_noise_std;
+  /* simulator parameter randomisation: n_rand entries of rand[] (0 = every aircraft flies the sim
+   * config's parameters).  Only parameters _forces reads at run time change the dynamics; the
+   * inertia gammas, I and the aspect ratio stay the sim config's (computed once by the reference). */
+  int32_t n_rand;
+  int32_t pad4_;
+  fw_rand_param rand[FW_NPARAM];
 } fw_env_config;
 
 /* Episode-metric record written for every done env (SoA [FW_NMETRIC][N] so the stores
@@ -241,7 +261,8 @@ enum fw_init_field {
 #define FW_BLK_WIND 3       /* 3 rows, T: steady wind n e d */
 #define FW_BLK_STEPS 4      /* 1 row, uint32: steps_count | steps_for_current_target << 16 */
 #define FW_BLK_COMMAND 5    /* 3 rows, T: last constrained commands (input order) */
-#define FW_NBLK 6
+#define FW_BLK_PARAMS 6     /* FW_NPARAM rows, T: per-aircraft parameters (only with env->n_rand > 0) */
+#define FW_NBLK 7
 
 typedef struct fw_handle fw_handle;
 

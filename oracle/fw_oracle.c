@@ -57,9 +57,9 @@ static double clipd(double x, double lo, double hi) {
 static double sgn(double x) { return (double)((x > 0) - (x < 0)); }
 
 /* gammas  pyfly.py:1086-1116 */
-static void gammas(const fw_sim_config* c, double G[9]) {
-  double Jx = c->param[FW_P_JX], Jy = c->param[FW_P_JY], Jz = c->param[FW_P_JZ];
-  double I02 = -c->param[FW_P_JXZ];
+static void gammas(const double* P0, double G[9]) {
+  double Jx = P0[FW_P_JX], Jy = P0[FW_P_JY], Jz = P0[FW_P_JZ];
+  double I02 = -P0[FW_P_JXZ];
   G[0] = Jx * Jz - I02 * I02;
   G[1] = (fabs(I02) * (Jx - Jy + Jz)) / G[0];
   G[2] = (Jz * (Jz - Jy) + I02 * I02) / G[0];
@@ -124,6 +124,10 @@ typedef struct ctx {
   double turb[6];    /* vel_lin (3), vel_ang (3) at cur_sim_step (held over the step) */
   double act_elev0, act_ail0; /* stored elevator/aileron values (t == 0 evaluation) */
   int nfev;
+  /* parameters PyFly.__init__ froze (inertia I / gammas pyfly.py:1086-1116, aspect ratio ar :1119):
+   * with simulator parameter randomisation (fixed_wing.py:748-813) c->param holds the aircraft's
+   * sampled values, which _forces reads at every call, while these stay the initial ones */
+  const double* P0;
 } ctx;
 
 /* PyFly._dynamics  pyfly.py:1450-1482 (with _set_states_from_ode_solution(save=False)
@@ -187,7 +191,7 @@ static int rhs(ctx* X, int first, const double* y, double* dy) {
   double fg[3] = {mg * (2 * (e1 * e3 - e2 * e0)), mg * (2 * (e2 * e3 + e1 * e0)),
                   mg * (e3 * e3 + e0 * e0 - e1 * e1 - e2 * e2)};
   double M = P[FW_P_M], a0 = P[FW_P_A0];
-  double ar = b * b / S;
+  double ar = X->P0[FW_P_B] * X->P0[FW_P_B] / X->P0[FW_P_S_WING]; /* frozen at __init__ (pyfly.py:1119) */
   double ex1 = exp(-M * (alpha - a0)), ex2 = exp(M * (alpha + a0));
   double sigma = (1 + ex1 + ex2) / ((1 + ex1) * (1 + ex2));
   double sa = sin(alpha), ca = cos(alpha);
@@ -228,7 +232,7 @@ static int rhs(ctx* X, int first, const double* y, double* dy) {
   /* _f_omega_dot pyfly.py:1659-1683 */
   const double* G = X->G;
   dy[4] = G[1] * P0 * Q0 - G[2] * Q0 * R0 + G[3] * tau[0] + G[4] * tau[2];
-  dy[5] = G[5] * P0 * R0 - G[6] * (P0 * P0 - R0 * R0) + tau[1] / P[FW_P_JY];
+  dy[5] = G[5] * P0 * R0 - G[6] * (P0 * P0 - R0 * R0) + tau[1] / X->P0[FW_P_JY]; /* I[1, 1] */
   dy[6] = G[7] * P0 * Q0 - G[1] * Q0 * R0 + G[4] * tau[0] + G[8] * tau[2];
   /* _f_p_dot pyfly.py:1706-1737 */
   double T00 = e1 * e1 + e0 * e0 - e2 * e2 - e3 * e3, T01 = 2 * (e1 * e2 - e3 * e0), T02 = 2 * (e1 * e3 + e2 * e0);
@@ -443,12 +447,13 @@ void orc_turbulence(const fw_sim_config* c, const double* noise, int64_t len, in
 /*   hist[9]: history[-1] of (roll pitch yaw Va alpha beta p q r) out         */
 /* Returns termination code (0 success).                                     */
 /* ------------------------------------------------------------------------- */
-int orc_sim_step(const fw_sim_config* c, double* y, double* der, double* hist, const double* wind,
-                 const double* turb, double* cmd, int* nfev, int* naccept) {
+int orc_sim_step_p(const fw_sim_config* c, const double* P0, double* y, double* der, double* hist,
+                   const double* wind, const double* turb, double* cmd, int* nfev, int* naccept) {
   ctx X;
   memset(&X, 0, sizeof(X));
   X.c = c;
-  gammas(c, X.G);
+  X.P0 = P0 ? P0 : c->param;
+  gammas(X.P0, X.G);
   for (int i = 0; i < 3; i++) X.wind[i] = wind[i];
   for (int i = 0; i < 6; i++) X.turb[i] = turb[i];
   X.act_elev0 = der[6];
@@ -533,6 +538,11 @@ int orc_sim_step(const fw_sim_config* c, double* y, double* der, double* hist, c
 #undef COMMIT_FAIL
 }
 
+int orc_sim_step(const fw_sim_config* c, double* y, double* der, double* hist, const double* wind,
+                 const double* turb, double* cmd, int* nfev, int* naccept) {
+  return orc_sim_step_p(c, NULL, y, der, hist, wind, turb, cmd, nfev, naccept);
+}
+
 /* Batched convenience wrapper: arrays are [n][19], [n][8], [n][9], [n][3], [n][6], [n][3]. */
 void orc_sim_step_batch(const fw_sim_config* c, int64_t n, double* y, double* der, double* hist,
                         const double* wind, const double* turb, double* cmd, int32_t* term, int32_t* nfev,
@@ -601,6 +611,11 @@ typedef struct orc_env {
   int32_t n_goal;
   int32_t goal_achieved;
   double ep_ret;
+  /* simulator parameter randomisation: the aircraft's sampled parameters (runtime) and the config's
+   * (what PyFly.__init__ froze into I / gammas / ar); has_params = 0: the sim config's for both */
+  int32_t has_params;
+  double params[FW_NPARAM];
+  double params0[FW_NPARAM];
 } orc_env;
 
 static void push_hist(double h[FW_MAX_WINDOW][3], int32_t* n, const double* v) {
@@ -852,7 +867,14 @@ int orc_env_step(const fw_sim_config* c, const fw_env_config* e, orc_env* s, con
   double turb[6];
   orc_turbulence(c, noise, noise_len, s->steps, turb);
   int nf = 0, na = 0;
-  int t = orc_sim_step(c, s->y, s->der, s->hist, s->wind, turb, cmd, &nf, &na);
+  int t;
+  if (s->has_params) {
+    fw_sim_config cp = *c;
+    memcpy(cp.param, s->params, sizeof(cp.param));
+    t = orc_sim_step_p(&cp, s->params0, s->y, s->der, s->hist, s->wind, turb, cmd, &nf, &na);
+  } else {
+    t = orc_sim_step(c, s->y, s->der, s->hist, s->wind, turb, cmd, &nf, &na);
+  }
   if (nfev_out) *nfev_out = nf;
   push_hist(s->cmd_hist, &s->n_cmd, cmd);
   s->steps += 1;
@@ -898,5 +920,13 @@ int orc_env_step(const fw_sim_config* c, const fw_env_config* e, orc_env* s, con
 }
 
 int orc_env_state_size(void) { return (int)sizeof(orc_env); }
+
+/* Give the env's aircraft its own parameter values (after orc_env_reset, which clears them). */
+void orc_env_set_params(void* state, const fw_sim_config* c, const double* params) {
+  orc_env* s = (orc_env*)state;
+  s->has_params = 1;
+  memcpy(s->params, params, sizeof(s->params));
+  memcpy(s->params0, c->param, sizeof(s->params0));
+}
 int orc_sizeof_sim_config(void) { return (int)sizeof(fw_sim_config); }
 int orc_sizeof_env_config(void) { return (int)sizeof(fw_env_config); }

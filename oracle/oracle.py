@@ -35,6 +35,10 @@ def lib():
         L = ctypes.CDLL(LIB)
         L.orc_sim_step.restype = ctypes.c_int
         L.orc_sim_step.argtypes = [ctypes.c_void_p, _d, _d, _d, _d, _d, _d, _i32, _i32]
+        L.orc_sim_step_p.restype = ctypes.c_int
+        L.orc_sim_step_p.argtypes = [ctypes.c_void_p, _d, _d, _d, _d, _d, _d, _d, _i32, _i32]
+        L.orc_env_set_params.restype = None
+        L.orc_env_set_params.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _d]
         L.orc_sim_step_batch.restype = None
         L.orc_sim_step_batch.argtypes = [ctypes.c_void_p, ctypes.c_int64, _d, _d, _d, _d, _d, _d, _i32, _i32, _i32]
         L.orc_turbulence.restype = None
@@ -78,6 +82,31 @@ def sim_step(cfg, y, der, wind, turb, cmd):
     return dict(y=y, der=der, hist=hist, cmd=cmd, term=term, nfev=nfev, naccept=nacc)
 
 
+def sim_step_params(cfg, params, y, der, wind, turb, cmd):
+    """PyFly.step of aircraft with their own parameters ``params`` [n][FW_NPARAM] (simulator parameter
+    randomisation): _forces reads them, the frozen inertia / gammas / aspect ratio stay ``cfg``'s."""
+    L = lib()
+    n = len(y)
+    out = dict(y=np.array(y, dtype=np.float64), der=np.array(der, dtype=np.float64), hist=np.zeros((n, 9)),
+               cmd=np.array(cmd, dtype=np.float64), term=np.zeros(n, np.int32), nfev=np.zeros(n, np.int32),
+               naccept=np.zeros(n, np.int32))
+    p0 = np.ascontiguousarray(np.array(cfg.param[:]), dtype=np.float64)
+    for i in range(n):
+        c = C.FwSimConfig.from_buffer_copy(cfg)
+        for k in range(C.FW_NPARAM):
+            c.param[k] = float(params[i][k])
+        yi, di, hi = out["y"][i].copy(), out["der"][i].copy(), out["hist"][i].copy()
+        ci = out["cmd"][i].copy()
+        nf, na = np.zeros(1, np.int32), np.zeros(1, np.int32)
+        out["term"][i] = L.orc_sim_step_p(ctypes.byref(c), _p(p0), _p(yi), _p(di), _p(hi),
+                                          _p(np.ascontiguousarray(wind[i], dtype=np.float64)),
+                                          _p(np.ascontiguousarray(turb[i], dtype=np.float64)), _p(ci),
+                                          _p(nf, _i32), _p(na, _i32))
+        out["y"][i], out["der"][i], out["hist"][i], out["cmd"][i] = yi, di, hi, ci
+        out["nfev"][i], out["naccept"][i] = nf[0], na[0]
+    return out
+
+
 def turbulence(cfg, noise, k):
     L = lib()
     noise = np.ascontiguousarray(noise, dtype=np.float64)
@@ -119,6 +148,11 @@ class OracleEnv:
             raise RuntimeError("reset constraint violation code %d" % t)
         self.noise = np.ascontiguousarray(noise if noise is not None else np.zeros((4, 1)), dtype=np.float64)
         return obs
+
+    def set_params(self, params):
+        """This aircraft's own simulator parameters (after reset, which clears them)."""
+        self.L.orc_env_set_params(self.buf, ctypes.byref(self.sim_cfg),
+                                  _p(np.ascontiguousarray(params, dtype=np.float64)))
 
     def step(self, action):
         a = np.ascontiguousarray(action, dtype=np.float64)

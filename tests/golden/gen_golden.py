@@ -26,6 +26,7 @@ Fixtures (all float64 unless noted):
   pyfly_solver_fail.npz   PyFly.step when the RK45 integration fails (sol.y[:, -1] committed)
   pyfly_energy.npz        energy states along PID / constraint-terminated trajectories
   env_curriculum.npz      set_curriculum_level ranges/constraints/targets and sampled resets
+  env_rand_params.npz     simulator parameter randomisation: sampled parameters and episodes flown with them
 """
 import hashlib
 import json
@@ -901,9 +902,74 @@ def gen_curriculum():
     np.savez_compressed(os.path.join(OUT, "env_curriculum.npz"), **out)
     print("curriculum: %d levels, %d simulator states" % (len(levels), len(names)))
 
+
+# ---------------------------------------------------------------------------
+# L. simulator parameter randomisation (FixedWingAircraft.sample_simulator_parameters,
+#    fixed_wing.py:748-813)
+# ---------------------------------------------------------------------------
+
+RAND_MODELS = {
+    # relative gaussian with a clip: negative originals (C_m_alpha, C_l_p, C_m_q) hit the reference's
+    # signed-clip quirk (lo > hi -> always original + clip); inertia / wing geometry exercise the
+    # frozen gammas / aspect ratio
+    "gauss_rel": {"var_type": "relative", "var": 0.1, "distribution": "gaussian", "clip": 0.25,
+                  "parameters": [{"name": "C_L_alpha"}, {"name": "mass"}, {"name": "Jy"}, {"name": "Jx"},
+                                 {"name": "C_m_alpha", "var": 0.2}, {"name": "b"}, {"name": "S_wing"},
+                                 {"name": "e"}, {"name": "C_D_p"}, {"name": "k_motor"}, {"name": "C_l_p"},
+                                 {"name": "C_m_q"}, {"name": "C_n_beta"}, {"name": "c"}]},
+    "unif_abs": {"var_type": "absolute", "var": 0.05, "distribution": "uniform",
+                 "parameters": [{"name": "C_L_0"}, {"name": "C_m_0", "var": 0.01}, {"name": "a_0"},
+                                {"name": "M", "var": 5.0}, {"name": "C_Y_beta"}, {"name": "k_T_P", "var": 1e-4}]},
+}
+
+
+def gen_rand_params():
+    import copy
+    out = {}
+    import tempfile
+    for name, model in RAND_MODELS.items():
+        # the gym config with a "model" block (config_kw cannot add keys, fixed_wing.py:34-48)
+        cfg = json.load(open(GYM_CFG))
+        cfg["simulator"]["model"] = copy.deepcopy(model)
+        path = os.path.join(tempfile.mkdtemp(), "fixed_wing_config.json")
+        with open(path, "w") as f:
+            json.dump(cfg, f)
+        out[name + "__config_json"] = np.array(json.dumps(cfg))
+        env = FixedWingAircraft(path, config_kw={"steps_max": 400},
+                                sim_config_kw={"turbulence": False, "turbulence_intensity": "light"})
+        env.seed(0)
+        pnames = sorted(env.simulator.params.keys())
+        out[name + "__model_json"] = np.array(json.dumps(model))
+        # distribution: 400 resets, the sampled value of every randomised parameter
+        env.seed(77)
+        draws = []
+        for _ in range(400):
+            env.reset()
+            draws.append([env.simulator.params[p["name"]] for p in model["parameters"]])
+        out[name + "__draws"] = np.array(draws)
+        # dynamics: episodes from explicit states with the reference's own draw, random actions
+        rng = np.random.RandomState(11)
+        for ep in range(3):
+            res = env_episode(env, rng, False, 400)
+            vals = {}
+            for p in pnames:
+                if p.startswith("__"):
+                    continue
+                try:
+                    vals[p] = float(np.asarray(env.simulator.params[p]).reshape(-1)[0])
+                except (TypeError, ValueError):
+                    continue
+            out["%s__ep%d__param_names" % (name, ep)] = np.array(sorted(vals))
+            out["%s__ep%d__param_values" % (name, ep)] = np.array([vals[p] for p in sorted(vals)])
+            for k, v in res.items():
+                out["%s__ep%d__%s" % (name, ep, k)] = v
+        print("rand params %s: %d draws, episode lengths %s" % (
+            name, len(draws), [len(out["%s__ep%d__rew" % (name, e)]) for e in range(3)]))
+    np.savez_compressed(os.path.join(OUT, "env_rand_params.npz"), **out)
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["single", "traj", "envelope", "dryden", "env", "pidset", "metrics", "obshist",
-                             "solverfail", "energy", "curriculum"]
+                             "solverfail", "energy", "curriculum", "randparams"]
     if "envelope" in which and "traj" not in which:
         gen_envelope()
     if "obshist" in which:
@@ -928,3 +994,5 @@ if __name__ == "__main__":
         gen_energy()
     if "curriculum" in which:
         gen_curriculum()
+    if "randparams" in which:
+        gen_rand_params()

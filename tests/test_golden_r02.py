@@ -128,3 +128,69 @@ def test_philox_noise_restatement_distribution():
     assert not np.allclose(RNG.turbulence_noise(77, np.arange(8), 2, 50), z[:8, :, :50])  # next episode
     assert not np.allclose(RNG.turbulence_noise(78, np.arange(8), 1, 50), z[:8, :, :50])  # other seed
     np.testing.assert_array_equal(RNG.turbulence_noise(77, np.arange(100, 108), 1, 50), z[100:108, :, :50])
+
+
+# ---------------------------------------------------------------------------- parameter randomisation
+RAND_CASES = ["gauss_rel", "unif_abs"]
+
+
+def rand_spec(name, tmpdir):
+    """EnvSpec of an env_rand_params.npz case (the reference's gym config with a "model" block)."""
+    import os
+    d = F.load("env_rand_params.npz")
+    path = os.path.join(str(tmpdir), name + ".json")
+    with open(path, "w") as f:
+        f.write(str(d[name + "__config_json"]))
+    return C.EnvSpec(config_path=path, config_kw={"steps_max": 400}, sim_config_kw={"turbulence": False}), d
+
+
+def episode_params(d, name, ep):
+    """The fixture episode's parameter values in fw_param order."""
+    vals = dict(zip([str(n) for n in d["%s__ep%d__param_names" % (name, ep)]], d["%s__ep%d__param_values" % (name, ep)]))
+    return np.array([vals[n] for n in C.PARAM_NAMES])
+
+
+@pytest.mark.parametrize("name", RAND_CASES)
+def test_rand_params_config_parsing(name, tmpdir):
+    """sample_simulator_parameters' arithmetic (fixed_wing.py:768-800) as fw_rand_param entries: relative
+    var scaled by |original|, clip by the signed original; checked against the reference's own draws
+    (all inside the clip window; a negative original makes the window empty, every draw = original + clip)."""
+    import json
+    spec, d = rand_spec(name, tmpdir)
+    model = json.loads(str(d[name + "__model_json"]))
+    assert len(spec.rand_params) == len(model["parameters"])
+    draws = d[name + "__draws"]
+    for j, (pi, dist, orig, var, clip) in enumerate(spec.rand_params):
+        assert C.PARAM_NAMES[pi] == model["parameters"][j]["name"]
+        x = draws[:, j]
+        if dist == C.FW_DIST_UNIFORM:
+            assert np.all(x >= orig - var - 1e-12) and np.all(x <= orig + var + 1e-12)
+            assert abs(x.mean() - orig) < 0.2 * var
+        else:
+            lo, hi = orig - clip, orig + clip
+            if lo > hi:
+                np.testing.assert_allclose(x, hi, rtol=1e-14)  # np.clip with a_min > a_max
+            else:
+                assert np.all(x >= lo - 1e-12) and np.all(x <= hi + 1e-12)
+                assert abs(np.median(x) - orig) < 0.2 * var and 0.7 * var < x.std() < 1.1 * var
+
+
+@pytest.mark.parametrize("name", RAND_CASES)
+def test_oracle_flies_reference_sampled_parameters(name, tmpdir):
+    """Episodes the reference flew with its sampled parameters: the oracle given the same parameters (and
+    the frozen inertia / gammas / aspect ratio of the config) reproduces obs and rewards."""
+    spec, d = rand_spec(name, tmpdir)
+    for ep in range(3):
+        g = lambda k: d["%s__ep%d__%s" % (name, ep, k)]  # noqa: E731
+        env = O.OracleEnv(spec.sim.struct(), spec.struct(), spec.n_obs)
+        obs0 = env.reset(F.env_init(g("init")), g("target0"))
+        env.set_params(episode_params(d, name, ep))
+        np.testing.assert_allclose(obs0, g("obs")[0], rtol=1e-12, atol=1e-12)
+        for s, a in enumerate(g("act")):
+            obs, r, done, term, _ = env.step(a)
+            assert done == bool(g("done")[s]), (ep, s)
+            tol = 1e-6 + 1e-6 * s
+            assert abs(r - g("rew")[s]) <= tol, (ep, s, r, g("rew")[s])
+            np.testing.assert_allclose(obs, g("obs")[s + 1], rtol=1e-5, atol=tol)
+            if done:
+                break

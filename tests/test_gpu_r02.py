@@ -467,3 +467,75 @@ def test_offpolicy_chunked_warmup_equals_stepwise():
     for name in ("observations", "next_observations", "actions", "rewards", "dones"):
         assert torch.equal(getattr(bufs[0], name), getattr(bufs[1], name)), name
     assert bufs[0].pos == bufs[1].pos and bufs[0].full == bufs[1].full
+
+
+# ---------------------------------------------------------------------------- parameter randomisation (a13)
+@pytest.mark.parametrize("name", ["gauss_rel", "unif_abs"])
+def test_device_rand_params_distribution(name, tmpdir):
+    """sample_simulator_parameters on the device (Philox): every aircraft's draw lies in the reference's
+    support, the signed-clip quirk gives the same constant, and the draws follow the reference's own
+    distribution (two-sample KS against its 400 draws); redrawn at each reset, shard-invariant."""
+    from scipy import stats
+    from test_golden_r02 import rand_spec
+    spec, d = rand_spec(name, tmpdir)
+    n = 4096
+    eng = _engine(spec.sim, spec, n, "float64")
+    eng.seed(3)
+    eng.reset()
+    P1 = eng.get_block(C.FW_BLK_PARAMS).cpu().numpy()
+    eng.reset()
+    P2 = eng.get_block(C.FW_BLK_PARAMS).cpu().numpy()
+    draws = d[name + "__draws"]
+    for j, (pi, dist, orig, var, clip) in enumerate(spec.rand_params):
+        x = P1[pi]
+        if dist == C.FW_DIST_GAUSSIAN and orig - clip > orig + clip:
+            np.testing.assert_allclose(x, orig + clip, rtol=1e-14)
+            continue
+        lo, hi = (orig - var, orig + var) if dist == C.FW_DIST_UNIFORM else (orig - clip, orig + clip)
+        assert np.all(x >= lo - 1e-12) and np.all(x <= hi + 1e-12), C.PARAM_NAMES[pi]
+        assert stats.ks_2samp(x, draws[:, j]).pvalue > 1e-3, C.PARAM_NAMES[pi]
+        assert not np.array_equal(P1[pi], P2[pi])  # a new draw per episode
+    untouched = sorted(set(range(C.FW_NPARAM)) - {r[0] for r in spec.rand_params})
+    base = np.array(spec.sim.struct().param[:])
+    np.testing.assert_array_equal(P1[untouched], np.repeat(base[untouched, None], n, axis=1))
+    half = _engine(spec.sim, spec, n // 2, "float64")
+    half.seed(3, env_offset=n // 2)
+    half.reset()
+    np.testing.assert_array_equal(half.get_block(C.FW_BLK_PARAMS).cpu().numpy(), P1[:, n // 2:])
+    eng.close()
+    half.close()
+
+
+@pytest.mark.parametrize("precision", ["float64", "float32"])
+@pytest.mark.parametrize("name", ["gauss_rel", "unif_abs"])
+def test_device_flies_reference_sampled_parameters(name, precision, tmpdir):
+    """The reference's episodes flown with its sampled parameters (env_rand_params.npz), replayed on the
+    device with the same per-aircraft parameters (fw_set_state FW_BLK_PARAMS): fp64 obs / rewards as
+    the env sequences (1e-6 + 1e-6/step), fp32 within 2e-3 (1 + |ref|) over the first 100 steps."""
+    from test_golden_r02 import episode_params, rand_spec
+    spec, d = rand_spec(name, tmpdir)
+    eps = 3
+    eng = _engine(spec.sim, spec, eps, precision)
+    g = lambda ep, k: d["%s__ep%d__%s" % (name, ep, k)]  # noqa: E731
+    init = np.stack([F.env_init(g(ep, "init")) for ep in range(eps)], axis=1)
+    tgt = np.stack([g(ep, "target0") for ep in range(eps)], axis=1)
+    eng.reset(init=init, target=tgt)
+    eng.set_block(C.FW_BLK_PARAMS, np.stack([episode_params(d, name, ep) for ep in range(eps)], axis=1))
+    steps = len(g(0, "act")) if precision == "float64" else 100
+    acts = np.stack([g(ep, "act")[:steps] for ep in range(eps)], axis=1)
+    for s in range(steps):
+        o, r, dn, _ = eng.env_step(torch.tensor(acts[s], dtype=eng.dtype, device=DEV), auto_reset=False)
+        o, r, dn = o.double().cpu().numpy(), r.double().cpu().numpy(), dn.cpu().numpy()
+        for ep in range(eps):
+            if s >= len(g(ep, "rew")):
+                continue
+            ref_o = eng.terminal_obs[ep].double().cpu().numpy() if dn[ep] else o[ep]
+            if precision == "float64":
+                tol = 1e-6 + 1e-6 * s
+                assert abs(r[ep] - g(ep, "rew")[s]) <= tol, (ep, s)
+                np.testing.assert_allclose(ref_o, g(ep, "obs")[s + 1], rtol=1e-5, atol=tol)
+            else:
+                assert abs(r[ep] - g(ep, "rew")[s]) <= 2e-3 * (1 + abs(g(ep, "rew")[s])), (ep, s)
+                assert np.all(np.abs(ref_o - g(ep, "obs")[s + 1]) <= 2e-3 * (1 + np.abs(g(ep, "obs")[s + 1])))
+            assert bool(dn[ep]) == bool(g(ep, "done")[s]), (ep, s)
+    eng.close()

@@ -22,7 +22,7 @@ SOURCES = UNITS + [os.path.join(CSRC, "fw_device.hpp")] + HEADERS
 ARCH = os.environ.get("FWSIM_ARCH", "gfx950")
 
 _lib = None
-ABI_VERSION = 3  # include/fwsim.h FWSIM_ABI_VERSION
+ABI_VERSION = 4  # include/fwsim.h FWSIM_ABI_VERSION
 
 
 class FwError(RuntimeError):

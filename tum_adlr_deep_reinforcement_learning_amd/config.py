@@ -63,7 +63,8 @@ FW_MAX_OBS_LEN, FW_MAX_OBS_HIST = 16, 64
  FW_I_ACT0, FW_I_ACT0_DOT, FW_I_ACT1, FW_I_ACT1_DOT, FW_I_ACT2, FW_I_ACT2_DOT, FW_I_WIND_N, FW_I_WIND_E,
  FW_I_WIND_D, FW_NINIT) = range(22)
 
-FW_BLK_ODE, FW_BLK_DERIVED, FW_BLK_TARGET, FW_BLK_WIND, FW_BLK_STEPS, FW_BLK_COMMAND = range(6)
+FW_BLK_ODE, FW_BLK_DERIVED, FW_BLK_TARGET, FW_BLK_WIND, FW_BLK_STEPS, FW_BLK_COMMAND, FW_BLK_PARAMS = range(7)
+FW_DIST_GAUSSIAN, FW_DIST_UNIFORM = 0, 1
 
 # episode-metric record (include/fwsim.h FW_M_*): name -> (first column, info keys)
 FW_NMETRIC = 28
@@ -121,6 +122,11 @@ class FwRewFactor(ctypes.Structure):
                 ("scaling", ctypes.c_double), ("max", ctypes.c_double), ("sign", ctypes.c_double)]
 
 
+class FwRandParam(ctypes.Structure):
+    _fields_ = [("param", ctypes.c_int32), ("dist", ctypes.c_int32), ("original", ctypes.c_double),
+                ("var", ctypes.c_double), ("clip", ctypes.c_double)]
+
+
 class FwEnvConfig(ctypes.Structure):
     _fields_ = [("steps_max", ctypes.c_int32), ("n_obs", ctypes.c_int32),
                 ("obs", FwObsEntry * FW_MAX_OBS),
@@ -142,7 +148,9 @@ class FwEnvConfig(ctypes.Structure):
                 ("rise_low", ctypes.c_double), ("rise_high", ctypes.c_double),
                 ("obs_length", ctypes.c_int32), ("obs_step", ctypes.c_int32),
                 ("obs_noise", ctypes.c_int32), ("pad3_", ctypes.c_int32),
-                ("obs_noise_mean", ctypes.c_double), ("obs_noise_std", ctypes.c_double)]
+                ("obs_noise_mean", ctypes.c_double), ("obs_noise_std", ctypes.c_double),
+                ("n_rand", ctypes.c_int32), ("pad4_", ctypes.c_int32),
+                ("rand", FwRandParam * FW_NPARAM)]
 
 
 # ---------------------------------------------------------------------------
@@ -477,13 +485,46 @@ class EnvSpec:
             raise NotImplementedError("target.resample_every")
         if cfg["target"].get("on_success", "none") not in ("none", "done"):
             raise NotImplementedError("target.on_success=%r" % cfg["target"].get("on_success"))
-        sim_keys = set(cfg.get("simulator", {}).keys()) - {"states"}
-        if sim_keys:
-            raise NotImplementedError("simulator parameter randomisation (%s)" % sorted(sim_keys))
+        sim_keys = set(cfg.get("simulator", {}).keys()) - {"states", "model"}
+        if sim_keys:  # setattr(simulator, key, sample) of arbitrary simulator attributes (fixed_wing.py:802-813)
+            raise NotImplementedError("randomised simulator attributes %s (only 'model' parameters)" % sorted(sim_keys))
+        self.rand_params = self._parse_model(cfg.get("simulator", {}).get("model"))
         self.scale_actions = bool(cfg["action"].get("scale_space", False))
         self.metrics_enabled = True  # track cfg["metrics"] on the device (False: skip that state traffic)
         self.set_curriculum_level(curriculum_level)
         self._build_spaces()
+
+    def _parse_model(self, m):
+        """The "simulator": {"model": ...} block -> fw_rand_param entries (sample_simulator_parameters,
+        fixed_wing.py:748-800): gaussian N(original, var) clipped to original -+ clip, or uniform
+        U(original -+ var); "relative" var_type scales var by |original| and clip by original (sign kept,
+        like the reference); parameters whose original value is 0 are skipped, as there."""
+        if not m:
+            return []
+        dist = m.get("distribution", "gaussian")
+        if dist not in ("gaussian", "uniform"):
+            raise ValueError("Unexpected distribution type {}".format(dist))
+        out = []
+        for pa in m["parameters"]:
+            name = pa["name"]
+            if name not in PARAM_NAMES:
+                raise NotImplementedError("randomised parameter %r (not a simulator parameter read by the "
+                                          "dynamics)" % name)
+            orig = pa.get("original")
+            orig = float(self.sim.params[name] if orig is None else orig)
+            if orig == 0:
+                continue
+            var = float(pa.get("var", m["var"]))
+            if m["var_type"] == "relative":
+                var *= abs(orig)
+            clip = pa.get("clip", m.get("clip"))
+            if clip is not None and dist == "gaussian":
+                clip = float(clip) * (orig if m["var_type"] == "relative" else 1.0)
+            else:
+                clip = None
+            out.append((PARAM_NAMES.index(name), FW_DIST_GAUSSIAN if dist == "gaussian" else FW_DIST_UNIFORM,
+                        orig, var, clip))
+        return out
 
     # fixed_wing.py:334-412
     def set_curriculum_level(self, level):
@@ -605,6 +646,11 @@ class EnvSpec:
         cfg = self.cfg
         e = FwEnvConfig()
         e.steps_max = self.steps_max
+        e.n_rand = len(self.rand_params)
+        for r, (pi, dist, orig, var, clip) in enumerate(self.rand_params):
+            R = e.rand[r]
+            R.param, R.dist, R.original, R.var = pi, dist, orig, var
+            R.clip = float("nan") if clip is None else clip
         states = cfg["observation"]["states"]
         if len(states) > FW_MAX_OBS:
             raise NotImplementedError("more than %d observation entries" % FW_MAX_OBS)

@@ -74,7 +74,7 @@ struct DevCfg {
   T CL0, CLa, CLq, CLde, CDp, CDq, CDb1, CDb2, CDde, Cm0, Cma, Cmq, Cmde, Cmfp;
   T CY0, CYb, CYp, CYr, CYda, CYdr, Cl0, Clb, Clp, Clr, Clda, Cldr, Cn0, Cnb, Cnp, Cnr, Cnda, Cndr;
   T kmotor, prop_k, kTP, kOmega;
-  T rho, Sprop, Cprop;
+  T Sprop, Cprop;
   T ac[3][6];                // actuator coefs c00 c01 c02 c10 c11 c12 (ControlVariable.coefs)
   T dot_max[3];
   Lim<T> lim[FW_NVAR];
@@ -83,6 +83,16 @@ struct DevCfg {
   uint32_t dotmask;                    // per actuator: dot_max finite
   int elevon, disabled_inputs, turbulence, turb_len, wind_random;
   int max_nfev;                        // RHS-evaluation budget of one step
+  // simulator parameter randomisation (FixedWingAircraft.sample_simulator_parameters,
+  // fixed_wing.py:748-813): per-aircraft parameter rows redrawn at every reset
+  int rand_params;                     // 1: aircraft read their own parameter rows (State::prm)
+  int n_rand;
+  struct RandP {
+    int param, dist, has_clip, pad;
+    T orig, var, clip;
+  } rp[FW_NPARAM];
+  T pdef[FW_NPARAM];                   // parameter values of the un-randomised aircraft (x8_param.mat)
+  T rho, grav, ar0;                    // air density, g, aspect ratio b^2/S of the config (pyfly.py:1119)
   int trig_alpha, trig_beta;           // alpha/beta limited -> use trig of the clipped angle
   int euler_exact;                     // roll/pitch/yaw limited -> Euler-angle rotation post step
   T wind_mag_min, wind_mag_max, wind_init_min[3], wind_init_max[3];
@@ -124,6 +134,7 @@ struct SpecCfg : DevCfg<T> {
   static constexpr uint32_t cmask = CM, clipmask = CLM, wrapmask = WM, dotmask = DM;
   static constexpr int elevon = ELEVON, trig_alpha = TA, trig_beta = TB, euler_exact = EE;
   static constexpr int obs_general = 0;  // specialisations serve plain length-1, noise-free observations
+  static constexpr int rand_params = 0;  // ... with one parameter set for all aircraft
 };
 // fixed_wing_config.json (gym): omega +-720 deg/s and Va <= 70 constrained; Va, actuators,
 // elevator / aileron / throttle clipped; roll / yaw wrapped; elevon rate limits
@@ -347,8 +358,10 @@ FW_HD void airspeed_vec_euler(T phi, T th, T psi, const T* w, const T* tl, const
 // conditioned first (_set_states_from_ode_solution(save=False)), which can
 // terminate the step.  Returns the first violated condition (0 = none).
 // ---------------------------------------------------------------------------
-template <typename T, typename C>
-FW_HD int rhs(const C& c0, const StepCtx<T>& X, bool first, const T* y, T* dy) {
+// `a` supplies the parameter-derived constants (qS, C_L_0, mass, ...): the config itself (same
+// field names, uniform) or a per-aircraft AeroP when simulator parameters are randomised.
+template <typename T, typename C, typename A>
+FW_HD int rhs(const C& c0, const A& a, const StepCtx<T>& X, bool first, const T* y, T* dy) {
 #ifdef FW_RHS_TRIVIAL  // ISA accounting experiment only (tools/isa_loop.sh -DFW_RHS_TRIVIAL)
   for (int i = 0; i < NY; i++) dy[i] = y[i] * X.sp[0];
   return 0;
@@ -424,41 +437,41 @@ FW_HD int rhs(const C& c0, const StepCtx<T>& X, bool first, const T* y, T* dy) {
   }
 
   const T V2a = Va * Va;
-  const T fg0 = c.mg * (T(2) * (e1 * e3 - e2 * e0));
-  const T fg1 = c.mg * (T(2) * (e2 * e3 + e1 * e0));
-  const T fg2 = c.mg * (e3 * e3 + e0 * e0 - e1 * e1 - e2 * e2);
-  const T ex1 = fexp(-c.M * (alpha - c.a0));
-  const T ex2 = fexp(c.M * (alpha + c.a0));
+  const T fg0 = a.mg * (T(2) * (e1 * e3 - e2 * e0));
+  const T fg1 = a.mg * (T(2) * (e2 * e3 + e1 * e0));
+  const T fg2 = a.mg * (e3 * e3 + e0 * e0 - e1 * e1 - e2 * e2);
+  const T ex1 = fexp(-a.M * (alpha - a.a0));
+  const T ex2 = fexp(a.M * (alpha + a.a0));
   // stall blend sigma = (1+e1+e2) / ((1+e1)(1+e2)) (pyfly.py:1541-1543).  Since
   // e1 e2 = exp(2 M a0) = C, the denominator is S + C with S = 1+e1+e2, so
   // sigma = 1 / (1 + C/S): the same value, but it never forms the ~1e38 product
   // (whose fp32 reciprocal flushes to 0 and flips sigma from 1 to 0 deep in
   // stall) and it is exactly 1 when an exponential overflows.
-  const T sigma = frcp(T(1) + c.sig_c * frcp(T(1) + ex1 + ex2));
+  const T sigma = frcp(T(1) + a.sig_c * frcp(T(1) + ex1 + ex2));
   const T osig = T(1) - sigma;
   const T sgna = sgn(alpha);
-  const T CLlin = c.CL0 + c.CLa * alpha;
+  const T CLlin = a.CL0 + a.CLa * alpha;
   const T CL = osig * CLlin + sigma * (T(2) * sgna * sa * sa * ca);
   const T iVa = frcp(Va);
   const T qn = q * iVa;  // q / Va
   // lift / drag / pitch moment per unit dynamic pressure (pyfly.py:1529-1579)
-  const T flift = c.qS * V2a * (CL + c.kCLq * qn + c.CLde * elev);
-  const T CD = c.CDp + osig * (CLlin * CLlin) * c.inv_pi_e_ar + sigma * (T(2) * sgna * (sa * sa * sa));
-  const T CDb = c.CDb1 * beta + c.CDb2 * beta * beta;
-  const T fdrag = c.qS * V2a * (CD + CDb + c.kCDq * qn + c.CDde * elev * elev);
-  const T Cm = osig * (c.Cm0 + c.Cma * alpha) + sigma * (c.Cmfp * sgna * sa * sa);
-  const T mm = c.qSc * V2a * (Cm + c.kCmq * qn + c.Cmde * elev);
-  const T bp = c.hb * p * iVa, br = c.hb * r * iVa;
-  const T fy = c.qS * V2a * (c.CY0 + c.CYb * beta + c.CYp * bp + c.CYr * br + c.CYda * ail);
-  const T ll = c.qSb * V2a * (c.Cl0 + c.Clb * beta + c.Clp * bp + c.Clr * br + c.Clda * ail);
-  const T nn = c.qSb * V2a * (c.Cn0 + c.Cnb * beta + c.Cnp * bp + c.Cnr * br + c.Cnda * ail);
+  const T flift = a.qS * V2a * (CL + a.kCLq * qn + a.CLde * elev);
+  const T CD = a.CDp + osig * (CLlin * CLlin) * a.inv_pi_e_ar + sigma * (T(2) * sgna * (sa * sa * sa));
+  const T CDb = a.CDb1 * beta + a.CDb2 * beta * beta;
+  const T fdrag = a.qS * V2a * (CD + CDb + a.kCDq * qn + a.CDde * elev * elev);
+  const T Cm = osig * (a.Cm0 + a.Cma * alpha) + sigma * (a.Cmfp * sgna * sa * sa);
+  const T mm = a.qSc * V2a * (Cm + a.kCmq * qn + a.Cmde * elev);
+  const T bp = a.hb * p * iVa, br = a.hb * r * iVa;
+  const T fy = a.qS * V2a * (a.CY0 + a.CYb * beta + a.CYp * bp + a.CYr * br + a.CYda * ail);
+  const T ll = a.qSb * V2a * (a.Cl0 + a.Clb * beta + a.Clp * bp + a.Clr * br + a.Clda * ail);
+  const T nn = a.qSb * V2a * (a.Cn0 + a.Cnb * beta + a.Cnp * bp + a.Cnr * br + a.Cnda * ail);
   // f_aero = R_euler(0, alpha, beta) . [-D, Y, -L]
   const T fa0 = ca * cb * (-fdrag) + ca * sb * fy - sa * (-flift);
   const T fa1 = -sb * (-fdrag) + cb * fy;
   const T fa2 = sa * cb * (-fdrag) + sa * sb * fy + ca * (-flift);
-  const T Vd = Va + thr * (c.kmotor - Va);
-  const T fprop = c.prop_k * Vd * (Vd - Va);
-  const T tprop = -c.kTP2 * (thr * thr);
+  const T Vd = Va + thr * (a.kmotor - Va);
+  const T fprop = a.prop_k * Vd * (Vd - Va);
+  const T tprop = -a.kTP2 * (thr * thr);
   const T f0 = fprop + fg0 + fa0, f1 = fg1 + fa1, f2 = fg2 + fa2;
   const T t0 = ll + tprop, t1 = mm, t2 = nn;
 
@@ -480,9 +493,9 @@ FW_HD int rhs(const C& c0, const StepCtx<T>& X, bool first, const T* y, T* dy) {
   dy[9] = T(2) * (e1 * e3 - e2 * e0) * vel[0] + T(2) * (e2 * e3 + e1 * e0) * vel[1] +
           (e3 * e3 + e0 * e0 - e1 * e1 - e2 * e2) * vel[2];
   // _f_v_dot (pyfly.py:1685-1704)
-  dy[10] = R0 * vel[1] - Q0 * vel[2] + f0 * c.inv_mass;
-  dy[11] = P0 * vel[2] - R0 * vel[0] + f1 * c.inv_mass;
-  dy[12] = Q0 * vel[0] - P0 * vel[1] + f2 * c.inv_mass;
+  dy[10] = R0 * vel[1] - Q0 * vel[2] + f0 * a.inv_mass;
+  dy[11] = P0 * vel[2] - R0 * vel[0] + f1 * a.inv_mass;
+  dy[12] = Q0 * vel[0] - P0 * vel[1] + f2 * a.inv_mass;
   // Actuation.rhs (pyfly.py:519-543)
 #pragma unroll
   for (int j = 0; j < 3; j++) {
@@ -530,8 +543,8 @@ constexpr int lds_slots() {
   return 2 + FW_ER_LDS + ((sizeof(T) == 4 && FW_P_LDS) ? 4 : 0);
 }
 
-template <typename T, typename C>
-FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy, V2<T>* __restrict__ sf, int stride,
+template <typename T, typename C, typename A>
+FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy, V2<T>* __restrict__ sf, int stride,
                int& nfev, int& nacc, V2<T>* __restrict__ se = nullptr) {
   using V = V2<T>;
   constexpr double A10 = 1.0 / 5;
@@ -613,7 +626,7 @@ FW_HD int rk45(const C& c, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy,
 #define YR(p) Y(p)
 #endif
     {
-      const int term = rhs(c, X, stage == 0, (const T*)ys, (T*)K);
+      const int term = rhs(c, a, X, stage == 0, (const T*)ys, (T*)K);
       K[NP - 1].y = T(0);  // pad element
       if (active) {
         nfev++;
@@ -831,6 +844,53 @@ FW_HD void dryden(const DevCfg<T>& c, int k, const T* un1, const T* u0, T* tl, T
 }
 
 // ---------------------------------------------------------------------------
+// Per-aircraft parameter-derived constants of the RHS (simulator parameter randomisation).  The
+// reference samples simulator.params at every reset and _forces reads them at every RHS call
+// (pyfly.py:1514-1643); the inertia gammas / I (pyfly.py:1086-1116) and the aspect ratio ar
+// (pyfly.py:1119) are computed once in PyFly.__init__ and are NOT refreshed (quirk kept: they stay
+// the config's values, DevCfg.gam / inv_Jy / ar0), nor are the EnergyVariable mass and inertia.
+// ---------------------------------------------------------------------------
+template <typename T>
+struct AeroP {
+  T qS, qSc, qSb, kCLq, kCDq, kCmq, hb, inv_pi_e_ar, kTP2, prop_k, mg, inv_mass, sig_c, M, a0, kmotor;
+  T CL0, CLa, CLde, CDp, CDb1, CDb2, CDde, Cm0, Cma, Cmde, Cmfp;
+  T CY0, CYb, CYp, CYr, CYda, Cl0, Clb, Clp, Clr, Clda, Cn0, Cnb, Cnp, Cnr, Cnda;
+};
+
+// P: the aircraft's parameter values in fw_param order (P(k) -> value)
+template <typename T, typename C, typename PF>
+FW_HD AeroP<T> aero_from(const C& c, PF P) {
+  AeroP<T> a;
+  const T S = P(FW_P_S_WING), b = P(FW_P_B), ch = P(FW_P_C);
+  a.qS = T(0.5) * c.rho * S;
+  a.qSc = a.qS * ch;
+  a.qSb = a.qS * b;
+  a.kCLq = P(FW_P_C_L_Q) * ch * T(0.5);
+  a.kCDq = P(FW_P_C_D_Q) * ch * T(0.5);
+  a.kCmq = P(FW_P_C_M_Q) * b * T(0.5);  // pyfly.py:1579 uses b, not c
+  a.hb = b * T(0.5);
+  a.inv_pi_e_ar = T(1) / (T(PI_D) * P(FW_P_E) * c.ar0);
+  a.kTP2 = P(FW_P_K_T_P) * P(FW_P_K_OMEGA) * P(FW_P_K_OMEGA);
+  a.prop_k = T(0.5) * c.rho * P(FW_P_S_PROP) * P(FW_P_C_PROP);
+  a.mg = P(FW_P_MASS) * c.grav;
+  a.inv_mass = T(1) / P(FW_P_MASS);
+  a.M = P(FW_P_M);
+  a.a0 = P(FW_P_A0);
+  a.sig_c = exp(T(2) * a.M * a.a0);
+  a.kmotor = P(FW_P_K_MOTOR);
+  a.CL0 = P(FW_P_C_L_0); a.CLa = P(FW_P_C_L_ALPHA); a.CLde = P(FW_P_C_L_DELTA_E);
+  a.CDp = P(FW_P_C_D_P); a.CDb1 = P(FW_P_C_D_BETA1); a.CDb2 = P(FW_P_C_D_BETA2); a.CDde = P(FW_P_C_D_DELTA_E);
+  a.Cm0 = P(FW_P_C_M_0); a.Cma = P(FW_P_C_M_ALPHA); a.Cmde = P(FW_P_C_M_DELTA_E); a.Cmfp = P(FW_P_C_M_FP);
+  a.CY0 = P(FW_P_C_Y_0); a.CYb = P(FW_P_C_Y_BETA); a.CYp = P(FW_P_C_Y_P); a.CYr = P(FW_P_C_Y_R);
+  a.CYda = P(FW_P_C_Y_DELTA_A);
+  a.Cl0 = P(FW_P_C_L0_ROLL); a.Clb = P(FW_P_C_L_BETA); a.Clp = P(FW_P_C_L_P); a.Clr = P(FW_P_C_L_R);
+  a.Clda = P(FW_P_C_L_DELTA_A);
+  a.Cn0 = P(FW_P_C_N_0); a.Cnb = P(FW_P_C_N_BETA); a.Cnp = P(FW_P_C_N_P); a.Cnr = P(FW_P_C_N_R);
+  a.Cnda = P(FW_P_C_N_DELTA_A);
+  return a;
+}
+
+// ---------------------------------------------------------------------------
 // One PyFly.step for one aircraft (pyfly.py:1358-1420).
 //   y[19]     ODE state (in/out)            der[8] roll pitch yaw Va alpha beta elev ail (in/out;
 //             only der[6..7] are read: the t == 0 elevator/aileron values)
@@ -851,8 +911,8 @@ struct KeepY {  // default: y stays live in registers across the integration
 // `reload(y)` runs right after the integration and may re-read the pre-step
 // state from memory (the kernels do: keeping 19 values live across the RK loop
 // costs registers the loop needs).
-template <typename T, typename C, typename R = KeepY>
-FW_HD int sim_step_masked(const C& c, T* y, T* der, T* cmd, const T* wind, const T* tl, const T* ta, int& nfev,
+template <typename T, typename C, typename A, typename R = KeepY>
+FW_HD int sim_step_masked(const C& c, const A& a, T* y, T* der, T* cmd, const T* wind, const T* tl, const T* ta, int& nfev,
                           int& nacc, uint32_t& dmask, V2<T>* sy, V2<T>* sf, int stride, R reload = R()) {
   dmask = 0;
   StepCtx<T> X;
@@ -871,7 +931,7 @@ FW_HD int sim_step_masked(const C& c, T* y, T* der, T* cmd, const T* wind, const
   T y1[NY];
 #pragma unroll
   for (int i = 0; i < NY; i++) y1[i] = y[i];
-  term = rk45(c, X, y1, sy, sf, stride, nfev, nacc, FW_ER_LDS ? sf + NP * stride : nullptr);
+  term = rk45(c, a, X, y1, sy, sf, stride, nfev, nacc, FW_ER_LDS ? sf + NP * stride : nullptr);
   reload(y);
   if (term < 0) {  // solver failure: y1 = the last accepted sub-step (rk45 wrote Y back), saved as usual
     dmask = DM_SOLVER_FAIL;

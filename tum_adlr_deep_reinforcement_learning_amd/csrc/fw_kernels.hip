@@ -85,6 +85,7 @@ struct State {
   T* met_out;         // [FW_NMETRIC][N] (SoA) record of done envs (null: not requested)
   T* obs_init;        // [n_obs][ld] raw observation row at the episode's reset (null: length-1 observations)
   T* obs_ring;        // [obs_hist][n_obs][ld] raw rows of past steps, slot = step % obs_hist
+  T* prm;             // [FW_NPARAM][ld] per-aircraft parameters (null: no randomisation)
 };
 
 // streaming episode-metric state (fixed_wing.py:1644-1736 restated over running sums):
@@ -605,6 +606,29 @@ __device__ __forceinline__ void reset_lane(const DevCfg<T>& c, const State<T>& s
   der[1] = st[1];
   der[2] = st[2];
   reset_derived(c, y, wind, der);
+  if (c.rand_params && s.prm) {
+    // sample_simulator_parameters (fixed_wing.py:748-813; FixedWingAircraft.reset calls it after
+    // PyFly.reset and before sample_target): Philox stream 5, one block per entry
+#pragma unroll 1
+    for (int k = 0; k < FW_NPARAM; k++) s.prm[k * s.ld + i] = c.pdef[k];
+#pragma unroll 1
+    for (int r = 0; r < c.n_rand; r++) {
+      uint32_t rnd[4];
+      philox(s.key0, s.key1, s.env_offset + (uint32_t)i, episode, 5u, (uint32_t)r, rnd);
+      const T orig = c.rp[r].orig, var = c.rp[r].var;
+      T v;
+      if (c.rp[r].dist == FW_DIST_UNIFORM) {
+        v = (orig - var) + (T(2) * var) * u01<T>(rnd[0]);  // np_random.uniform(orig - var, orig + var)
+      } else {
+        T z[4];
+        normal4<T>(rnd, z);
+        v = orig + var * z[0];  // np_random.normal(loc=orig, scale=var)
+        if (c.rp[r].has_clip)  // np.clip(v, orig - clip, orig + clip) = min(max(v, lo), hi)
+          v = fmin(fmax(v, orig - c.rp[r].clip), orig + c.rp[r].clip);
+      }
+      s.prm[c.rp[r].param * s.ld + i] = v;
+    }
+  }
   if (c.has_env) {
     // sample_target (fixed_wing.py:654-746)
     const T vals[3] = {der[0], der[1], der[3]};
@@ -727,7 +751,7 @@ struct ReloadRow {
   }
 };
 
-template <typename T, typename C>
+template <typename T, typename C, bool RP = false>
 __global__ __launch_bounds__(BLOCK) void k_sim_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
                                                     const T* __restrict__ cmd_in, T* __restrict__ cmd_out,
                                                     uint8_t* __restrict__ success, int32_t* __restrict__ term_out,
@@ -750,8 +774,15 @@ __global__ __launch_bounds__(BLOCK) void k_sim_step(const DevCfg<T>* __restrict_
   int nfev = 0, nacc = 0;
   uint32_t dmask = 0;
   __shared__ V2<T> lds[lds_slots<T>() * NP * BLOCK];  // y, f (+ error sum) of the block's aircraft (pairs)
-  const int term = sim_step_masked(c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
-                                   lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i});
+  int term;
+  if constexpr (RP) {
+    const AeroP<T> ap = aero_from<T>(c, [&](int k) { return s.prm[k * ld + i]; });
+    term = sim_step_masked(c, ap, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
+                           lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i});
+  } else {
+    term = sim_step_masked(c, c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
+                           lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i});
+  }
   if (term) {  // uncommitted derived values keep their previous (history[-1]) value
 #pragma unroll
     for (int r = 0; r < 6; r++)
@@ -774,7 +805,7 @@ __global__ __launch_bounds__(BLOCK) void k_sim_step(const DevCfg<T>* __restrict_
 
 // FixedWingAircraft.step of aircraft i (the body of k_env_step and of one k_env_rollout step).
 // lds: this block's RK45 slots (lds_slots<T>() * NP * BLOCK pairs).
-template <typename T, typename C>
+template <typename T, typename C, bool RP = false>
 __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, const int64_t i, V2<T>* lds,
                                               const T* __restrict__ actions, T* __restrict__ obs_out,
                                               T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
@@ -808,13 +839,15 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   FW_TSTAMP(1);
   int nfev = 0, nacc = 0;
   uint32_t dmask = 0;
-#if FW_LDS_STATE
-  const int sterm = sim_step_masked(c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
-                                    lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i});
-#else
-  V2<T> ry[NP], rf[NP];  // accepted RK state y and f in VGPRs
-  const int sterm = sim_step_masked(c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, ry, rf, 1);
-#endif
+  int sterm;
+  if constexpr (RP) {  // this aircraft's own parameters (simulator parameter randomisation)
+    const AeroP<T> ap = aero_from<T>(c, [&](int k) { return s.prm[k * ld + i]; });
+    sterm = sim_step_masked(c, ap, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
+                            lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i});
+  } else {
+    sterm = sim_step_masked(c, c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
+                            lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i});
+  }
   // keep the epilogue's loads (action ring, goal bits, ...) below the integrator:
   // hoisted above it they would sit in VGPRs for the whole RK loop.  Actions and
   // targets are re-read for the same reason.
@@ -988,7 +1021,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   FW_TSTAMP(4);
 }
 
-template <typename T, typename C>
+template <typename T, typename C, bool RP = false>
 __global__ __launch_bounds__(BLOCK, FW_MIN_WAVES) void k_env_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
                                                     const T* __restrict__ actions, T* __restrict__ obs_out,
                                                     T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
@@ -999,7 +1032,8 @@ __global__ __launch_bounds__(BLOCK, FW_MIN_WAVES) void k_env_step(const DevCfg<T
   if (i >= s.n) return;
   const C& c = *reinterpret_cast<const C*>(cfgp);  // structural specialisation view (fw_device.hpp SpecCfg)
   __shared__ V2<T> lds[lds_slots<T>() * NP * BLOCK];  // y, f (+ error sum) of the block's aircraft (pairs)
-  env_step_lane(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out, stats, auto_reset);
+  env_step_lane<T, C, RP>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out, stats,
+                          auto_reset);
 }
 
 // One env step of k_env_rollout.  Inlined (default), the step loop's kernel spills ~230 VGPRs
@@ -1013,12 +1047,13 @@ __global__ __launch_bounds__(BLOCK, FW_MIN_WAVES) void k_env_step(const DevCfg<T
 #else
 #define FW_ROLLOUT_INLINE __forceinline__
 #endif
-template <typename T, typename C>
+template <typename T, typename C, bool RP>
 __device__ FW_ROLLOUT_INLINE void env_step_call(const C& c, const State<T>& s, const int64_t i, V2<T>* lds,
                                            const T* actions, T* obs_out, T* rew_out, uint8_t* done_out,
                                            int32_t* term_out, T* tobs_out, T* episode_out, int32_t* stats,
                                            int auto_reset) {
-  env_step_lane(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out, stats, auto_reset);
+  env_step_lane<T, C, RP>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out, stats,
+                          auto_reset);
 }
 
 // Open-loop rollout: n_steps consecutive FixedWingAircraft.step calls per aircraft in ONE launch, actions
@@ -1026,7 +1061,7 @@ __device__ FW_ROLLOUT_INLINE void env_step_call(const C& c, const State<T>& s, c
 // the results equal K k_env_step launches bit for bit; what changes is synchronisation: a wave moves on
 // to its next step as soon as its own aircraft are done, instead of every step waiting for the slowest
 // aircraft of the whole batch (the RK45 straggler tail).
-template <typename T, typename C>
+template <typename T, typename C, bool RP = false>
 __global__ __launch_bounds__(BLOCK, FW_MIN_WAVES) void k_env_rollout(const DevCfg<T>* __restrict__ cfgp, State<T> s, int n_steps,
                                                        const T* __restrict__ actions, T* __restrict__ obs_out,
                                                        T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
@@ -1039,7 +1074,7 @@ __global__ __launch_bounds__(BLOCK, FW_MIN_WAVES) void k_env_rollout(const DevCf
   const int64_t n = s.n, ow = (int64_t)cfgp->n_obs * cfgp->obs_len;
   for (int k = 0; k < n_steps; k++) {
     const C& c = *reinterpret_cast<const C*>(cfgp);
-    env_step_call(c, s, i, lds, actions + k * n * 3, obs_out + k * n * ow, rew_out + k * n, done_out + k * n,
+    env_step_call<T, C, RP>(c, s, i, lds, actions + k * n * 3, obs_out + k * n * ow, rew_out + k * n, done_out + k * n,
                   term_out ? term_out + k * n : nullptr, tobs_out ? tobs_out + k * n * ow : nullptr,
                   episode_out ? episode_out + k * n * 5 : nullptr, stats ? stats + k * n : nullptr, auto_reset);
   }
@@ -1073,6 +1108,8 @@ struct fw_handle {
   size_t o_met = 0, o_metu = 0;
   int obs_hist = 0;         // past raw observation rows kept per env ((length - 1) * step + 2, 0 = none)
   size_t o_obs_init = 0, o_obs_ring = 0;
+  size_t o_prm = 0;         // per-aircraft parameter rows (env->n_rand > 0 at create; 0 = none)
+  int rand_active = 0;      // the current config randomises parameters (kernels read the rows)
 };
 
 namespace {
@@ -1088,6 +1125,9 @@ void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
   d.atol = (T)s.atol;
   d.half_rho = (T)(0.5 * s.rho);
   d.rho = (T)s.rho;
+  d.grav = (T)s.g;
+  d.ar0 = (T)(P[FW_P_B] * P[FW_P_B] / P[FW_P_S_WING]);
+  for (int k = 0; k < FW_NPARAM; k++) d.pdef[k] = (T)P[k];
   d.S = (T)P[FW_P_S_WING];
   d.b = (T)P[FW_P_B];
   d.c = (T)P[FW_P_C];
@@ -1232,6 +1272,17 @@ void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
     d.obs_general = d.obs_len > 1 || d.obs_noise;
     std::memcpy(d.obs, e.obs, sizeof(d.obs));
     std::memcpy(d.rew, e.rew, sizeof(d.rew));
+    d.rand_params = e.n_rand > 0 && h->o_prm != 0;
+    d.n_rand = d.rand_params ? e.n_rand : 0;
+    for (int r = 0; r < d.n_rand; r++) {
+      const fw_rand_param& R = e.rand[r];
+      d.rp[r].param = R.param;
+      d.rp[r].dist = R.dist;
+      d.rp[r].has_clip = !std::isnan(R.clip);
+      d.rp[r].orig = (T)R.original;
+      d.rp[r].var = (T)R.var;
+      d.rp[r].clip = d.rp[r].has_clip ? (T)R.clip : T(0);
+    }
   }
 }
 
@@ -1250,6 +1301,11 @@ int validate(const fw_sim_config* s, const fw_env_config* e) {
         (e->obs_length > 1 && (e->obs_length - 1) * std::max(e->obs_step, 1) + 2 > FW_MAX_OBS_HIST))
       return set_err(FW_E_UNSUPPORTED, "observation length / step out of range");
     if (e->obs_noise && !(e->obs_noise_std >= 0)) return set_err(FW_E_INVALID, "observation noise scale < 0");
+    if (e->n_rand < 0 || e->n_rand > FW_NPARAM) return set_err(FW_E_INVALID, "n_rand out of range");
+    for (int r = 0; r < e->n_rand; r++)
+      if (e->rand[r].param < 0 || e->rand[r].param >= FW_NPARAM ||
+          (e->rand[r].dist != FW_DIST_GAUSSIAN && e->rand[r].dist != FW_DIST_UNIFORM))
+        return set_err(FW_E_INVALID, "bad parameter randomisation entry");
     for (int o = 0; o < e->n_obs; o++)
       if (e->obs[o].kind == FW_OBS_ACTION_WINDOW && (e->obs[o].window < 1 || e->obs[o].window > FW_MAX_WINDOW))
         return set_err(FW_E_UNSUPPORTED, "action window out of range");
@@ -1265,7 +1321,8 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // Which compiled structural specialisation (fw_device.hpp SpecCfg) matches this config.
 template <typename S, typename T>
 bool same_structure(const DevCfg<T>& d) {
-  return d.cmask == S::cmask && d.clipmask == S::clipmask && d.wrapmask == S::wrapmask && d.dotmask == S::dotmask &&
+  return d.rand_params == S::rand_params && d.cmask == S::cmask && d.clipmask == S::clipmask &&
+         d.wrapmask == S::wrapmask && d.dotmask == S::dotmask &&
          d.elevon == S::elevon && d.trig_alpha == S::trig_alpha && d.trig_beta == S::trig_beta &&
          d.euler_exact == S::euler_exact && d.obs_general == S::obs_general;
 }
@@ -1282,11 +1339,13 @@ int upload_cfg(fw_handle* h) {
   if (h->precision == FW_F64) {
     DevCfg<double> d;
     fill_devcfg(h, d);
+    h->rand_active = d.rand_params;
     h->spec = spec_of(d);
     FW_HIP(hipMemcpy(h->dcfg, &d, sizeof(d), hipMemcpyHostToDevice));
   } else {
     DevCfg<float> d;
     fill_devcfg(h, d);
+    h->rand_active = d.rand_params;
     h->spec = spec_of(d);
     FW_HIP(hipMemcpy(h->dcfg, &d, sizeof(d), hipMemcpyHostToDevice));
   }
@@ -1297,7 +1356,9 @@ int upload_cfg(fw_handle* h) {
 #define FW_LAUNCH_SPEC(KERNEL, T, h, st, ...)                                                                     \
   do {                                                                                                           \
     const dim3 g_(grid_of(h)), b_(BLOCK);                                                                        \
-    if ((h)->spec == 1)                                                                                          \
+    if ((h)->rand_active)                                                                                        \
+      hipLaunchKernelGGL((KERNEL<T, DevCfg<T>, true>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);  \
+    else if ((h)->spec == 1)                                                                                     \
       hipLaunchKernelGGL((KERNEL<T, GymX8Cfg<T>>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);      \
     else if ((h)->spec == 2)                                                                                     \
       hipLaunchKernelGGL((KERNEL<T, PyflyX8Cfg<T>>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);    \
@@ -1332,6 +1393,7 @@ State<T> state_of(const fw_handle* h) {
   s.met_out = (T*)h->met_out;
   s.obs_init = h->obs_hist ? (T*)(b + h->o_obs_init) : nullptr;
   s.obs_ring = h->obs_hist ? (T*)(b + h->o_obs_ring) : nullptr;
+  s.prm = h->o_prm ? (T*)(b + h->o_prm) : nullptr;
   return s;
 }
 
@@ -1406,6 +1468,9 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
   if (h->metrics) {
     h->o_met = off; off += (size_t)MT_ROWS * row;
     h->o_metu = off; off += (size_t)MU_ROWS * row32;
+  }
+  if (env && env->n_rand > 0) {  // per-aircraft parameters (simulator parameter randomisation)
+    h->o_prm = off; off += (size_t)FW_NPARAM * row;
   }
   if (env && env->obs_length > 1) {  // observation history: first row of the episode + ring of past rows
     const int step = env->obs_step > 1 ? env->obs_step : 1;
@@ -1493,6 +1558,8 @@ int fw_update_config(fw_handle* h, const fw_sim_config* sim, const fw_env_config
       return set_err(FW_E_UNSUPPORTED, "config update may not change observation layout or window sizes");
     if (env->metrics && !h->metrics)
       return set_err(FW_E_UNSUPPORTED, "episode metrics must be enabled when the handle is created");
+    if (env->n_rand > 0 && !h->o_prm)
+      return set_err(FW_E_UNSUPPORTED, "parameter randomisation must be enabled when the handle is created");
     h->env = *env;
   }
   h->sim = *sim;
@@ -1597,6 +1664,9 @@ static int block_info(const fw_handle* h, int32_t block, size_t* off, int* rows,
     case FW_BLK_WIND: *off = h->o_wind; *rows = 3; *esz = T_; return FW_OK;
     case FW_BLK_STEPS: *off = h->o_steps; *rows = 1; *esz = 4; return FW_OK;
     case FW_BLK_COMMAND: *off = h->o_cmd; *rows = 3; *esz = T_; return FW_OK;
+    case FW_BLK_PARAMS:
+      if (!h->o_prm) return set_err(FW_E_INVALID, "handle has no per-aircraft parameters (env n_rand = 0)");
+      *off = h->o_prm; *rows = FW_NPARAM; *esz = T_; return FW_OK;
     default: return set_err(FW_E_INVALID, "unknown state block");
   }
 }

@@ -187,7 +187,7 @@ class Engine:
 
     # ------------------------------------------------------------------
     _ROWS = {C.FW_BLK_ODE: C.FW_NY, C.FW_BLK_DERIVED: 8, C.FW_BLK_TARGET: 3, C.FW_BLK_WIND: 3, C.FW_BLK_STEPS: 1,
-             C.FW_BLK_COMMAND: 3}
+             C.FW_BLK_COMMAND: 3, C.FW_BLK_PARAMS: C.FW_NPARAM}
 
     def get_block(self, blk):
         rows = self._ROWS[blk]
