@@ -27,6 +27,7 @@ Fixtures (all float64 unless noted):
   pyfly_energy.npz        energy states along PID / constraint-terminated trajectories
   env_curriculum.npz      set_curriculum_level ranges/constraints/targets and sampled resets
   env_rand_params.npz     simulator parameter randomisation: sampled parameters and episodes flown with them
+  env_history.npz         FixedWingAircraft.history of a PID episode and of a constraint-terminated one
 """
 import hashlib
 import json
@@ -967,9 +968,41 @@ def gen_rand_params():
             name, len(draws), [len(out["%s__ep%d__rew" % (name, e)]) for e in range(3)]))
     np.savez_compressed(os.path.join(OUT, "env_rand_params.npz"), **out)
 
+
+# ---------------------------------------------------------------------------
+# M. FixedWingAircraft.history (fixed_wing.py:455-467, 491-585)
+# ---------------------------------------------------------------------------
+
+
+def gen_history():
+    out = {}
+    for name, policy, omega, ckw in [("pid", "pid", 60.0, {"action": {"scale_space": False}}),
+                                     ("rand_fail", "rand", 700.0, None)]:
+        env = make_env(False, steps_max=300, config_kw=ckw)
+        for seed in range(5, 200):  # rand_fail: the first seed whose episode ends in a constraint violation
+            rng = np.random.RandomState(seed)
+            res = env_episode(env, rng, False, 300, policy=policy, omega_deg=omega)
+            if name != "rand_fail" or (str(res["term"][-1]) not in ("steps", "") and len(res["rew"]) >= 20):
+                break
+        h = env.history
+        for k, v in res.items():
+            out[name + "__" + k] = v
+        out[name + "__h_action"] = np.array(h["action"], dtype=np.float64)
+        out[name + "__h_reward"] = np.array(h["reward"], dtype=np.float64)
+        out[name + "__h_observation"] = np.array(h["observation"], dtype=np.float64)
+        for t in ("roll", "pitch", "Va"):
+            out[name + "__h_target_" + t] = np.array(h["target"][t], dtype=np.float64)
+            out[name + "__h_error_" + t] = np.array(h["error"][t], dtype=np.float64)
+        for g in h.get("goal", {}):
+            out[name + "__h_goal_" + g] = np.array(h["goal"][g], dtype=bool)
+        out[name + "__goal_keys"] = np.array(sorted(h.get("goal", {})))
+        print("history %s: %d actions, %d rewards, last term %r" % (name, len(h["action"]), len(h["reward"]),
+                                                                   str(res["term"][-1])))
+    np.savez_compressed(os.path.join(OUT, "env_history.npz"), **out)
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["single", "traj", "envelope", "dryden", "env", "pidset", "metrics", "obshist",
-                             "solverfail", "energy", "curriculum", "randparams"]
+                             "solverfail", "energy", "curriculum", "randparams", "history"]
     if "envelope" in which and "traj" not in which:
         gen_envelope()
     if "obshist" in which:
@@ -996,3 +1029,5 @@ if __name__ == "__main__":
         gen_curriculum()
     if "randparams" in which:
         gen_rand_params()
+    if "history" in which:
+        gen_history()

@@ -539,3 +539,91 @@ def test_device_flies_reference_sampled_parameters(name, precision, tmpdir):
                 assert np.all(np.abs(ref_o - g(ep, "obs")[s + 1]) <= 2e-3 * (1 + np.abs(g(ep, "obs")[s + 1])))
             assert bool(dn[ep]) == bool(g(ep, "done")[s]), (ep, s)
     eng.close()
+
+
+# ---------------------------------------------------------------------------- FixedWingAircraft.history
+def _check_history(h, d, name, tol_obs=1e-5):
+    g = lambda k: d[name + "__" + k]  # noqa: E731
+    assert len(h["action"]) == len(g("h_action")) and len(h["reward"]) == len(g("h_reward"))
+    assert len(h["observation"]) == len(g("h_observation"))
+    np.testing.assert_allclose(np.array(h["action"], dtype=np.float64), g("h_action"), rtol=0, atol=1e-7)
+    np.testing.assert_allclose(h["reward"], g("h_reward"), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(np.array(h["observation"], dtype=np.float64), g("h_observation"), rtol=1e-5,
+                               atol=tol_obs)
+    for t in ("roll", "pitch", "Va"):
+        np.testing.assert_allclose(h["target"][t], g("h_target_" + t), rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(h["error"][t], g("h_error_" + t), rtol=1e-5, atol=1e-5)
+    keys = [str(k) for k in g("goal_keys")]
+    assert sorted(h.get("goal", {})) == keys
+    for k in keys:
+        got, want = np.array(h["goal"][k]), g("h_goal_" + k)
+        assert len(got) == len(want) and (got == want).mean() >= 0.99, k  # a bound crossing may flip in the last digit
+
+
+@pytest.mark.parametrize("name", ["pid", "rand_fail"])
+def test_facade_history_matches_reference(name):
+    """FixedWingAircraft.history of the facade (fp64) == the reference's for a PID episode and for one that
+    ends in a constraint violation (the failed step appends its action only)."""
+    from _pid import PID
+    from tum_adlr_deep_reinforcement_learning_amd.fixed_wing import FixedWingAircraft
+    d = F.load("env_history.npz")
+    g = lambda k: d[name + "__" + k]  # noqa: E731
+    ckw = {"steps_max": 300}
+    if name == "pid":
+        ckw["action"] = {"scale_space": False}
+    env = FixedWingAircraft(config_kw=ckw, sim_config_kw={"turbulence": False}, device=DEV, precision="float64")
+    init = F.env_init(g("init"))
+    st = {k: float(init[j]) for j, k in enumerate(["roll", "pitch", "yaw", "omega_p", "omega_q", "omega_r",
+                                                   "position_n", "position_e", "position_d", "velocity_u",
+                                                   "velocity_v", "velocity_w"])}
+    st["wind"] = list(init[C.FW_I_WIND_N:C.FW_I_WIND_D + 1])
+    for j, a in enumerate(("elevon_right", "elevon_left", "throttle")):
+        st[a] = float(init[C.FW_I_ACT0 + 2 * j])
+    t0 = g("target0")
+    env.reset(state=st, target={"roll": t0[0], "pitch": t0[1], "Va": t0[2]})
+    for a in g("act"):
+        _, _, done, _ = env.step(a)
+        if done:
+            break
+    _check_history(env.history, d, name)
+    env.close()
+
+
+def test_vecenv_record_history_matches_reference():
+    """FixedWingVecEnv(record_history=True).get_attr("history"): the same per-env histories, with the
+    episode of a done env recorded up to its last step before the auto-reset restarts it."""
+    from tum_adlr_deep_reinforcement_learning_amd.vec_env import FixedWingVecEnv
+    d = F.load("env_history.npz")
+    name = "rand_fail"
+    g = lambda k: d[name + "__" + k]  # noqa: E731
+    env = FixedWingVecEnv(2, config_kw={"steps_max": 300}, sim_config_kw={"turbulence": False}, device=DEV,
+                          precision="float64", record_history=True)
+    env.reset()
+    init = np.stack([F.env_init(g("init"))] * 2, axis=1)
+    tgt = np.stack([g("target0")] * 2, axis=1)
+    env.engine.reset(init=init, target=tgt)  # both envs replay the fixture episode
+    o = env.engine.obs.cpu().numpy()
+    t, v = env._targets_vals()
+    for i in range(2):
+        env._hists[i].reset(o[i], t[:, i], v[:, i])
+    env._tgt = t
+    import copy
+    prev = None
+    for a in g("act"):
+        _, _, done, _ = env.step(np.stack([a, a]).astype(np.float32))
+        if done[0]:
+            break
+        prev = copy.deepcopy(env.get_attr("history", indices=[0])[0])
+    # up to the step before the failure the recorder holds the reference's history prefix
+    n = len(prev["action"])
+    assert n == len(g("h_action")) - 1
+    np.testing.assert_allclose(np.array(prev["action"], dtype=np.float64), g("h_action")[:n], atol=1e-7)
+    np.testing.assert_allclose(prev["reward"], g("h_reward")[:n], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(np.array(prev["observation"]), g("h_observation")[:n + 1], rtol=1e-5, atol=1e-5)
+    for t in ("roll", "pitch", "Va"):
+        np.testing.assert_allclose(prev["target"][t], g("h_target_" + t)[:n + 1], rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(prev["error"][t], g("h_error_" + t)[:n + 1], rtol=1e-5, atol=1e-5)
+    # the failed last step ends the episode; the auto-reset restarts the history (as env.reset() does)
+    h = env.get_attr("history", indices=[0])[0]
+    assert len(h["action"]) == 0 and len(h["observation"]) == 1
+    env.close()

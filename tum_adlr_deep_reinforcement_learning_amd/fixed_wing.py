@@ -11,6 +11,7 @@ import torch
 
 from . import config as C
 from .engine import Engine
+from .history import EpisodeHistory, step_succeeded
 from .pyfly import SimulatorView
 from .spaces import Box
 from .vec_env import metric_info, termination_name
@@ -30,7 +31,18 @@ class FixedWingAircraft:
         self.steps_max = self.spec.steps_max
         self.training = True
         self._act = torch.zeros(1, 3, dtype=self.engine.dtype, device=self.engine.device)
+        self._hist = EpisodeHistory(self.spec)
         self.seed(None)
+
+    @property
+    def history(self):
+        """FixedWingAircraft.history (fixed_wing.py:455-467, 491-585), recorded on the host."""
+        return self._hist.history
+
+    def _targets_vals(self):
+        t = self.engine.get_block(C.FW_BLK_TARGET)[:, 0].double().cpu().numpy()
+        d = self.engine.get_block(C.FW_BLK_DERIVED)[:, 0].double().cpu().numpy()
+        return t, d[[0, 1, 3]]
 
     def seed(self, seed=None):
         """FixedWingAircraft.seed (fixed_wing.py:324-332) -> Philox stream (seed, 0)."""
@@ -63,7 +75,11 @@ class FixedWingAircraft:
             for k, v in target.items():
                 tgt[C.TARGET_INDEX[k], 0] = v
         obs = self.engine.reset(init=init, target=tgt)
-        return obs[0].cpu().numpy().astype(np.float32).reshape(self.spec.obs_shape)
+        o = obs[0].cpu().numpy().astype(np.float32).reshape(self.spec.obs_shape)
+        t, v = self._targets_vals()
+        self._hist.reset(o, t, v)
+        self._tgt = t
+        return o
 
     def step(self, action):
         a = np.asarray(action, dtype=np.float64).reshape(1, 3)
@@ -71,14 +87,19 @@ class FixedWingAircraft:
         self._act.copy_(torch.as_tensor(a))
         obs, rew, done, term = self.engine.env_step(self._act, auto_reset=False, terminal_obs=False, episode=False)
         d = bool(done[0].item())
+        t, v = self._targets_vals()
+        o = obs[0].cpu().numpy().astype(np.float32).reshape(self.spec.obs_shape)
+        self._hist.step(np.asarray(action).reshape(-1), step_succeeded(term[0].item()), o, float(rew[0].item()),
+                        self._tgt, t, v)
+        self._tgt = t
         info = {}
         if d:
             info["termination"] = termination_name(term[0].item(), tuple(self.spec.sim.dynamics))
             if self.engine.metrics is not None:
                 info.update(metric_info(self.engine.metrics[:, 0].cpu().numpy(),
                                         [m["name"] for m in self.cfg.get("metrics", [])]))
-        info["target"] = self.target
-        return obs[0].cpu().numpy().astype(np.float32).reshape(self.spec.obs_shape), float(rew[0].item()), d, info
+        info["target"] = {"roll": float(t[0]), "pitch": float(t[1]), "Va": float(t[2])}
+        return o, float(rew[0].item()), d, info
 
     def render(self, mode="plot", **kw):
         raise NotImplementedError("rendering is host-side plotting; out of scope for the device engine")

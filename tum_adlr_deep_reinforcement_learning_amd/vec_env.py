@@ -149,7 +149,7 @@ class FixedWingVecEnv(VecEnv):
 
     def __init__(self, num_envs=1, config_path=None, config_kw=None, sim_config_path=None, sim_parameter_path=None,
                  sim_config_kw=None, device=None, precision="float32", seed=None, return_tensors=False,
-                 info_target=True, curriculum_level=1, env_offset=0):
+                 info_target=True, curriculum_level=1, env_offset=0, record_history=False):
         self.spec = C.EnvSpec(config_path, config_kw, sim_config_path, sim_parameter_path, sim_config_kw,
                               curriculum_level=curriculum_level)
         obs_space = Box(self.spec.obs_low, self.spec.obs_high, dtype=np.float32)
@@ -166,6 +166,12 @@ class FixedWingVecEnv(VecEnv):
         self._dyn = tuple(self.spec.sim.dynamics)
         self.seed(seed if seed is not None else 0)
         self._reset_pending = True
+        # per-env FixedWingAircraft.history on the host (get_attr("history")): pulls every step's data
+        # to the host, meant for evaluation with few envs
+        self._hists = None
+        if record_history:
+            from .history import EpisodeHistory
+            self._hists = [EpisodeHistory(self.spec) for _ in range(self.num_envs)]
 
     @property
     def cfg(self):
@@ -182,7 +188,42 @@ class FixedWingVecEnv(VecEnv):
     def reset(self):
         obs = self.engine.reset()
         self._reset_pending = False
+        if self._hists is not None:
+            o = obs.cpu().numpy().astype(np.float32)
+            t, v = self._targets_vals()
+            for i, h in enumerate(self._hists):
+                h.reset(self._shaped(o[i:i + 1])[0], t[:, i], v[:, i])
+            self._tgt = t
         return self._out(obs)
+
+    def _targets_vals(self):
+        t = self.engine.get_block(C.FW_BLK_TARGET).double().cpu().numpy()
+        d = self.engine.get_block(C.FW_BLK_DERIVED).double().cpu().numpy()
+        return t, d[[0, 1, 3]]
+
+    def _step_recording(self, actions):
+        """env step with the history recorder: step without auto-reset, record every env's step from its
+        post-step state, then reset the done envs (what the SubprocVecEnv worker does, subproc_vec_env.py:
+        25-31) and restart their histories with the reset observation."""
+        from .history import step_succeeded
+        eng = self.engine
+        obs, rew, done, term = eng.env_step(actions, auto_reset=False)
+        dn = done.cpu().numpy().astype(bool)
+        tm, r = term.cpu().numpy(), rew.double().cpu().numpy()
+        o = self._shaped(obs.cpu().numpy().astype(np.float32))
+        to = self._shaped(eng.terminal_obs.cpu().numpy().astype(np.float32))
+        t, v = self._targets_vals()
+        a = actions.double().cpu().numpy()
+        for i, h in enumerate(self._hists):
+            h.step(a[i], step_succeeded(tm[i]), to[i] if dn[i] else o[i], r[i], self._tgt[:, i], t[:, i], v[:, i])
+        if dn.any():
+            obs = eng.reset(mask=dn)
+            o = self._shaped(obs.cpu().numpy().astype(np.float32))
+            t, v = self._targets_vals()
+            for i in np.nonzero(dn)[0]:
+                self._hists[i].reset(o[i], t[:, i], v[:, i])
+        self._tgt = t
+        return obs, rew, done, term
 
     def step_async(self, actions):
         if isinstance(actions, torch.Tensor):
@@ -195,7 +236,10 @@ class FixedWingVecEnv(VecEnv):
         if self._actions is None:
             raise RuntimeError("step_wait() without step_async()")
         eng = self.engine
-        obs, rew, done, term = eng.env_step(self._actions, auto_reset=True)
+        if self._hists is not None:
+            obs, rew, done, term = self._step_recording(self._actions)
+        else:
+            obs, rew, done, term = eng.env_step(self._actions, auto_reset=True)
         self._actions = None
         if self.return_tensors:
             return self._shaped(obs), rew, done.bool(), self._infos_lazy_device()
@@ -267,6 +311,10 @@ class FixedWingVecEnv(VecEnv):
                    "action_space": self.action_space, "training": self.training,
                    "steps_max": self.spec.steps_max}[attr_name]
             return [val for _ in idx]
+        if attr_name == "history":
+            if self._hists is None:
+                raise AttributeError("history is recorded on the host only with FixedWingVecEnv(record_history=True)")
+            return [self._hists[i].history for i in idx]
         if attr_name == "steps_count":
             s, _ = self.engine.steps()
             s = s.cpu().numpy()
