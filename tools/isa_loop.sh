@@ -7,7 +7,7 @@ W=$(mktemp -d)
 cd "$W"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-slp-vectorize --save-temps "$@" -c "$SRC" -o k.o 2>/dev/null
 S=$(ls *gfx950.s)
-awk -v pat="${KPAT:-k_env_stepIfN2fw7SpecCfgIfLj4152}" '$0 ~ "^_ZN12_GLOBAL__N_1[0-9]+" pat && /:/ {f=1} f&&/s_endpgm/{print; f=0} f' "$S" > env.s
+awk -v pat="${KPAT:-k_env_stepIfN2fw8GymX8CfgIfEELb0}" '$0 ~ "^_ZN12_GLOBAL__N_1[0-9]+" pat && /:/ {f=1} f&&/s_endpgm/{print; f=0} f' "$S" > env.s
 grep -E "^\s+\.(vgpr_count|sgpr_count|vgpr_spill_count|sgpr_spill_count|private_segment_fixed_size):" "$S" | tail -5 | tr -s ' ' | tr '\n' ' '
 echo
 # the RK loop = the depth-1 loop with the largest body

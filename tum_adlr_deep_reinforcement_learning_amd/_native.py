@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(LIB_DIR, "libfwsim.so")
 HEADER = os.path.join(ROOT, "include", "fwsim.h")
 HEADERS = [HEADER, os.path.join(ROOT, "include", "fwrollout.h")]
 UNITS = [os.path.join(CSRC, "fw_kernels.hip"), os.path.join(CSRC, "fw_rollout.hip")]
-SOURCES = UNITS + [os.path.join(CSRC, "fw_device.hpp")] + HEADERS
+SOURCES = UNITS + [os.path.join(CSRC, "fw_device.hpp"), os.path.join(CSRC, "fw_x8_consts.inc")] + HEADERS
 ARCH = os.environ.get("FWSIM_ARCH", "gfx950")
 
 _lib = None

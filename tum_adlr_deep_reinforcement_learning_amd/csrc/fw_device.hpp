@@ -134,15 +134,67 @@ struct SpecCfg : DevCfg<T> {
   static constexpr uint32_t cmask = CM, clipmask = CLM, wrapmask = WM, dotmask = DM;
   static constexpr int elevon = ELEVON, trig_alpha = TA, trig_beta = TB, euler_exact = EE;
   static constexpr int obs_general = 0;  // specialisations serve plain length-1, noise-free observations
+  static constexpr int const_limits = 0;  // limit values compile-time constants too (see GymX8Cfg)
+  static constexpr int const_params = 0;  // airframe constants compile-time too
   static constexpr int rand_params = 0;  // ... with one parameter set for all aircraft
 };
+// The limit VALUES of the two shipped configurations as compile-time constants as well (the host
+// selects a specialisation only if every runtime value equals these bit for bit): the conditions then
+// compare against immediates instead of ~20 config scalars that do not fit the SGPR budget next to
+// the rest of the loop (they were spilled to VGPR lanes and re-read every RHS, v_readlane).
+#ifndef FW_CONST_CFG
+#define FW_CONST_CFG 2  // 0: runtime values only; 1: + limit values; 2: + airframe constants (fw_x8_consts.inc)
+#endif
+#include "fw_x8_consts.inc"
+#define FW_X8_MEMBER(name, val) static constexpr T name = (T)(val);
+#define FW_INF_ __builtin_inf()
+#define FW_X8_LIMS(OM, VACMAX)                                                                          \
+  {{(T)-FW_INF_, (T)FW_INF_, (T)-FW_INF_, (T)FW_INF_}, {(T)-FW_INF_, (T)FW_INF_, (T)-FW_INF_, (T)FW_INF_}, \
+   {(T)-FW_INF_, (T)FW_INF_, (T)-FW_INF_, (T)FW_INF_}, {(T)-FW_INF_, (T)FW_INF_, (T)-(OM), (T)(OM)},          \
+   {(T)-FW_INF_, (T)FW_INF_, (T)-(OM), (T)(OM)},       {(T)-FW_INF_, (T)FW_INF_, (T)-(OM), (T)(OM)},          \
+   {(T)-FW_INF_, (T)FW_INF_, (T)-FW_INF_, (T)FW_INF_}, {(T)-FW_INF_, (T)FW_INF_, (T)-FW_INF_, (T)FW_INF_}, \
+   {(T)-FW_INF_, (T)FW_INF_, (T)-FW_INF_, (T)FW_INF_}, {(T)-FW_INF_, (T)FW_INF_, (T)-FW_INF_, (T)FW_INF_}, \
+   {(T)-FW_INF_, (T)FW_INF_, (T)-FW_INF_, (T)FW_INF_}, {(T)-FW_INF_, (T)FW_INF_, (T)-FW_INF_, (T)FW_INF_}, \
+   {(T)0x1.0c6f7a0b5ed8dp-20, (T)FW_INF_, (T)-FW_INF_, (T)(VACMAX)},                                       \
+   {(T)-FW_INF_, (T)FW_INF_, (T)-FW_INF_, (T)FW_INF_}, {(T)-FW_INF_, (T)FW_INF_, (T)-FW_INF_, (T)FW_INF_}, \
+   {(T)-0x1.0c152382d7365p-1, (T)0x1.38c35418a5bf6p-1, (T)-FW_INF_, (T)FW_INF_},                           \
+   {(T)-0x1.0c152382d7365p-1, (T)0x1.38c35418a5bf6p-1, (T)-FW_INF_, (T)FW_INF_},                           \
+   {(T)0.0, (T)1.0, (T)-FW_INF_, (T)FW_INF_},                                                               \
+   {(T)-0x1.0c152382d7365p-1, (T)0x1.38c35418a5bf6p-1, (T)-FW_INF_, (T)FW_INF_},                           \
+   {(T)-0x1.226c3bcdbe7aep-1, (T)0x1.226c3bcdbe7aep-1, (T)-FW_INF_, (T)FW_INF_},                           \
+   {(T)0.0, (T)1.0, (T)-FW_INF_, (T)FW_INF_}}
 // fixed_wing_config.json (gym): omega +-720 deg/s and Va <= 70 constrained; Va, actuators,
-// elevator / aileron / throttle clipped; roll / yaw wrapped; elevon rate limits
+// elevator / aileron / throttle clipped; roll / yaw wrapped; elevon rate limits 200 deg/s
 template <typename T>
-using GymX8Cfg = SpecCfg<T, 0x1038u, 0x1F9000u, 0x5u, 0x3u, 1, 0, 0, 0>;
-// pyfly_config.json: as above without the Va constraint
+struct GymX8Cfg : SpecCfg<T, 0x1038u, 0x1F9000u, 0x5u, 0x3u, 1, 0, 0, 0> {
+#if FW_CONST_CFG >= 1
+  static constexpr int const_limits = 1;
+  static constexpr Lim<T> lim[FW_NVAR] = FW_X8_LIMS(0x1.921fb54442d18p+3, 0x1.1800000000000p+6);
+  static constexpr T dot_max[3] = {(T)0x1.becf41f212d77p+1, (T)0x1.becf41f212d77p+1, (T)FW_INF_};
+#endif
+#if FW_CONST_CFG >= 2
+  static constexpr int const_params = 1;
+  FW_X8_SCALARS(FW_X8_MEMBER)
+  static constexpr T gam[9] = FW_X8_GAM;
+  static constexpr T ac[3][6] = FW_X8_AC;
+#endif
+};
+// pyfly_config.json: omega +-180 deg/s, no Va constraint, otherwise as above
 template <typename T>
-using PyflyX8Cfg = SpecCfg<T, 0x38u, 0x1F9000u, 0x5u, 0x3u, 1, 0, 0, 0>;
+struct PyflyX8Cfg : SpecCfg<T, 0x38u, 0x1F9000u, 0x5u, 0x3u, 1, 0, 0, 0> {
+#if FW_CONST_CFG >= 1
+  static constexpr int const_limits = 1;
+  static constexpr Lim<T> lim[FW_NVAR] = FW_X8_LIMS(0x1.921fb54442d18p+1, FW_INF_);
+  static constexpr T dot_max[3] = {(T)0x1.becf41f212d77p+1, (T)0x1.becf41f212d77p+1, (T)FW_INF_};
+#endif
+#if FW_CONST_CFG >= 2
+  static constexpr int const_params = 1;
+  FW_X8_SCALARS(FW_X8_MEMBER)
+  static constexpr T gam[9] = FW_X8_GAM;
+  static constexpr T ac[3][6] = FW_X8_AC;
+#endif
+};
+#undef FW_X8_LIMS
 
 // Re-materialise the (wave-uniform) config pointer so the scalar loads of the
 // ~90 aircraft constants are issued where they are used instead of being

@@ -1320,7 +1320,31 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // Which compiled structural specialisation (fw_device.hpp SpecCfg) matches this config.
 template <typename S, typename T>
+bool same_limits(const DevCfg<T>& d) {
+  if constexpr (S::const_limits) {
+    for (int v = 0; v < FW_NVAR; v++)
+      if (std::memcmp(&d.lim[v], &S::lim[v], sizeof(Lim<T>)) != 0) return false;
+    if (std::memcmp(d.dot_max, S::dot_max, sizeof(d.dot_max)) != 0) return false;
+  }
+  return true;
+}
+
+template <typename S, typename T>
+bool same_params(const DevCfg<T>& d) {
+  if constexpr (S::const_params) {
+#define FW_X8_CMP(name, val) \
+  if (std::memcmp(&d.name, &S::name, sizeof(T)) != 0) return false;
+    FW_X8_SCALARS(FW_X8_CMP)
+#undef FW_X8_CMP
+    if (std::memcmp(d.gam, S::gam, sizeof(d.gam)) != 0) return false;
+    if (std::memcmp(d.ac, S::ac, sizeof(d.ac)) != 0) return false;
+  }
+  return true;
+}
+
+template <typename S, typename T>
 bool same_structure(const DevCfg<T>& d) {
+  if (!same_limits<S>(d) || !same_params<S>(d)) return false;
   return d.rand_params == S::rand_params && d.cmask == S::cmask && d.clipmask == S::clipmask &&
          d.wrapmask == S::wrapmask && d.dotmask == S::dotmask &&
          d.elevon == S::elevon && d.trig_alpha == S::trig_alpha && d.trig_beta == S::trig_beta &&
@@ -1352,19 +1376,21 @@ int upload_cfg(fw_handle* h) {
   return FW_OK;
 }
 
-// launch KERNEL<T, C> with C chosen by the handle's structural specialisation
-#define FW_LAUNCH_SPEC(KERNEL, T, h, st, ...)                                                                     \
+// launch KERNEL<T, C> with C chosen by the handle's structural specialisation (G / P: the gym / pyfly
+// X8 view types of this kernel)
+#define FW_LAUNCH_SPEC_AS(KERNEL, G, P, T, h, st, ...)                                                          \
   do {                                                                                                           \
     const dim3 g_(grid_of(h)), b_(BLOCK);                                                                        \
     if ((h)->rand_active)                                                                                        \
       hipLaunchKernelGGL((KERNEL<T, DevCfg<T>, true>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);  \
     else if ((h)->spec == 1)                                                                                     \
-      hipLaunchKernelGGL((KERNEL<T, GymX8Cfg<T>>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);      \
+      hipLaunchKernelGGL((KERNEL<T, G<T>>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);             \
     else if ((h)->spec == 2)                                                                                     \
-      hipLaunchKernelGGL((KERNEL<T, PyflyX8Cfg<T>>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);    \
+      hipLaunchKernelGGL((KERNEL<T, P<T>>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);             \
     else                                                                                                         \
       hipLaunchKernelGGL((KERNEL<T, DevCfg<T>>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);        \
   } while (0)
+#define FW_LAUNCH_SPEC(KERNEL, T, h, st, ...) FW_LAUNCH_SPEC_AS(KERNEL, GymX8Cfg, PyflyX8Cfg, T, h, st, __VA_ARGS__)
 
 template <typename T>
 State<T> state_of(const fw_handle* h) {
