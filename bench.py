@@ -322,12 +322,22 @@ def timed_env_steps(n, args, spec, dev, rank, world, env_offset, early=True):
     # k_env_step device duration per launch: HIP events on the launch stream around the timed steps
     # themselves (graph replays keep the queue full, so this is kernel time plus dispatch gaps)
     kern_ms = ev0.elapsed_time(ev1) / args.steps
-    el = torch.tensor([elapsed, kern_ms, early_ms or 0.0], dtype=torch.float64, device=dev)
+    # the same population over a long window: rare extreme stragglers (an aircraft needing thousands of
+    # RHS evaluations in one step) make a short window's mean depend on luck
+    long_ms = 0.0
+    if args.long_window > 0:
+        l0, l1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        l0.record(stream)
+        run(args.long_window)
+        l1.record(stream)
+        torch.cuda.synchronize(dev)
+        long_ms = l0.elapsed_time(l1) / args.long_window
+    el = torch.tensor([elapsed, kern_ms, early_ms or 0.0, long_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     eng.close()
     del graph
-    return float(el[0]), float(el[1]), (float(el[2]) if early else None)
+    return float(el[0]), float(el[1]), (float(el[2]) if early else None), float(el[3])
 
 
 def open_loop_leg(n, args, spec, dev, rank, world, env_offset, K=256, launches=4):
@@ -382,6 +392,8 @@ def main():
                     help="do not track the config's streaming episode metrics (fixed_wing.py:1644-1736)")
     ap.add_argument("--no-weak", action="store_true", help="skip the weak-scaling line (65536 aircraft per GPU)")
     ap.add_argument("--no-open-loop", action="store_true", help="skip the open-loop rollout line (fw_env_rollout)")
+    ap.add_argument("--long-window", type=int, default=1000,
+                    help="after the timed steps, time this many more for the long-window steady-state line")
     ap.add_argument("--rollout-steps", type=int, default=0,
                     help="also run one PPO collect_rollouts of this horizon (2048 = BASELINE configs[2]/[3])")
     ap.add_argument("--sac-fill-steps", type=int, default=0,
@@ -413,13 +425,13 @@ def main():
     spec = C.EnvSpec(sim_config_kw={"turbulence": bool(args.turbulence), "turbulence_intensity": "light"})
     spec.metrics_enabled = not args.no_metrics
     n = args.envs // world  # strong scaling: the global batch is split over the GPUs
-    elapsed, kern_ms, early_ms = timed_env_steps(n, args, spec, dev, rank, world, rank * n)
+    elapsed, kern_ms, early_ms, long_ms = timed_env_steps(n, args, spec, dev, rank, world, rank * n)
     value = args.envs * args.steps / elapsed
 
     weak = None
     if world > 1 and not args.no_weak:  # secondary: 65536 aircraft per GPU
         nw = 65536
-        w_el, w_k, _ = timed_env_steps(nw, args, spec, dev, rank, world, rank * nw, early=False)
+        w_el, w_k, _, _ = timed_env_steps(nw, args, spec, dev, rank, world, rank * nw, early=False)
         weak = {"envs_per_gpu": nw, "global_envs": nw * world, "value": nw * world * args.steps / w_el,
                 "ms_per_step": w_el / args.steps * 1e3, "kernel_ms": w_k}
 
@@ -475,6 +487,8 @@ def main():
                          "binding_limit": "valu issue + RK45 straggler latency (see roofline_valu, DESIGN.md 3)"},
             "roofline_valu": roof_valu,
             "early_regime": {"steps": 96, "kernel_ms": early_ms, "env_steps_per_s_per_gpu": n / (early_ms * 1e-3)},
+            "long_window": ({"steps": args.long_window, "kernel_ms": long_ms,
+                             "env_steps_per_s": args.envs / (long_ms * 1e-3)} if long_ms > 0 else None),
             "cpu_baseline": cpu,
             "cpu_baseline_reference": REFERENCE_CPU,
         }
