@@ -7,7 +7,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out/traffic tools/_build
 export TMPDIR=/tmp
-BENCH_ARGS=${BENCH_ARGS:-"--steps 200 --warmup 16 --no-cpu-baseline"}
+BENCH_ARGS=${BENCH_ARGS:-"--steps 200 --warmup 16 --no-cpu-baseline --long-window 0 --no-open-loop"}
 step() { local name=$1 to=$2; shift 2; timeout -k 10 "$to" "$@" > "gpurun_out/traffic/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"; tail -3 "gpurun_out/traffic/$name.log"; [ $rc -eq 0 ] || exit $rc; }
 [ -x tools/_build/fetch_calib ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o tools/_build/fetch_calib tools/fetch_calib.hip || exit 3
 step calib_fetch 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/traffic/calib_fetch -- tools/_build/fetch_calib
