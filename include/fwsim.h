@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FWSIM_ABI_VERSION 4
+#define FWSIM_ABI_VERSION 5
 
 /* ---- error codes ---------------------------------------------------------- */
 #define FW_OK 0
@@ -320,6 +320,16 @@ int fw_env_step(fw_handle* h, const void* actions_dev, void* obs_dev, void* rewa
 int fw_env_rollout(fw_handle* h, int32_t n_steps, const void* actions_dev, void* obs_dev, void* reward_dev,
                    uint8_t* done_dev, int32_t* term_dev, void* terminal_obs_dev, void* episode_dev, int32_t* stats_dev,
                    int32_t auto_reset, void* stream);
+
+/* Lanes per aircraft of fw_env_step / fw_sim_step (an execution choice, no reference counterpart):
+ * 1 = one lane integrates one aircraft; 4 = a lane quad integrates it (the RHS split by rows,
+ * DESIGN.md 3.3): lower latency per aircraft, for shards of few aircraft and the RK45 straggler tail.
+ * FW_LANES_AUTO (0, the default) picks by N.  The two agree within rounding, not bit for bit; a config
+ * with a wrapped ODE-state variable always runs 1 (fw_set_lanes(h, 4) fails).  fw_get_lanes returns the
+ * value the next launch uses; fw_env_rollout runs the same, so it still equals fw_env_step launches.   */
+#define FW_LANES_AUTO 0
+int fw_set_lanes(fw_handle* h, int32_t lanes);
+int fw_get_lanes(const fw_handle* h, int32_t* lanes);
 
 /* Observation of the current state (FixedWingAircraft.get_observation). */
 int fw_observe(fw_handle* h, void* obs_dev, void* stream);

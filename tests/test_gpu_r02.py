@@ -419,8 +419,9 @@ def test_partial_collect_bootstraps_at_last_stored_row():
 
 
 # ---------------------------------------------------------------------------- open-loop rollout kernel
+@pytest.mark.parametrize("lanes", [1, 4])
 @pytest.mark.parametrize("precision", ["float64", "float32"])
-def test_env_rollout_equals_env_steps_bitwise(precision):
+def test_env_rollout_equals_env_steps_bitwise(precision, lanes):
     """fw_env_rollout (K steps in one launch) == K fw_env_step launches, bit for bit: observations,
     rewards, dones, terminations, terminal observations, Monitor records and the metric records --
     ragged batch, light Dryden (Philox), short episodes so auto-resets happen inside the launch."""
@@ -428,6 +429,7 @@ def test_env_rollout_equals_env_steps_bitwise(precision):
     n, K = 1000, 70
     a, b = _engine(spec.sim, spec, n, precision), _engine(spec.sim, spec, n, precision)
     for e in (a, b):
+        e.set_lanes(lanes)
         e.seed(21)
         e.reset()
     g = torch.Generator(device=DEV)

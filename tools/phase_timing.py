@@ -30,7 +30,9 @@ pool = torch.rand(16, n, 3, generator=gen, device="cuda:0") * 2 - 1
 for s in range(20):
     eng.env_step(pool[s % 16], stats=True)
 torch.cuda.synchronize()
-waves = (n + 63) // 64
+lanes = eng.lanes  # FWSIM_LANES=1|4 selects the integrator
+per = 64 // lanes  # aircraft per wave
+waves = (n * lanes + 63) // 64
 rows = []
 for s in range(60):
     eng.episode.zero_()
@@ -38,7 +40,7 @@ for s in range(60):
     torch.cuda.synchronize()
     st = eng.episode.view(-1).view(torch.int64)[: waves * 8].view(waves, 8).cpu().numpy().astype(np.float64) * 10.0
     nf = (eng.stats & 0xFFFF).cpu().numpy()
-    wmax = nf[: waves * 64].reshape(waves, 64).max(1) if n % 64 == 0 else None
+    wmax = nf[: waves * per].reshape(waves, per).max(1) if n % per == 0 else None
     t0 = st[:, 0]
     end = np.where(st[:, 4] > 0, st[:, 4], st[:, 5])
     k0 = t0.min()
@@ -53,7 +55,7 @@ for s in range(60):
                                "end_us": (end[slow] - st[slow, 3]) / 1e3,
                                "wave_max_nfev": int(wmax[slow]) if wmax is not None else None}})
 keys = ["span_us", "entry_spread_us", "prologue_us", "sim_us_median", "epilogue_us", "tail_us"]
-print(json.dumps({k: round(float(np.median([r[k] for r in rows])), 2) for k in keys}))
+print(json.dumps(dict({k: round(float(np.median([r[k] for r in rows])), 2) for k in keys}, n=n, lanes=lanes)))
 for r in rows[:6]:
     print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in r["slow_wave"].items()}),
           "span", round(r["span_us"], 1))

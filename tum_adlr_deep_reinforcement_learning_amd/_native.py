@@ -18,11 +18,11 @@ LIB_PATH = os.path.join(LIB_DIR, "libfwsim.so")
 HEADER = os.path.join(ROOT, "include", "fwsim.h")
 HEADERS = [HEADER, os.path.join(ROOT, "include", "fwrollout.h")]
 UNITS = [os.path.join(CSRC, "fw_kernels.hip"), os.path.join(CSRC, "fw_rollout.hip")]
-SOURCES = UNITS + [os.path.join(CSRC, "fw_device.hpp"), os.path.join(CSRC, "fw_x8_consts.inc")] + HEADERS
+SOURCES = UNITS + [os.path.join(CSRC, "fw_device.hpp"), os.path.join(CSRC, "fw_quad.hpp"), os.path.join(CSRC, "fw_x8_consts.inc")] + HEADERS
 ARCH = os.environ.get("FWSIM_ARCH", "gfx950")
 
 _lib = None
-ABI_VERSION = 4  # include/fwsim.h FWSIM_ABI_VERSION
+ABI_VERSION = 5  # include/fwsim.h FWSIM_ABI_VERSION
 
 
 class FwError(RuntimeError):
@@ -97,6 +97,8 @@ SIGNATURES = {
     "fw_sim_step": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "fw_env_step": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
     "fw_env_rollout": (_c.c_int, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
+    "fw_set_lanes": (_c.c_int, [_vp, _i32]),
+    "fw_get_lanes": (_c.c_int, [_vp, _c.POINTER(_i32)]),
     "fw_observe": (_c.c_int, [_vp, _vp, _vp]),
     "fw_get_state": (_c.c_int, [_vp, _i32, _vp, _vp]),
     "fw_set_state": (_c.c_int, [_vp, _i32, _vp, _vp]),

@@ -598,19 +598,23 @@ constexpr int lds_slots() {
   return 2 + FW_ER_LDS + ((sizeof(T) == 4 && FW_P_LDS) ? 4 : 0);
 }
 
+// Dormand-Prince 5(4) tableau (scipy rk.py RK45.A / B / E)
+namespace dp5 {
+constexpr double A10 = 1.0 / 5;
+constexpr double A20 = 3.0 / 40, A21 = 9.0 / 40;
+constexpr double A30 = 44.0 / 45, A31 = -56.0 / 15, A32 = 32.0 / 9;
+constexpr double A40 = 19372.0 / 6561, A41 = -25360.0 / 2187, A42 = 64448.0 / 6561, A43 = -212.0 / 729;
+constexpr double A50 = 9017.0 / 3168, A51 = -355.0 / 33, A52 = 46732.0 / 5247, A53 = 49.0 / 176, A54 = -5103.0 / 18656;
+constexpr double B0 = 35.0 / 384, B2 = 500.0 / 1113, B3 = 125.0 / 192, B4 = -2187.0 / 6784, B5 = 11.0 / 84;
+constexpr double E0 = -71.0 / 57600, E2 = 71.0 / 16695, E3 = -71.0 / 1920, E4 = 17253.0 / 339200, E5 = -22.0 / 525,
+                 E6 = 1.0 / 40;
+}  // namespace dp5
+
 template <typename T, typename C, typename A>
 FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy, V2<T>* __restrict__ sf, int stride,
                int& nfev, int& nacc, V2<T>* __restrict__ se = nullptr) {
   using V = V2<T>;
-  constexpr double A10 = 1.0 / 5;
-  constexpr double A20 = 3.0 / 40, A21 = 9.0 / 40;
-  constexpr double A30 = 44.0 / 45, A31 = -56.0 / 15, A32 = 32.0 / 9;
-  constexpr double A40 = 19372.0 / 6561, A41 = -25360.0 / 2187, A42 = 64448.0 / 6561, A43 = -212.0 / 729;
-  constexpr double A50 = 9017.0 / 3168, A51 = -355.0 / 33, A52 = 46732.0 / 5247, A53 = 49.0 / 176,
-                   A54 = -5103.0 / 18656;
-  constexpr double B0 = 35.0 / 384, B2 = 500.0 / 1113, B3 = 125.0 / 192, B4 = -2187.0 / 6784, B5 = 11.0 / 84;
-  constexpr double E0 = -71.0 / 57600, E2 = 71.0 / 16695, E3 = -71.0 / 1920, E4 = 17253.0 / 339200,
-                   E5 = -22.0 / 525, E6 = 1.0 / 40;
+  using namespace dp5;
   const T rtol = c.rtol, atol = c.atol;
   const double t_bound = c.t_bound;
   const T inv_sqrt_n = T(0.22941573387056177);  // 1 / sqrt(19)
@@ -870,6 +874,8 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
   return result;
 }
 
+#include "fw_quad.hpp"
+
 // ---------------------------------------------------------------------------
 // Actuation.set_and_constrain_commands (pyfly.py:545-582).  cmd in/out in input
 // order (elevator, aileron, throttle); sp = dynamics set-points.
@@ -987,9 +993,11 @@ struct KeepY {  // default: y stays live in registers across the integration
 // `reload(y)` runs right after the integration and may re-read the pre-step
 // state from memory (the kernels do: keeping 19 values live across the RK loop
 // costs registers the loop needs).
-template <typename T, typename C, typename A, typename R = KeepY>
+// Q = 4: the integration runs on the lane quad of the aircraft (fw_quad.hpp; qr = lane in the quad,
+// every lane of the quad returns the same result).
+template <int Q = 1, typename T, typename C, typename A, typename R = KeepY>
 FW_HD int sim_step_masked(const C& c, const A& a, T* y, T* der, T* cmd, const T* wind, const T* tl, const T* ta, int& nfev,
-                          int& nacc, uint32_t& dmask, V2<T>* sy, V2<T>* sf, int stride, R reload = R()) {
+                          int& nacc, uint32_t& dmask, V2<T>* sy, V2<T>* sf, int stride, R reload = R(), int qr = 0) {
   dmask = 0;
   StepCtx<T> X;
 #pragma unroll
@@ -1007,7 +1015,8 @@ FW_HD int sim_step_masked(const C& c, const A& a, T* y, T* der, T* cmd, const T*
   T y1[NY];
 #pragma unroll
   for (int i = 0; i < NY; i++) y1[i] = y[i];
-  term = rk45(c, a, X, y1, sy, sf, stride, nfev, nacc, FW_ER_LDS ? sf + NP * stride : nullptr);
+  if constexpr (Q == 4) term = qd::rk45_quad(c, a, X, y1, nfev, nacc, qr);
+  else term = rk45(c, a, X, y1, sy, sf, stride, nfev, nacc, FW_ER_LDS ? sf + NP * stride : nullptr);
   reload(y);
   if (term < 0) {  // solver failure: y1 = the last accepted sub-step (rk45 wrote Y back), saved as usual
     dmask = DM_SOLVER_FAIL;

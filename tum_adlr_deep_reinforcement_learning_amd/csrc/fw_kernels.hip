@@ -54,6 +54,10 @@ constexpr int BLOCK = FW_BLOCK;
 #ifndef FW_MIN_WAVES
 #define FW_MIN_WAVES 1  // __launch_bounds__ minimum waves per SIMD of the env-step kernels (VGPR budget 512 / this)
 #endif
+#ifndef FW_QUAD_MIN_WAVES
+#define FW_QUAD_MIN_WAVES 1  // ... of their quad (Q = 4) instances (k_env_step also has a 2-wave instance)
+#endif
+#define FW_WAVES(Q) ((Q) == 4 ? FW_QUAD_MIN_WAVES : FW_MIN_WAVES)
 #ifndef FW_LDS_STATE
 #define FW_LDS_STATE 1  // 0 = y/f in VGPRs (measured: 512 VGPRs + spills, slower)
 #endif
@@ -108,7 +112,8 @@ constexpr uint32_t M_NONE = 0xFFFFFFFFu;
   do {                                                                                               \
     __builtin_amdgcn_s_waitcnt(0);                                                                   \
     if ((threadIdx.x & 63) == 0 && episode_out)                                                      \
-      ((unsigned long long*)episode_out)[(i >> 6) * 8 + (k)] = __builtin_amdgcn_s_memrealtime();     \
+      ((unsigned long long*)episode_out)[(((int64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6) * 8 + (k)] = \
+          __builtin_amdgcn_s_memrealtime();                                                          \
   } while (0)
 #else
 #define FW_TSTAMP(k) \
@@ -751,12 +756,14 @@ struct ReloadRow {
   }
 };
 
-template <typename T, typename C, bool RP = false>
-__global__ __launch_bounds__(BLOCK) void k_sim_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
+template <typename T, typename C, bool RP = false, int Q = 1>
+__global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_sim_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
                                                     const T* __restrict__ cmd_in, T* __restrict__ cmd_out,
                                                     uint8_t* __restrict__ success, int32_t* __restrict__ term_out,
                                                     int32_t* __restrict__ stats) {
-  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const int64_t tid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const int64_t i = tid / Q;  // Q = 4: lanes 4i..4i+3 integrate aircraft i (fw_quad.hpp)
+  const int qr = (int)(tid % Q);
   if (i >= s.n) return;
   const C& c = *reinterpret_cast<const C*>(cfgp);  // structural specialisation view (fw_device.hpp SpecCfg)
   const int64_t ld = s.ld;
@@ -773,16 +780,17 @@ __global__ __launch_bounds__(BLOCK) void k_sim_step(const DevCfg<T>* __restrict_
   turbulence_at(c, s, i, s.episode[i], k, tl, ta);
   int nfev = 0, nacc = 0;
   uint32_t dmask = 0;
-  __shared__ V2<T> lds[lds_slots<T>() * NP * BLOCK];  // y, f (+ error sum) of the block's aircraft (pairs)
+  __shared__ V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];  // y, f (+ error sum) of the block's aircraft (pairs)
   int term;
   if constexpr (RP) {
     const AeroP<T> ap = aero_from<T>(c, [&](int k) { return s.prm[k * ld + i]; });
-    term = sim_step_masked(c, ap, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
-                           lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i});
+    term = sim_step_masked<Q>(c, ap, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
+                              lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i}, qr);
   } else {
-    term = sim_step_masked(c, c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
-                           lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i});
+    term = sim_step_masked<Q>(c, c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
+                              lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i}, qr);
   }
+  if (qr != 0) return;  // the quad's other lanes hold the same result
   if (term) {  // uncommitted derived values keep their previous (history[-1]) value
 #pragma unroll
     for (int r = 0; r < 6; r++)
@@ -805,13 +813,15 @@ __global__ __launch_bounds__(BLOCK) void k_sim_step(const DevCfg<T>* __restrict_
 
 // FixedWingAircraft.step of aircraft i (the body of k_env_step and of one k_env_rollout step).
 // lds: this block's RK45 slots (lds_slots<T>() * NP * BLOCK pairs).
-template <typename T, typename C, bool RP = false>
+// Q = 4: called on the four lanes of aircraft i's quad (qr = 0..3); they integrate together, then
+// lane 0 alone runs the epilogue.
+template <typename T, typename C, bool RP = false, int Q = 1>
 __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, const int64_t i, V2<T>* lds,
                                               const T* __restrict__ actions, T* __restrict__ obs_out,
                                               T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
                                               int32_t* __restrict__ term_out, T* __restrict__ tobs_out,
                                               T* __restrict__ episode_out, int32_t* __restrict__ stats,
-                                              int auto_reset) {
+                                              int auto_reset, int qr = 0) {
   const int64_t ld = s.ld;
   FW_TSTAMP(0);
 
@@ -842,12 +852,13 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   int sterm;
   if constexpr (RP) {  // this aircraft's own parameters (simulator parameter randomisation)
     const AeroP<T> ap = aero_from<T>(c, [&](int k) { return s.prm[k * ld + i]; });
-    sterm = sim_step_masked(c, ap, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
-                            lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i});
+    sterm = sim_step_masked<Q>(c, ap, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
+                               lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i}, qr);
   } else {
-    sterm = sim_step_masked(c, c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
-                            lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i});
+    sterm = sim_step_masked<Q>(c, c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
+                               lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i}, qr);
   }
+  if (Q > 1 && qr != 0) return;
   // keep the epilogue's loads (action ring, goal bits, ...) below the integrator:
   // hoisted above it they would sit in VGPRs for the whole RK loop.  Actions and
   // targets are re-read for the same reason.
@@ -1021,19 +1032,22 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   FW_TSTAMP(4);
 }
 
-template <typename T, typename C, bool RP = false>
-__global__ __launch_bounds__(BLOCK, FW_MIN_WAVES) void k_env_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
+// MW > 0: minimum waves per SIMD instead of FW_WAVES(Q) (the 2-wave quad instance: 256 VGPRs, its
+// epilogue spills, but twice the quads fit the chip in one round)
+template <typename T, typename C, bool RP = false, int Q = 1, int MW = 0>
+__global__ __launch_bounds__(BLOCK, MW > 0 ? MW : FW_WAVES(Q)) void k_env_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
                                                     const T* __restrict__ actions, T* __restrict__ obs_out,
                                                     T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
                                                     int32_t* __restrict__ term_out, T* __restrict__ tobs_out,
                                                     T* __restrict__ episode_out, int32_t* __restrict__ stats,
                                                     int auto_reset) {
-  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const int64_t tid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const int64_t i = tid / Q;  // Q = 4: lanes 4i..4i+3 integrate aircraft i (fw_quad.hpp)
   if (i >= s.n) return;
   const C& c = *reinterpret_cast<const C*>(cfgp);  // structural specialisation view (fw_device.hpp SpecCfg)
-  __shared__ V2<T> lds[lds_slots<T>() * NP * BLOCK];  // y, f (+ error sum) of the block's aircraft (pairs)
-  env_step_lane<T, C, RP>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out, stats,
-                          auto_reset);
+  __shared__ V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];  // y, f (+ error sum) of the block's aircraft (pairs)
+  env_step_lane<T, C, RP, Q>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out, stats,
+                             auto_reset, (int)(tid % Q));
 }
 
 // One env step of k_env_rollout.  Inlined (default), the step loop's kernel spills ~230 VGPRs
@@ -1047,13 +1061,13 @@ __global__ __launch_bounds__(BLOCK, FW_MIN_WAVES) void k_env_step(const DevCfg<T
 #else
 #define FW_ROLLOUT_INLINE __forceinline__
 #endif
-template <typename T, typename C, bool RP>
+template <typename T, typename C, bool RP, int Q>
 __device__ FW_ROLLOUT_INLINE void env_step_call(const C& c, const State<T>& s, const int64_t i, V2<T>* lds,
                                            const T* actions, T* obs_out, T* rew_out, uint8_t* done_out,
                                            int32_t* term_out, T* tobs_out, T* episode_out, int32_t* stats,
-                                           int auto_reset) {
-  env_step_lane<T, C, RP>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out, stats,
-                          auto_reset);
+                                           int auto_reset, int qr) {
+  env_step_lane<T, C, RP, Q>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out, stats,
+                             auto_reset, qr);
 }
 
 // Open-loop rollout: n_steps consecutive FixedWingAircraft.step calls per aircraft in ONE launch, actions
@@ -1061,22 +1075,26 @@ __device__ FW_ROLLOUT_INLINE void env_step_call(const C& c, const State<T>& s, c
 // the results equal K k_env_step launches bit for bit; what changes is synchronisation: a wave moves on
 // to its next step as soon as its own aircraft are done, instead of every step waiting for the slowest
 // aircraft of the whole batch (the RK45 straggler tail).
-template <typename T, typename C, bool RP = false>
-__global__ __launch_bounds__(BLOCK, FW_MIN_WAVES) void k_env_rollout(const DevCfg<T>* __restrict__ cfgp, State<T> s, int n_steps,
+// Q = 4: the quad integrator as in k_env_step (lanes 1..3 of a quad skip each step's epilogue; lane 0's
+// stores of step k precede the quad's loads of step k + 1 in the wave's program order).
+template <typename T, typename C, bool RP = false, int Q = 1>
+__global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_env_rollout(const DevCfg<T>* __restrict__ cfgp, State<T> s, int n_steps,
                                                        const T* __restrict__ actions, T* __restrict__ obs_out,
                                                        T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
                                                        int32_t* __restrict__ term_out, T* __restrict__ tobs_out,
                                                        T* __restrict__ episode_out, int32_t* __restrict__ stats,
                                                        int auto_reset) {
-  const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const int64_t tid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const int64_t i = tid / Q;
+  const int qr = (int)(tid % Q);
   if (i >= s.n) return;
-  __shared__ V2<T> lds[lds_slots<T>() * NP * BLOCK];
+  __shared__ V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];
   const int64_t n = s.n, ow = (int64_t)cfgp->n_obs * cfgp->obs_len;
   for (int k = 0; k < n_steps; k++) {
     const C& c = *reinterpret_cast<const C*>(cfgp);
-    env_step_call<T, C, RP>(c, s, i, lds, actions + k * n * 3, obs_out + k * n * ow, rew_out + k * n, done_out + k * n,
+    env_step_call<T, C, RP, Q>(c, s, i, lds, actions + k * n * 3, obs_out + k * n * ow, rew_out + k * n, done_out + k * n,
                   term_out ? term_out + k * n : nullptr, tobs_out ? tobs_out + k * n * ow : nullptr,
-                  episode_out ? episode_out + k * n * 5 : nullptr, stats ? stats + k * n : nullptr, auto_reset);
+                  episode_out ? episode_out + k * n * 5 : nullptr, stats ? stats + k * n : nullptr, auto_reset, qr);
   }
 }
 
@@ -1110,6 +1128,8 @@ struct fw_handle {
   size_t o_obs_init = 0, o_obs_ring = 0;
   size_t o_prm = 0;         // per-aircraft parameter rows (env->n_rand > 0 at create; 0 = none)
   int rand_active = 0;      // the current config randomises parameters (kernels read the rows)
+  int lanes_opt = FW_LANES_AUTO;  // fw_set_lanes: 0 = automatic, 1, 4
+  int quad_ok = 1;          // the config allows the quad integrator (no wrapped ODE-state variable)
 };
 
 namespace {
@@ -1359,21 +1379,54 @@ int spec_of(const DevCfg<T>& d) {
   return 0;
 }
 
+// the quad integrator's conditions have no wrap (fw_quad.hpp qcond): ODE-state variables must not wrap
+constexpr uint32_t ODE_VAR_MASK = (7u << FW_V_OMEGA_P) | (7u << FW_V_POS_N) | (7u << FW_V_VEL_U) | (7u << FW_V_ACT0);
+
 int upload_cfg(fw_handle* h) {
   if (h->precision == FW_F64) {
     DevCfg<double> d;
     fill_devcfg(h, d);
     h->rand_active = d.rand_params;
     h->spec = spec_of(d);
+    h->quad_ok = (d.wrapmask & ODE_VAR_MASK) == 0;
     FW_HIP(hipMemcpy(h->dcfg, &d, sizeof(d), hipMemcpyHostToDevice));
   } else {
     DevCfg<float> d;
     fill_devcfg(h, d);
     h->rand_active = d.rand_params;
     h->spec = spec_of(d);
+    h->quad_ok = (d.wrapmask & ODE_VAR_MASK) == 0;
     FW_HIP(hipMemcpy(h->dcfg, &d, sizeof(d), hipMemcpyHostToDevice));
   }
   return FW_OK;
+}
+
+// Lanes per aircraft of the step kernels.  Automatic: the quad integrator while the aircraft fit the
+// chip in quads (its per-aircraft latency is lower), one lane each beyond (profiles/r02_quad.log):
+// up to FW_QUAD_1W_MAX aircraft one quad wave per SIMD, up to FW_QUAD_AUTO_MAX (fp32 X8 configurations)
+// the 2-wave instance of k_env_step.
+#ifndef FW_QUAD_AUTO_MAX
+#define FW_QUAD_AUTO_MAX 32768
+#endif
+#ifndef FW_QUAD_1W_MAX
+#define FW_QUAD_1W_MAX 16384
+#endif
+int lanes_of(const fw_handle* h) {
+  if (!h->quad_ok) return 1;
+  if (h->lanes_opt != FW_LANES_AUTO) return h->lanes_opt;
+  static const int env_lanes = [] {  // A/B switch for tests and profiling: FWSIM_LANES=1|4 replaces auto
+    const char* e = std::getenv("FWSIM_LANES");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (env_lanes == 1 || env_lanes == 4) return env_lanes;
+  if (h->n <= FW_QUAD_1W_MAX) return 4;
+  const bool wide_ok = h->precision == FW_F32 && !h->rand_active && (h->spec == 1 || h->spec == 2);
+  return wide_ok && h->n <= FW_QUAD_AUTO_MAX ? 4 : 1;
+}
+// the 2-wave quad instance of k_env_step (fp32, X8 specialisations) for shards beyond one quad wave per SIMD
+bool quad_wide(const fw_handle* h) {
+  return lanes_of(h) == 4 && h->n > FW_QUAD_1W_MAX && h->precision == FW_F32 && !h->rand_active &&
+         (h->spec == 1 || h->spec == 2);
 }
 
 // launch KERNEL<T, C> with C chosen by the handle's structural specialisation (G / P: the gym / pyfly
@@ -1391,6 +1444,23 @@ int upload_cfg(fw_handle* h) {
       hipLaunchKernelGGL((KERNEL<T, DevCfg<T>>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);        \
   } while (0)
 #define FW_LAUNCH_SPEC(KERNEL, T, h, st, ...) FW_LAUNCH_SPEC_AS(KERNEL, GymX8Cfg, PyflyX8Cfg, T, h, st, __VA_ARGS__)
+
+// ... and Q = lanes per aircraft (1, or 4 for the quad integrator)
+#define FW_LAUNCH_SPEC_Q(KERNEL, T, h, st, ...)                                                                   \
+  do {                                                                                                             \
+    const dim3 b_(BLOCK);                                                                                          \
+    const int q_ = lanes_of(h);                                                                                    \
+    const dim3 g_((unsigned)(((h)->n * q_ + BLOCK - 1) / BLOCK));                                                  \
+    const DevCfg<T>* d_ = (const DevCfg<T>*)(h)->dcfg;                                                             \
+    if (q_ == 4) {                                                                                                 \
+      if ((h)->rand_active) hipLaunchKernelGGL((KERNEL<T, DevCfg<T>, true, 4>), g_, b_, 0, st, d_, __VA_ARGS__);   \
+      else if ((h)->spec == 1) hipLaunchKernelGGL((KERNEL<T, GymX8Cfg<T>, false, 4>), g_, b_, 0, st, d_, __VA_ARGS__); \
+      else if ((h)->spec == 2) hipLaunchKernelGGL((KERNEL<T, PyflyX8Cfg<T>, false, 4>), g_, b_, 0, st, d_, __VA_ARGS__); \
+      else hipLaunchKernelGGL((KERNEL<T, DevCfg<T>, false, 4>), g_, b_, 0, st, d_, __VA_ARGS__);                  \
+    } else {                                                                                                       \
+      FW_LAUNCH_SPEC(KERNEL, T, h, st, __VA_ARGS__);                                                               \
+    }                                                                                                              \
+  } while (0)
 
 template <typename T>
 State<T> state_of(const fw_handle* h) {
@@ -1629,10 +1699,10 @@ int fw_sim_step(fw_handle* h, const void* commands_dev, void* commands_out_dev, 
   FW_HIP(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
   if (h->precision == FW_F64)
-    FW_LAUNCH_SPEC(k_sim_step, double, h, st, state_of<double>(h), (const double*)commands_dev,
+    FW_LAUNCH_SPEC_Q(k_sim_step, double, h, st, state_of<double>(h), (const double*)commands_dev,
                    (double*)commands_out_dev, success_dev, term_dev, stats_dev);
   else
-    FW_LAUNCH_SPEC(k_sim_step, float, h, st, state_of<float>(h), (const float*)commands_dev, (float*)commands_out_dev,
+    FW_LAUNCH_SPEC_Q(k_sim_step, float, h, st, state_of<float>(h), (const float*)commands_dev, (float*)commands_out_dev,
                    success_dev, term_dev, stats_dev);
   return check_launch();
 }
@@ -1645,13 +1715,26 @@ int fw_env_step(fw_handle* h, const void* actions_dev, void* obs_dev, void* rewa
   FW_HIP(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
   if (h->precision == FW_F64)
-    FW_LAUNCH_SPEC(k_env_step, double, h, st, state_of<double>(h), (const double*)actions_dev, (double*)obs_dev,
+    FW_LAUNCH_SPEC_Q(k_env_step, double, h, st, state_of<double>(h), (const double*)actions_dev, (double*)obs_dev,
                    (double*)reward_dev, done_dev, term_dev, (double*)terminal_obs_dev, (double*)episode_dev, stats_dev,
                    auto_reset);
   else
-    FW_LAUNCH_SPEC(k_env_step, float, h, st, state_of<float>(h), (const float*)actions_dev, (float*)obs_dev,
-                   (float*)reward_dev, done_dev, term_dev, (float*)terminal_obs_dev, (float*)episode_dev, stats_dev,
-                   auto_reset);
+    if (quad_wide(h)) {
+      const dim3 g((unsigned)((h->n * 4 + BLOCK - 1) / BLOCK)), b(BLOCK);
+      const DevCfg<float>* d = (const DevCfg<float>*)h->dcfg;
+      if (h->spec == 1)
+        hipLaunchKernelGGL((k_env_step<float, GymX8Cfg<float>, false, 4, 2>), g, b, 0, st, d, state_of<float>(h),
+                           (const float*)actions_dev, (float*)obs_dev, (float*)reward_dev, done_dev, term_dev,
+                           (float*)terminal_obs_dev, (float*)episode_dev, stats_dev, auto_reset);
+      else
+        hipLaunchKernelGGL((k_env_step<float, PyflyX8Cfg<float>, false, 4, 2>), g, b, 0, st, d, state_of<float>(h),
+                           (const float*)actions_dev, (float*)obs_dev, (float*)reward_dev, done_dev, term_dev,
+                           (float*)terminal_obs_dev, (float*)episode_dev, stats_dev, auto_reset);
+    } else {
+      FW_LAUNCH_SPEC_Q(k_env_step, float, h, st, state_of<float>(h), (const float*)actions_dev, (float*)obs_dev,
+                       (float*)reward_dev, done_dev, term_dev, (float*)terminal_obs_dev, (float*)episode_dev,
+                       stats_dev, auto_reset);
+    }
   return check_launch();
 }
 
@@ -1664,14 +1747,29 @@ int fw_env_rollout(fw_handle* h, int32_t n_steps, const void* actions_dev, void*
   FW_HIP(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
   if (h->precision == FW_F64)
-    FW_LAUNCH_SPEC(k_env_rollout, double, h, st, state_of<double>(h), n_steps, (const double*)actions_dev,
+    FW_LAUNCH_SPEC_Q(k_env_rollout, double, h, st, state_of<double>(h), n_steps, (const double*)actions_dev,
                    (double*)obs_dev, (double*)reward_dev, done_dev, term_dev, (double*)terminal_obs_dev,
                    (double*)episode_dev, stats_dev, auto_reset);
   else
-    FW_LAUNCH_SPEC(k_env_rollout, float, h, st, state_of<float>(h), n_steps, (const float*)actions_dev,
+    FW_LAUNCH_SPEC_Q(k_env_rollout, float, h, st, state_of<float>(h), n_steps, (const float*)actions_dev,
                    (float*)obs_dev, (float*)reward_dev, done_dev, term_dev, (float*)terminal_obs_dev,
                    (float*)episode_dev, stats_dev, auto_reset);
   return check_launch();
+}
+
+int fw_set_lanes(fw_handle* h, int32_t lanes) {
+  if (!h) return set_err(FW_E_INVALID, "NULL handle");
+  if (lanes != FW_LANES_AUTO && lanes != 1 && lanes != 4) return set_err(FW_E_INVALID, "lanes must be 0 (auto), 1 or 4");
+  if (lanes == 4 && !h->quad_ok)
+    return set_err(FW_E_INVALID, "lanes = 4 needs a config without wrapped ODE-state variables");
+  h->lanes_opt = lanes;
+  return FW_OK;
+}
+
+int fw_get_lanes(const fw_handle* h, int32_t* lanes) {
+  if (!h || !lanes) return set_err(FW_E_INVALID, "NULL argument");
+  *lanes = lanes_of(h);
+  return FW_OK;
 }
 
 int fw_set_metrics_output(fw_handle* h, void* metrics_dev) {

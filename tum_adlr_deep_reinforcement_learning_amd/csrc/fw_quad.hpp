@@ -1,0 +1,514 @@
+// fw_quad.hpp -- one aircraft's RK45 integration on a quad of four lanes (included by fw_device.hpp).
+//
+// The one-lane integrator (rk45 / rhs above) is a serial chain of ~600 instructions per RHS
+// evaluation, and a wave is as slow as its slowest aircraft: when aircraft are few (the per-GPU
+// shard of the strong-scaling configurations) or one aircraft needs thousands of evaluations (the
+// RK45 straggler tail), the step time is the latency of that chain.  Here lanes
+// 4a..4a+3 own aircraft a and split every 3-vector operation of the RHS by ROW (SIMT-uniform
+// code: lane r computes row r of the same formula):
+//
+//   lane r < 3 holds   eps_r (quaternion e_{r+1}), omega_r, pos_r, vel_r, actuator r, its rate r
+//   lane 3 holds       e0 (and zeros)
+//
+// so the Dormand-Prince folds, the error norm and the state conditioning run on 6 elements per
+// lane instead of 19, and the airspeed rotation, kinematics, force/moment rows and actuator
+// dynamics are computed once per row.  The scalar front (Va, alpha, beta, stall blend, the
+// aerodynamic coefficients) is computed redundantly on the four lanes.  Row values cross lanes
+// with DPP quad permutations (no LDS); norms are quad butterfly sums, bit-identical on the four
+// lanes, so the step-size control (and every branch) stays uniform within the quad.
+//
+// Reference behaviour: the same as rhs() / rk45() (PyFly._dynamics / _forces / _f_*,
+// pyfly.py:1450-1747; scipy 1.15.3 RK45, rk.py:111-173, common.py:68-134).  Sums are formed in a
+// different order (rows before lanes), so results differ from the one-lane path by rounding.
+#pragma once
+
+namespace qd {
+
+template <int A, int B, int C, int D>
+__device__ __forceinline__ int perm_i(int x) {
+  return __builtin_amdgcn_mov_dpp(x, A | (B << 2) | (C << 4) | (D << 6), 0xF, 0xF, false);
+}
+template <int A, int B, int C, int D>
+__device__ __forceinline__ float perm(float x) {
+  return __int_as_float(perm_i<A, B, C, D>(__float_as_int(x)));
+}
+template <int A, int B, int C, int D>
+__device__ __forceinline__ double perm(double x) {
+  const unsigned long long v = (unsigned long long)__double_as_longlong(x);
+  const unsigned lo = (unsigned)perm_i<A, B, C, D>((int)(unsigned)v);
+  const unsigned hi = (unsigned)perm_i<A, B, C, D>((int)(unsigned)(v >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// lane K's value on all four lanes
+template <int K, typename T>
+__device__ __forceinline__ T bc(T x) {
+  return perm<K, K, K, K>(x);
+}
+// row (r + 1) % 3 / (r + 2) % 3 of a row-distributed 3-vector (lane 3 keeps its own)
+template <typename T>
+__device__ __forceinline__ T nx1(T x) {
+  return perm<1, 2, 0, 3>(x);
+}
+template <typename T>
+__device__ __forceinline__ T nx2(T x) {
+  return perm<2, 0, 1, 3>(x);
+}
+// butterfly sum / min over the quad: the same bits on all four lanes
+template <typename T>
+__device__ __forceinline__ T sum4(T x) {
+  x = x + perm<1, 0, 3, 2>(x);
+  return x + perm<2, 3, 0, 1>(x);
+}
+__device__ __forceinline__ int min4(int k) {
+  k = min(k, perm_i<1, 0, 3, 2>(k));
+  return min(k, perm_i<2, 3, 0, 1>(k));
+}
+
+// Violation keys in rhs()'s order of checks (first violation wins = smallest key):
+// omega p q r, pos n e d, vel u v w, actuators 0 1 2, aileron, elevator, Va, alpha, beta.
+constexpr int KEY_NONE = 64;
+__device__ __forceinline__ int key_var(int k) {
+  if (k < 12) return (k < 9 ? FW_V_OMEGA_P : FW_V_ACT0 - 9) + k;
+  return k == 12 ? FW_V_AILERON : k == 13 ? FW_V_ELEVATOR : k == 14 ? FW_V_VA : k == 15 ? FW_V_ALPHA : FW_V_BETA;
+}
+
+// Per-lane constants of one step (lane r's rows; lane 3: no conditions)
+template <typename T>
+struct QCtx {
+  int r;
+  bool row;
+  T w0, w1, w2;           // steady wind components r, r+1, r+2 (cyclic)
+  T tl, ta, sp;           // linear / angular turbulence and actuator set-point of row r
+  T elev0, ail0;          // t == 0 elevator / aileron (StepCtx)
+  // conditions: constraint interval (+-inf: none) and clip interval + flag of this lane's variables
+  T om_cl, om_ch, om_vl, om_vh, pos_cl, pos_ch, vel_cl, vel_ch, vel_vl, vel_vh, act_cl, act_ch, act_vl, act_vh;
+  T dmax;
+  bool om_clip, vel_clip, act_clip, dclip;
+  T ac0, ac1, ac2, ac3, ac4, ac5;  // actuator coefficients of row r
+  // _f_omega_dot row r = kpq PQ + kqr QR + kpr PR + kpp (P^2 - R^2) + kt0 t0 + kt1 t1 + kt2 t2
+  T kpq, kqr, kpr, kpp, kt0, kt1, kt2;
+};
+
+template <typename T, typename C>
+__device__ __forceinline__ QCtx<T> qctx(const C& c, const StepCtx<T>& X, int r) {
+  QCtx<T> Q;
+  auto s3 = [r](T a0, T a1, T a2) { return r == 0 ? a0 : (r == 1 ? a1 : a2); };
+  const T inf = T(__builtin_inf());
+  Q.r = r;
+  Q.row = r < 3;
+  Q.w0 = s3(X.wind[0], X.wind[1], X.wind[2]);
+  Q.w1 = s3(X.wind[1], X.wind[2], X.wind[0]);
+  Q.w2 = s3(X.wind[2], X.wind[0], X.wind[1]);
+  Q.tl = s3(X.tl[0], X.tl[1], X.tl[2]);
+  Q.ta = s3(X.ta[0], X.ta[1], X.ta[2]);
+  Q.sp = s3(X.sp[0], X.sp[1], X.sp[2]);
+  Q.elev0 = X.elev0;
+  Q.ail0 = X.ail0;
+  auto lim = [&](int v0, T& cl, T& ch, T& vl, T& vh, bool& clip) {
+    T l[3], h[3], a[3], b[3];
+    bool k[3];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const uint32_t bit = 1u << (v0 + j);
+      const bool hc = (c.cmask & bit) != 0;
+      l[j] = hc ? c.lim[v0 + j].cmin : -inf;
+      h[j] = hc ? c.lim[v0 + j].cmax : inf;
+      a[j] = c.lim[v0 + j].vmin;
+      b[j] = c.lim[v0 + j].vmax;
+      k[j] = (c.clipmask & bit) != 0;
+    }
+    cl = Q.row ? s3(l[0], l[1], l[2]) : -inf;
+    ch = Q.row ? s3(h[0], h[1], h[2]) : inf;
+    vl = s3(a[0], a[1], a[2]);
+    vh = s3(b[0], b[1], b[2]);
+    clip = Q.row && (r == 0 ? k[0] : (r == 1 ? k[1] : k[2]));
+  };
+  bool pclip;
+  T pvl, pvh;
+  lim(FW_V_OMEGA_P, Q.om_cl, Q.om_ch, Q.om_vl, Q.om_vh, Q.om_clip);
+  lim(FW_V_POS_N, Q.pos_cl, Q.pos_ch, pvl, pvh, pclip);  // positions are checked, never clipped (rhs())
+  lim(FW_V_VEL_U, Q.vel_cl, Q.vel_ch, Q.vel_vl, Q.vel_vh, Q.vel_clip);
+  lim(FW_V_ACT0, Q.act_cl, Q.act_ch, Q.act_vl, Q.act_vh, Q.act_clip);
+  Q.dmax = s3(c.dot_max[0], c.dot_max[1], c.dot_max[2]);
+  Q.dclip = Q.row && ((c.dotmask >> (r & 3)) & 1u);
+  Q.ac0 = s3(c.ac[0][0], c.ac[1][0], c.ac[2][0]);
+  Q.ac1 = s3(c.ac[0][1], c.ac[1][1], c.ac[2][1]);
+  Q.ac2 = s3(c.ac[0][2], c.ac[1][2], c.ac[2][2]);
+  Q.ac3 = s3(c.ac[0][3], c.ac[1][3], c.ac[2][3]);
+  Q.ac4 = s3(c.ac[0][4], c.ac[1][4], c.ac[2][4]);
+  Q.ac5 = s3(c.ac[0][5], c.ac[1][5], c.ac[2][5]);
+  // pyfly.py:1659-1683: p' = g1 PQ - g2 QR + g3 l + g4 n;  q' = g5 PR - g6 (P^2 - R^2) + m / Jy;
+  //                     r' = g7 PQ - g1 QR + g4 l + g8 n
+  const T z = T(0);
+  Q.kpq = s3(c.gam[1], z, c.gam[7]);
+  Q.kqr = s3(-c.gam[2], z, -c.gam[1]);
+  Q.kpr = s3(z, c.gam[5], z);
+  Q.kpp = s3(z, -c.gam[6], z);
+  Q.kt0 = s3(c.gam[3], z, c.gam[4]);
+  Q.kt1 = s3(z, c.inv_Jy, z);
+  Q.kt2 = s3(c.gam[4], z, c.gam[8]);
+  return Q;
+}
+
+// Variable.apply_conditions of a row variable (interval form of cond(); the ODE-state variables
+// of a quad configuration never wrap, fw_kernels.hip checks that before choosing this path)
+template <typename T>
+__device__ __forceinline__ T qcond(T x, T cl, T ch, T vl, T vh, bool clip, int& key, int k) {
+  const bool viol = (x < cl) | (x > ch);
+  key = (key == KEY_NONE && viol) ? k : key;
+  return clip ? clipv(x, vl, vh) : x;
+}
+// ... of a scalar (quad-uniform) variable: cond() itself
+template <typename T, typename C>
+__device__ __forceinline__ T ucond(const C& c, int v, T x, int& key, int k) {
+  int t = 0;
+  x = cond(c, v, x, t);
+  key = (key == KEY_NONE && t) ? k : key;
+  return x;
+}
+
+// PyFly._dynamics (pyfly.py:1450-1482) of lane Q.r's rows: s = this lane's 6 stage values,
+// ds = their derivatives.  Returns the first violated condition of the aircraft (0 = none).
+template <typename T, typename C, typename A>
+__device__ __forceinline__ int rhs_quad(const C& c, const A& a, const QCtx<T>& Q, bool first, const T* s, T* ds) {
+  int key = KEY_NONE;
+  T om = s[1], vel = s[3], av = s[4], ad = s[5];
+  T elev = Q.elev0, ail = Q.ail0;
+  if (!first) {  // _set_states_from_ode_solution(save=False) + Actuation.set_states (pyfly.py:479-492)
+    om = qcond(om, Q.om_cl, Q.om_ch, Q.om_vl, Q.om_vh, Q.om_clip, key, Q.r);
+    (void)qcond(s[2], Q.pos_cl, Q.pos_ch, T(0), T(0), false, key, 3 + Q.r);
+    vel = qcond(vel, Q.vel_cl, Q.vel_ch, Q.vel_vl, Q.vel_vh, Q.vel_clip, key, 6 + Q.r);
+    av = qcond(av, Q.act_cl, Q.act_ch, Q.act_vl, Q.act_vh, Q.act_clip, key, 9 + Q.r);
+    ad = Q.dclip ? clipv(ad, -Q.dmax, Q.dmax) : ad;
+    const T a0 = bc<0>(av), a1 = bc<1>(av);
+    if (c.elevon) {
+      ail = (-a0 + a1) * T(0.5);
+      elev = (a0 + a1) * T(0.5);
+      ail = ucond(c, FW_V_AILERON, ail, key, 12);
+      elev = ucond(c, FW_V_ELEVATOR, elev, key, 13);
+    } else {
+      elev = a0;
+      ail = a1;
+    }
+  }
+  const T thr = bc<2>(av);
+  const T er = s[0];  // raw attitude (pyfly.py:1464): eps_r, lane 3: e0
+  const T e0 = bc<3>(er), e1 = bc<0>(er), e2 = bc<1>(er), e3 = bc<2>(er);
+  const T er1 = nx1(er), er2 = nx2(er);
+
+  // ---- _forces (pyfly.py:1484-1643) ----
+  const T omt = c.turbulence ? om - Q.ta : om;
+  const T p = bc<0>(omt), q = bc<1>(omt), r = bc<2>(omt);
+  // row r of wind_b = R(q) w + turb (_rot_b_v quaternion branch, pyfly.py:1780-1800; 1843)
+  const T Rrr = T(-1) + T(2) * (e0 * e0 + er * er);
+  const T Rr1 = T(2) * (er * er1 + er2 * e0);
+  const T Rr2 = T(2) * (er * er2 - er1 * e0);
+  const T var_ = vel - (Rrr * Q.w0 + Rr1 * Q.w1 + Rr2 * Q.w2 + Q.tl);
+  const T va0 = bc<0>(var_), va1 = bc<1>(var_), va2 = bc<2>(var_);
+  // the scalar front's transcendental work split over the lanes (lane 1: the beta chain, the others:
+  // the alpha chain), the results broadcast: the same values as rhs() computes serially
+  const bool l1 = Q.r == 1;
+  const T rxz2 = va0 * va0 + va2 * va2;
+  const T sq = fsqrt(l1 ? rxz2 + va1 * va1 : rxz2);
+  const T rxz = bc<0>(sq), Va_raw = bc<1>(sq);
+  const T at = fatan2(l1 ? va1 : va2, l1 ? rxz : va0);
+  T alpha = bc<0>(at), beta = bc<1>(at);
+  const T Va = ucond(c, FW_V_VA, Va_raw, key, 14);
+  alpha = ucond(c, FW_V_ALPHA, alpha, key, 15);
+  beta = ucond(c, FW_V_BETA, beta, key, 16);
+  const T rc = frcp(Q.r == 0 ? rxz : (l1 ? Va_raw : Va));  // 1 / rxz, 1 / Va_raw, 1 / Va on lanes 0, 1, 2
+  const T irxz = bc<0>(rc), iVr = bc<1>(rc), iVa = bc<2>(rc);
+  T sa, ca, sb, cb;
+  if (c.trig_alpha) {
+    sa = sin(alpha);
+    ca = cos(alpha);
+  } else {
+    sa = rxz2 > T(0) ? va2 * irxz : T(0);
+    ca = rxz2 > T(0) ? va0 * irxz : T(1);
+  }
+  if (c.trig_beta) {
+    sb = sin(beta);
+    cb = cos(beta);
+  } else {
+    sb = va1 * iVr;
+    cb = rxz * iVr;
+  }
+  const T V2a = Va * Va;
+  const T ex = fexp(l1 ? a.M * (alpha + a.a0) : -a.M * (alpha - a.a0));
+  const T ex1 = bc<0>(ex), ex2 = bc<1>(ex);
+  const T sigma = frcp(T(1) + a.sig_c * frcp(T(1) + ex1 + ex2));  // overflow-safe form, see rhs()
+  const T osig = T(1) - sigma;
+  const T sgna = sgn(alpha);
+  const T CLlin = a.CL0 + a.CLa * alpha;
+  const T CL = osig * CLlin + sigma * (T(2) * sgna * sa * sa * ca);
+  const T qn = q * iVa;
+  const T flift = a.qS * V2a * (CL + a.kCLq * qn + a.CLde * elev);
+  const T CD = a.CDp + osig * (CLlin * CLlin) * a.inv_pi_e_ar + sigma * (T(2) * sgna * (sa * sa * sa));
+  const T CDb = a.CDb1 * beta + a.CDb2 * beta * beta;
+  const T fdrag = a.qS * V2a * (CD + CDb + a.kCDq * qn + a.CDde * elev * elev);
+  const T Cm = osig * (a.Cm0 + a.Cma * alpha) + sigma * (a.Cmfp * sgna * sa * sa);
+  const T mm = a.qSc * V2a * (Cm + a.kCmq * qn + a.Cmde * elev);
+  const T bp = a.hb * p * iVa, br = a.hb * r * iVa;
+  const T fy = a.qS * V2a * (a.CY0 + a.CYb * beta + a.CYp * bp + a.CYr * br + a.CYda * ail);
+  const T ll = a.qSb * V2a * (a.Cl0 + a.Clb * beta + a.Clp * bp + a.Clr * br + a.Clda * ail);
+  const T nn = a.qSb * V2a * (a.Cn0 + a.Cnb * beta + a.Cnp * bp + a.Cnr * br + a.Cnda * ail);
+  // Row selections below pick among values computed on every lane: selects, not divergent branches
+  // (a conditional expression with work in its arms compiles to exec-masked branches here).
+  const bool r0 = Q.r == 0, r1 = Q.r == 1;
+  // row r of f_aero = R_euler(0, alpha, beta) . [-D, Y, -L]
+  const T fa0 = ca * cb * (-fdrag) + ca * sb * fy - sa * (-flift);
+  const T fa1 = -sb * (-fdrag) + cb * fy;
+  const T fa2 = sa * cb * (-fdrag) + sa * sb * fy + ca * (-flift);
+  const T fa = r0 ? fa0 : (r1 ? fa1 : fa2);
+  // gravity: column 2 of R(q) (the diagonal term in the raw-quaternion form of pyfly.py:1493-1499)
+  const T Dr = er * er + e0 * e0 - er1 * er1 - er2 * er2;
+  const T fg = a.mg * (r0 ? Rr2 : (r1 ? Rr1 : Dr));
+  const T Vd = Va + thr * (a.kmotor - Va);
+  const T fprop = a.prop_k * Vd * (Vd - Va);
+  const T tprop = -a.kTP2 * (thr * thr);
+  const T fr = (r0 ? fprop : T(0)) + fg + fa;
+  const T t0 = ll + tprop, t1 = mm, t2 = nn;
+
+  const T P0 = bc<0>(om), Q0 = bc<1>(om), R0 = bc<2>(om);
+  const T om1 = nx1(om), om2 = nx2(om), vel1 = nx1(vel), vel2 = nx2(vel);
+  // _f_attitude_dot (pyfly.py:1645-1657): row r = d eps_r, lane 3 = d e0
+  const T deps = T(0.5) * (om * e0 + om2 * er1 - om1 * er2);
+  const T de0 = T(0.5) * (-P0 * e1 - Q0 * e2 - R0 * e3);
+  // _f_omega_dot (pyfly.py:1659-1683), row r
+  const T dw = Q.kpq * (P0 * Q0) + Q.kqr * (Q0 * R0) + Q.kpr * (P0 * R0) + Q.kpp * (P0 * P0 - R0 * R0) + Q.kt0 * t0 +
+               Q.kt1 * t1 + Q.kt2 * t2;
+  // _f_p_dot (pyfly.py:1706-1737), row r
+  const T dp = Dr * vel + T(2) * (er * er1 - er2 * e0) * vel1 +
+               T(2) * (er * er2 + er1 * e0) * vel2;
+  // _f_v_dot (pyfly.py:1685-1704), row r
+  const T dv = om2 * vel1 - om1 * vel2 + fr * a.inv_mass;
+  // Actuation.rhs (pyfly.py:519-543), actuator r
+  const T da = av * Q.ac0 + Q.sp * Q.ac2 + ad * Q.ac1;
+  const T dd = av * Q.ac3 + Q.sp * Q.ac5 + ad * Q.ac4;
+  ds[0] = Q.row ? deps : de0;
+  ds[1] = Q.row ? dw : T(0);
+  ds[2] = Q.row ? dp : T(0);
+  ds[3] = Q.row ? dv : T(0);
+  ds[4] = Q.row ? da : T(0);
+  ds[5] = Q.row ? dd : T(0);
+  key = min4(key);
+  return key == KEY_NONE ? 0 : FW_TERM_VAR(key_var(key));
+}
+
+// rk45() on a quad: same stage machine, step-size control and failure semantics; each lane folds
+// its 3 pairs (6 elements), norms are quad sums.  y_io: the full 19-element state on every lane of
+// the quad, in and out.
+template <typename T, typename C, typename A>
+__device__ __forceinline__ int rk45_quad(const C& c, const A& a, const StepCtx<T>& X, T* y_io, int& nfev, int& nacc,
+                                         int r) {
+  using V = V2<T>;
+  using namespace dp5;
+  constexpr int NQ = 3;
+  const QCtx<T> Q = qctx<T>(c, X, r);
+  const T rtol = c.rtol, atol = c.atol;
+  const double t_bound = c.t_bound;
+  const T inv_sqrt_n = T(0.22941573387056177);  // 1 / sqrt(19)
+  V Y[NQ], F[NQ], ER[NQ], ys[NQ], K[NQ], P2v[NQ], P3[NQ], P4[NQ], P5[NQ], YB[NQ];
+  {
+    auto s3 = [r](T a0, T a1, T a2) { return r == 0 ? a0 : (r == 1 ? a1 : a2); };
+    T v[6];  // slot k of row r = y[1 + 3k + r]; lane 3: e0, 0, ...
+    v[0] = Q.row ? s3(y_io[1], y_io[2], y_io[3]) : y_io[0];
+#pragma unroll
+    for (int k = 1; k < 6; k++) v[k] = Q.row ? s3(y_io[3 * k + 1], y_io[3 * k + 2], y_io[3 * k + 3]) : T(0);
+#pragma unroll
+    for (int p = 0; p < NQ; p++) {
+      V w;
+      w.x = v[2 * p];
+      w.y = v[2 * p + 1];
+      Y[p] = w;
+      ys[p] = w;
+    }
+  }
+  double t = 0.0, h_abs = 0.0, h0 = 0.0, t_new = 0.0, min_step = 0.0;
+  T ht = T(0), d1 = T(0);
+  bool rejected = false, active = true;
+  int result = 0;
+  nfev = 0;
+  nacc = 0;
+  auto iscale = [&](V y) {
+    V s;
+    s.x = frcp(atol + fabs(y.x) * rtol);
+    s.y = frcp(atol + fabs(y.y) * rtol);
+    return s;
+  };
+  auto sq2 = [](V v) { return v.x * v.x + v.y * v.y; };
+
+  for (int stage = 0;;) {
+    if (!any_lane(active)) break;
+    {
+      const int term = rhs_quad(c, a, Q, stage == 0, (const T*)ys, (T*)K);
+      if (active) {
+        nfev++;
+        if (term) {
+          result = term;
+          active = false;
+        } else if (nfev >= c.max_nfev) {
+          result = -2;
+          active = false;
+        }
+      }
+    }
+    bool begin_step = false, begin_attempt = false;
+    if (stage == 0) {  // f0; select_initial_step (common.py:68-110)
+      T d0s = T(0), d1s = T(0);
+#pragma unroll
+      for (int p = 0; p < NQ; p++) {
+        F[p] = K[p];
+        const V isc = iscale(Y[p]);
+        d0s += sq2(Y[p] * isc);
+        d1s += sq2(K[p] * isc);
+      }
+      const T d0 = fsqrt(qd::sum4(d0s)) * inv_sqrt_n;
+      d1 = fsqrt(qd::sum4(d1s)) * inv_sqrt_n;
+      h0 = (d0 < T(1e-5) || d1 < T(1e-5)) ? 1e-6 : 0.01 * (double)d0 / (double)d1;
+      if (h0 > t_bound) h0 = t_bound;
+      const T h0t = (T)h0;
+#pragma unroll
+      for (int p = 0; p < NQ; p++) ys[p] = Y[p] + h0t * F[p];
+      stage = 1;
+    } else if (stage == 1) {  // probe; select_initial_step (common.py:111-134)
+      T d2s = T(0);
+#pragma unroll
+      for (int p = 0; p < NQ; p++) d2s += sq2((K[p] - F[p]) * iscale(Y[p]));
+      const double d2 = (double)(fsqrt(qd::sum4(d2s)) * inv_sqrt_n) / h0;
+      double h1;
+      if ((double)d1 <= 1e-15 && d2 <= 1e-15) h1 = fmax(1e-6, h0 * 1e-3);
+      else h1 = pow(0.01 / fmax((double)d1, d2), 1.0 / 5.0);
+      h_abs = fmin(fmin(100 * h0, h1), t_bound);
+      begin_step = active;
+      stage = 2;
+    } else if (stage == 2) {  // K = K1
+#pragma unroll
+      for (int p = 0; p < NQ; p++) {
+        ys[p] = Y[p] + (P2v[p] + K[p] * T(A21)) * ht;
+        P3[p] += K[p] * T(A31);
+        P4[p] += K[p] * T(A41);
+        P5[p] += K[p] * T(A51);
+      }
+      stage = 3;
+    } else if (stage == 3) {  // K = K2
+#pragma unroll
+      for (int p = 0; p < NQ; p++) {
+        P3[p] += K[p] * T(A32);
+        P4[p] += K[p] * T(A42);
+        P5[p] += K[p] * T(A52);
+        YB[p] += K[p] * T(B2);
+        ER[p] += K[p] * T(E2);
+        ys[p] = Y[p] + P3[p] * ht;
+      }
+      stage = 4;
+    } else if (stage == 4) {  // K = K3
+#pragma unroll
+      for (int p = 0; p < NQ; p++) {
+        P4[p] += K[p] * T(A43);
+        P5[p] += K[p] * T(A53);
+        YB[p] += K[p] * T(B3);
+        ER[p] += K[p] * T(E3);
+        ys[p] = Y[p] + P4[p] * ht;
+      }
+      stage = 5;
+    } else if (stage == 5) {  // K = K4
+#pragma unroll
+      for (int p = 0; p < NQ; p++) {
+        P5[p] += K[p] * T(A54);
+        YB[p] += K[p] * T(B4);
+        ER[p] += K[p] * T(E4);
+        ys[p] = Y[p] + P5[p] * ht;
+      }
+      stage = 6;
+    } else if (stage == 6) {  // K = K5; ys <- y_new
+#pragma unroll
+      for (int p = 0; p < NQ; p++) {
+        YB[p] += K[p] * T(B5);
+        ER[p] += K[p] * T(E5);
+        ys[p] = Y[p] + ht * YB[p];
+      }
+      stage = 7;
+    } else {  // K = f(t_new, y_new): error norm + step control (rk.py:138-173)
+      T es = T(0);
+#pragma unroll
+      for (int p = 0; p < NQ; p++) {
+        const V e = (ER[p] + K[p] * T(E6)) * ht;
+        const V y0 = Y[p], y1 = ys[p];
+        V sc;
+        sc.x = frcp(atol + fmax(fabs(y0.x), fabs(y1.x)) * rtol);
+        sc.y = frcp(atol + fmax(fabs(y0.y), fabs(y1.y)) * rtol);
+        es += sq2(e * sc);
+      }
+      const T en = fsqrt(qd::sum4(es)) * inv_sqrt_n;
+      if (active) {
+        if (en < T(1)) {
+          double factor = (en == T(0)) ? 10.0 : fmin(10.0, 0.9 * (double)fpow(en, T(-0.2)));
+          if (rejected) factor = fmin(1.0, factor);
+          h_abs *= factor;
+          t = t_new;
+#pragma unroll
+          for (int p = 0; p < NQ; p++) {
+            Y[p] = ys[p];
+            F[p] = K[p];
+          }
+          nacc++;
+          if (t - t_bound >= 0.0) active = false;
+          else begin_step = true;
+        } else {
+          h_abs *= fmax(0.2, 0.9 * (double)fpow(en, T(-0.2)));
+          rejected = true;
+          if (!(h_abs >= min_step)) {  // TOO_SMALL_STEP (or a NaN step size): solver failure
+            result = -1;
+            active = false;
+          } else {
+            begin_attempt = true;
+          }
+        }
+      }
+      stage = 2;
+    }
+    if (begin_step) {  // RungeKutta._step_impl entry (rk.py:111-124)
+      min_step = 10.0 * fabs(nextafter(t, 1e300) - t);
+      if (h_abs < min_step) h_abs = min_step;
+      rejected = false;
+      begin_attempt = true;
+    }
+    if (begin_attempt) {  // one trial step (rk.py:126-137); stage 1 input, accumulators seeded
+      double h = h_abs;
+      t_new = t + h;
+      if (t_new - t_bound > 0) t_new = t_bound;
+      h = t_new - t;
+      h_abs = fabs(h);
+      ht = (T)h;
+#pragma unroll
+      for (int p = 0; p < NQ; p++) {
+        const V f = F[p];
+        ys[p] = Y[p] + (f * T(A10)) * ht;
+        P2v[p] = f * T(A20);
+        P3[p] = f * T(A30);
+        P4[p] = f * T(A40);
+        P5[p] = f * T(A50);
+        YB[p] = f * T(B0);
+        ER[p] = f * T(E0);
+      }
+    }
+  }
+  // the accepted state back on every lane of the quad
+  T v[6];
+#pragma unroll
+  for (int p = 0; p < NQ; p++) {
+    v[2 * p] = Y[p].x;
+    v[2 * p + 1] = Y[p].y;
+  }
+  y_io[0] = bc<3>(v[0]);
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    y_io[1 + 3 * k] = bc<0>(v[k]);
+    y_io[2 + 3 * k] = bc<1>(v[k]);
+    y_io[3 + 3 * k] = bc<2>(v[k]);
+  }
+  return result;
+}
+
+}  // namespace qd

@@ -21,7 +21,7 @@ def _ptr(t):
 
 
 class Engine:
-    def __init__(self, sim_spec, env_spec=None, num_envs=1, device=None, precision="float32"):
+    def __init__(self, sim_spec, env_spec=None, num_envs=1, device=None, precision="float32", lanes=None):
         if not torch.cuda.is_available():
             raise _native.FwError("no HIP device visible: the fixed-wing engine runs on MI355X only (no CPU fallback)")
         self.lib = _native.load()
@@ -62,6 +62,19 @@ class Engine:
             _native.check(self.lib.fw_set_metrics_output(self.h, _ptr(self.metrics)), "fw_set_metrics_output")
         self._noise = None
         self.seed(0)
+        if lanes is not None:
+            self.set_lanes(lanes)
+
+    def set_lanes(self, lanes):
+        """Lanes per aircraft of the step kernels: 1, 4 (quad integrator) or 0 = automatic (fw_set_lanes)."""
+        _native.check(self.lib.fw_set_lanes(self.h, int(lanes)), "fw_set_lanes")
+
+    @property
+    def lanes(self):
+        """Lanes per aircraft the next fw_env_step / fw_sim_step launch uses."""
+        v = ctypes.c_int32()
+        _native.check(self.lib.fw_get_lanes(self.h, ctypes.byref(v)), "fw_get_lanes")
+        return v.value
 
     # ------------------------------------------------------------------
     def stream(self):
