@@ -230,14 +230,15 @@ def _batch_vs_oracle(n, steps, seed):
             break
 
 
-@pytest.mark.parametrize("n", [65536, 262144 + 37])
-def test_full_size_properties_fp32(n):
+@pytest.mark.parametrize("n,lanes", [(65536, 1), (65536, 4), (262144 + 37, 1)])
+def test_full_size_properties_fp32(n, lanes):
     """65536 envs (configs[2]) and a ragged batch above the largest config (262144 + 37), 300 steps of
-    U(-1,1) actions with auto-reset: finite, bounded, deterministic, shard-invariant."""
+    U(-1,1) actions with auto-reset: finite, bounded, deterministic, shard-invariant -- bit for bit for a
+    fixed integrator (the automatic lanes choice depends on the shard size, fw_set_lanes)."""
     spec = C.EnvSpec(sim_config_kw={"turbulence": False})
 
     def run(seed, offset=0, count=n, steps=300):
-        eng = _engine(spec.sim, spec, count, "float32")
+        eng = _engine(spec.sim, spec, count, "float32", lanes)
         eng.seed(seed, env_offset=offset)
         eng.reset()
         g = torch.Generator(device="cuda:0")
