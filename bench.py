@@ -274,7 +274,8 @@ def timed_env_steps(n, args, spec, dev, rank, world, env_offset, early=True):
     """Steady-state timing of ``args.steps`` env steps of ``n`` aircraft on this rank.
 
     Returns (elapsed_s, kernel_ms, early_ms) with elapsed/kernel_ms max-reduced over ranks."""
-    eng = Engine(spec.sim, spec, n, device=dev, precision=args.precision)
+    eng = Engine(spec.sim, spec, n, device=dev, precision=args.precision, lanes=args.lanes)
+    timed_env_steps.lanes = eng.lanes  # the integrator this shard size runs (fw_set_lanes)
     eng.seed(1234, env_offset=env_offset)
     eng.reset()
     gen = torch.Generator(device=dev)
@@ -399,6 +400,8 @@ def main():
     ap.add_argument("--sac-fill-steps", type=int, default=0,
                     help="also run a SAC replay-buffer fill of this many steps (BASELINE configs[4])")
     ap.add_argument("--sac-envs", type=int, default=262144, help="global envs of the SAC fill leg")
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="lanes per aircraft of k_env_step: 0 = automatic by shard size, 1, or 4 (quad integrator)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -426,6 +429,7 @@ def main():
     spec.metrics_enabled = not args.no_metrics
     n = args.envs // world  # strong scaling: the global batch is split over the GPUs
     elapsed, kern_ms, early_ms, long_ms = timed_env_steps(n, args, spec, dev, rank, world, rank * n)
+    lanes = timed_env_steps.lanes
     value = args.envs * args.steps / elapsed
 
     weak = None
@@ -480,6 +484,7 @@ def main():
                                       "steady wind, turbulence off")
                                    + (", streaming episode metrics" if spec.metrics_enabled else ""),
                        "global_envs": args.envs, "envs_per_gpu": n, "kernel": "k_env_step",
+                       "lanes_per_aircraft": lanes,
                        "parallelism": "env-dp%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

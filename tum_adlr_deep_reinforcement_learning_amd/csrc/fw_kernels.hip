@@ -814,8 +814,10 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_sim_step(const DevCfg<T>
 // FixedWingAircraft.step of aircraft i (the body of k_env_step and of one k_env_rollout step).
 // lds: this block's RK45 slots (lds_slots<T>() * NP * BLOCK pairs).
 // Q = 4: called on the four lanes of aircraft i's quad (qr = 0..3); they integrate together, then
-// lane 0 alone runs the epilogue.
-template <typename T, typename C, bool RP = false, int Q = 1>
+// lane 0 alone runs the epilogue.  PREF: the epilogue's loads (rings, goal register, metric state) are
+// issued before the integration, so their latency hides under it instead of following it; that keeps
+// ~90 more values live across the RK loop, which the one-wave quad instances have room for.
+template <typename T, typename C, bool RP = false, int Q = 1, bool PREF = false>
 __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, const int64_t i, V2<T>* lds,
                                               const T* __restrict__ actions, T* __restrict__ obs_out,
                                               T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
@@ -843,6 +845,40 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
 #pragma unroll
   for (int q = 0; q < 3; q++) cmd[q] = c.scale_actions ? scale_fwd(c, q, clipv(a[q], c.scale_low, c.scale_high)) : a[q];
 
+  const int steps = steps0 + 1;
+  const int steps_tgt = steps_tgt0 + 1;
+  // ---- epilogue inputs: action / command histories (newest first), goal register, metric state ----
+  T seqA[RING + 1][3], seqC[RING + 1][3];
+  uint32_t g[4];
+  Met<T> M;
+  T prev_cmd[3];
+  T ep_ret0;
+  auto load_epilogue = [&]() {
+#pragma unroll
+    for (int j = 1; j <= RING; j++) {
+#pragma unroll
+      for (int q = 0; q < 3; q++) seqA[j][q] = seqC[j][q] = T(0);
+      // previous action j = action number steps-j (1-based) -> slot (steps-j-1) % window
+      if (j <= c.act_window && steps - j >= 1) {
+        const int slot = (steps - j - 1) % c.act_window;
+#pragma unroll
+        for (int q = 0; q < 3; q++) seqA[j][q] = s.act_ring[((int64_t)slot * 3 + q) * ld + i];
+      }
+      if (j <= c.cmd_window && steps - j >= 1) {
+        const int slot = (steps - j - 1) % c.cmd_window;
+#pragma unroll
+        for (int q = 0; q < 3; q++) seqC[j][q] = s.cmd_ring[((int64_t)slot * 3 + q) * ld + i];
+      }
+    }
+    load_row(s.goal, 4, ld, i, g);
+    if (c.metrics) {
+      M.load(s, i, steps0);
+      load_row(s.cmd, 3, ld, i, prev_cmd);
+    }
+    ep_ret0 = ld_(s.ep_ret, 0, ld, i);
+  };
+  if constexpr (PREF) load_epilogue();
+
   // ---- PyFly.step ----
   T tl[3], ta[3];
   turbulence_at(c, s, i, episode, steps0, tl, ta);
@@ -859,44 +895,26 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
                                lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i}, qr);
   }
   if (Q > 1 && qr != 0) return;
-  // keep the epilogue's loads (action ring, goal bits, ...) below the integrator:
-  // hoisted above it they would sit in VGPRs for the whole RK loop.  Actions and
-  // targets are re-read for the same reason.
-  asm volatile("" ::: "memory");
-  load_row(s.target, 3, ld, i, tgt);
+  if constexpr (!PREF) {
+    // keep the epilogue's loads (action ring, goal bits, ...) below the integrator:
+    // hoisted above it they would sit in VGPRs for the whole RK loop.  Actions and
+    // targets are re-read for the same reason.
+    asm volatile("" ::: "memory");
+    load_row(s.target, 3, ld, i, tgt);
 #pragma unroll
-  for (int q = 0; q < 3; q++) a[q] = actions[i * 3 + q];
+    for (int q = 0; q < 3; q++) a[q] = actions[i * 3 + q];
+  }
   FW_TSTAMP(2);
   if (sterm) {
 #pragma unroll
     for (int r = 0; r < 6; r++)
       if (!(dmask & (1u << r))) der[r] = ld_(s.der, r, ld, i);
   }
-  const int steps = steps0 + 1;
-  const int steps_tgt = steps_tgt0 + 1;
-
-  // ---- action / command histories (newest first) ----
-  T seqA[RING + 1][3], seqC[RING + 1][3];
+  if constexpr (!PREF) load_epilogue();
 #pragma unroll
   for (int q = 0; q < 3; q++) {
     seqA[0][q] = a[q];
     seqC[0][q] = cmd[q];
-  }
-#pragma unroll
-  for (int j = 1; j <= RING; j++) {
-#pragma unroll
-    for (int q = 0; q < 3; q++) seqA[j][q] = seqC[j][q] = T(0);
-    // previous action j = action number steps-j (1-based) -> slot (steps-j-1) % window
-    if (j <= c.act_window && steps - j >= 1) {
-      const int slot = (steps - j - 1) % c.act_window;
-#pragma unroll
-      for (int q = 0; q < 3; q++) seqA[j][q] = s.act_ring[((int64_t)slot * 3 + q) * ld + i];
-    }
-    if (j <= c.cmd_window && steps - j >= 1) {
-      const int slot = (steps - j - 1) % c.cmd_window;
-#pragma unroll
-      for (int q = 0; q < 3; q++) seqC[j][q] = s.cmd_ring[((int64_t)slot * 3 + q) * ld + i];
-    }
   }
   {
     const int slot = (steps - 1) % c.act_window;
@@ -917,14 +935,8 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
     term = FW_TERM_STEPS;
   }
   T reward;
-  uint32_t g[4];
-  load_row(s.goal, 4, ld, i, g);
   // command history (control_variation): one constrained command per step, success or not
-  Met<T> M;
   if (c.metrics) {
-    M.load(s, i, steps0);
-    T prev_cmd[3];
-    load_row(s.cmd, 3, ld, i, prev_cmd);
     if (steps0 >= 1)
 #pragma unroll
       for (int q = 0; q < 3; q++) M.row[MR_CV] += fabs(cmd[q] - prev_cmd[q]);
@@ -966,7 +978,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
     reward = c.step_fail_timesteps ? (T)(steps - c.steps_max) : c.step_fail_value;
     term = sterm;
   }
-  const T ep_ret = ld_(s.ep_ret, 0, ld, i) + reward;
+  const T ep_ret = ep_ret0 + reward;
 
   // ---- observation (also the terminal observation) ----
   const int64_t ow = (int64_t)c.n_obs * c.obs_len;  // values per observation (rows x entries)
@@ -1046,8 +1058,8 @@ __global__ __launch_bounds__(BLOCK, MW > 0 ? MW : FW_WAVES(Q)) void k_env_step(c
   if (i >= s.n) return;
   const C& c = *reinterpret_cast<const C*>(cfgp);  // structural specialisation view (fw_device.hpp SpecCfg)
   __shared__ V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];  // y, f (+ error sum) of the block's aircraft (pairs)
-  env_step_lane<T, C, RP, Q>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out, stats,
-                             auto_reset, (int)(tid % Q));
+  env_step_lane<T, C, RP, Q, (Q == 4 && MW <= 1)>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out,
+                                                  episode_out, stats, auto_reset, (int)(tid % Q));
 }
 
 // One env step of k_env_rollout.  Inlined (default), the step loop's kernel spills ~230 VGPRs
@@ -1066,8 +1078,8 @@ __device__ FW_ROLLOUT_INLINE void env_step_call(const C& c, const State<T>& s, c
                                            const T* actions, T* obs_out, T* rew_out, uint8_t* done_out,
                                            int32_t* term_out, T* tobs_out, T* episode_out, int32_t* stats,
                                            int auto_reset, int qr) {
-  env_step_lane<T, C, RP, Q>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out, stats,
-                             auto_reset, qr);
+  env_step_lane<T, C, RP, Q, false>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out,
+                                    stats, auto_reset, qr);  // no prefetch: this kernel spills already
 }
 
 // Open-loop rollout: n_steps consecutive FixedWingAircraft.step calls per aircraft in ONE launch, actions
