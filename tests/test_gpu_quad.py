@@ -170,3 +170,30 @@ def test_quad_wide_instance_equals_rollout():
     assert torch.equal(a.get_block(C.FW_BLK_ODE), b.get_block(C.FW_BLK_ODE))
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("precision", ["float64", "float32"])
+def test_tail_handoff_matches_one_lane(precision, monkeypatch):
+    """One-lane kernels hand a wave's last <= 16 integrating aircraft to lane quads (rk45 HO): against
+    the same kernels with the handoff off (FWSIM_TAIL_QUAD=0), fp64 agrees within 1e-9 with the same
+    terminations and RHS-evaluation counts (up to rounding-level accept/reject flips); fp32 as the
+    generic-vs-specialised gate."""
+    spec = C.EnvSpec(config_kw={"steps_max": 60}, sim_config_kw={"turbulence": True, "turbulence_intensity": "light"})
+    n = 4096 + 37  # ragged last wave
+    steps = 60 if precision == "float64" else 10
+    outs = []
+    for tq in ("0", "16"):
+        monkeypatch.setenv("FWSIM_TAIL_QUAD", tq)
+        outs.append(_run(spec, n, precision, 1, steps)[0])
+    flips = 0
+    for (o1, r1, d1, t1, s1), (o2, r2, d2, t2, s2) in zip(*outs):
+        if precision == "float64":
+            assert torch.equal(d1, d2) and torch.equal(t1, t2)
+            flips += int((s1 != s2).sum())
+            same = (s1 == s2)
+            assert torch.allclose(o1[same], o2[same], rtol=1e-9, atol=1e-9)
+        else:
+            close = ((o1 - o2).abs() <= 1e-4 * (1 + o2.abs())).all(1) & ((r1 - r2).abs() <= 1e-4 * (1 + r2.abs()))
+            assert close.float().mean() >= 0.99
+    if precision == "float64":
+        assert flips <= 0.002 * n * steps, flips

@@ -193,7 +193,7 @@ def test_full_size_turbulence_properties_fp32(n):
     assert torch.isfinite(tot).all() and dones > 0
     tot2, dones2, ode2 = run()
     assert torch.equal(tot, tot2) and dones == dones2 and torch.equal(ode, ode2)
-    half = n // 2
+    half = n // 2 // 64 * 64  # shard offsets on wave boundaries: bitwise invariance holds per wave (tail handoff)
     tot_b, _, ode_b = run(offset=half, count=n - half)
     assert torch.equal(tot_b, tot[half:]) and torch.equal(ode_b, ode[:, half:])
 

@@ -26,7 +26,7 @@ static void run_sim(const fw_sim_config* sc, int64_t n, const double* y_in, cons
     int nf = 0, na = 0;
     uint32_t dm = 0;
     fw::V2<T> sy[fw::NP], sf[2 * fw::NP];  // sf + NP: error-sum slots when FW_ER_LDS
-    term[i] = sim_step_masked<T>(d, d, y, der, cmd, w, tl, ta, nf, na, dm, sy, sf, 1);
+    term[i] = sim_step_masked<1, false, T>(d, d, y, der, cmd, w, tl, ta, nf, na, dm, sy, sf, 1);
     nfev[i] = nf;
     nacc[i] = na;
     for (int k = 0; k < FW_NY; k++) y_out[i * FW_NY + k] = (double)y[k];

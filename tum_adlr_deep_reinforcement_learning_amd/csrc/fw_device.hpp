@@ -86,6 +86,7 @@ struct DevCfg {
   uint32_t dotmask;                    // per actuator: dot_max finite
   int elevon, disabled_inputs, turbulence, turb_len, wind_random;
   int max_nfev;                        // RHS-evaluation budget of one step
+  int tail_quad;                       // one-lane kernels: tail handoff to lane quads at <= this many (0 = off)
   // simulator parameter randomisation (FixedWingAircraft.sample_simulator_parameters,
   // fixed_wing.py:748-813): per-aircraft parameter rows redrawn at every reset
   int rand_params;                     // 1: aircraft read their own parameter rows (State::prm)
@@ -610,9 +611,19 @@ constexpr double E0 = -71.0 / 57600, E2 = 71.0 / 16695, E3 = -71.0 / 1920, E4 = 
                  E6 = 1.0 / 40;
 }  // namespace dp5
 
-template <typename T, typename C, typename A>
+#include "fw_quad.hpp"
+
+#ifndef FW_TAIL_QUAD
+#define FW_TAIL_QUAD 16  // one-lane waves hand their last <= this many integrating aircraft to lane quads (0 = off)
+#endif
+
+// HO: tail handoff (one-wave blocks, stride = 64): once at most FW_TAIL_QUAD aircraft of the wave are
+// still integrating, at the start of a trial step, they continue on lane quads of the same wave
+// (qd::handoff, fw_quad.hpp; ho = the block's handoff slots in LDS) -- the straggler tail at the
+// quad integrator's per-evaluation latency instead of the one-lane one.
+template <typename T, typename C, typename A, bool HO = false>
 FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy, V2<T>* __restrict__ sf, int stride,
-               int& nfev, int& nacc, V2<T>* __restrict__ se = nullptr) {
+               int& nfev, int& nacc, V2<T>* __restrict__ se = nullptr, void* ho = nullptr) {
   using V = V2<T>;
   using namespace dp5;
   const T rtol = c.rtol, atol = c.atol;
@@ -675,6 +686,7 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
   // dead data): only the writes that define a lane's result (Y/F on accept,
   // result, counters) are predicated.  Unpredicated folds keep the stage
   // arrays in place across the wave-uniform stage switch (no phi copies).
+  bool handoff = false;
   for (int stage = 0;;) {
     if (!any_lane(active)) break;
 #if FW_Y_PREFETCH
@@ -856,7 +868,30 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
 #endif
       }
     }
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (HO && FW_TAIL_QUAD > 0) {
+      if (stage == 2) {  // every integrating lane is at the start of a trial step
+        const unsigned long long am = __ballot(active);
+        const int na = __popcll(am);  // (lanes of the wave's aircraft past N have returned: quads need 4 na live lanes)
+        if (na > 0 && na <= c.tail_quad && 4 * na <= __popcll(__ballot(true))) {
+          handoff = true;
+          break;
+        }
+      }
+    }
+#endif
   }
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (HO && FW_TAIL_QUAD > 0) {
+    if (handoff) {
+      qd::QRun R{t, t_new, h_abs, min_step, rejected ? 1 : 0, nfev, nacc};
+      if (qd::handoff<T>(c, a, X, sy, sf, stride, active, R, result, ho)) {
+        nfev = R.nfev;
+        nacc = R.nacc;
+      }
+    }
+  }
+#endif
 #pragma unroll
   for (int p = 0; p < NP; p++) {
     const V v = Y(p);
@@ -873,8 +908,6 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
 #undef YB
   return result;
 }
-
-#include "fw_quad.hpp"
 
 // ---------------------------------------------------------------------------
 // Actuation.set_and_constrain_commands (pyfly.py:545-582).  cmd in/out in input
@@ -995,9 +1028,11 @@ struct KeepY {  // default: y stays live in registers across the integration
 // costs registers the loop needs).
 // Q = 4: the integration runs on the lane quad of the aircraft (fw_quad.hpp; qr = lane in the quad,
 // every lane of the quad returns the same result).
-template <int Q = 1, typename T, typename C, typename A, typename R = KeepY>
+// HO: the one-lane integration's tail handoff (rk45; ho = the block's qd::HoSlot array in LDS).
+template <int Q = 1, bool HO = false, typename T, typename C, typename A, typename R = KeepY>
 FW_HD int sim_step_masked(const C& c, const A& a, T* y, T* der, T* cmd, const T* wind, const T* tl, const T* ta, int& nfev,
-                          int& nacc, uint32_t& dmask, V2<T>* sy, V2<T>* sf, int stride, R reload = R(), int qr = 0) {
+                          int& nacc, uint32_t& dmask, V2<T>* sy, V2<T>* sf, int stride, R reload = R(), int qr = 0,
+                          void* ho = nullptr) {
   dmask = 0;
   StepCtx<T> X;
 #pragma unroll
@@ -1016,7 +1051,7 @@ FW_HD int sim_step_masked(const C& c, const A& a, T* y, T* der, T* cmd, const T*
 #pragma unroll
   for (int i = 0; i < NY; i++) y1[i] = y[i];
   if constexpr (Q == 4) term = qd::rk45_quad(c, a, X, y1, nfev, nacc, qr);
-  else term = rk45(c, a, X, y1, sy, sf, stride, nfev, nacc, FW_ER_LDS ? sf + NP * stride : nullptr);
+  else term = rk45<T, C, A, HO>(c, a, X, y1, sy, sf, stride, nfev, nacc, FW_ER_LDS ? sf + NP * stride : nullptr, ho);
   reload(y);
   if (term < 0) {  // solver failure: y1 = the last accepted sub-step (rk45 wrote Y back), saved as usual
     dmask = DM_SOLVER_FAIL;
@@ -1033,7 +1068,10 @@ FW_HD int sim_step_masked(const C& c, const A& a, T* y, T* der, T* cmd, const T*
   y[3] = e3;
   T eul[3];
   eul[0] = atan2(T(2) * (e0 * e1 + e2 * e3), e0 * e0 + e3 * e3 - e1 * e1 - e2 * e2);
-  eul[1] = asin(T(2) * (e0 * e2 - e1 * e3));
+  // fp32: the rounded argument can exceed 1 in magnitude at pitch +-90 deg (NaN in asin); the fp64 parity
+  // build keeps the reference's unclamped np.arcsin (pyfly.py:702)
+  const T sp2 = T(2) * (e0 * e2 - e1 * e3);
+  eul[1] = asin(sizeof(T) == 4 ? clipv(sp2, T(-1), T(1)) : sp2);
   eul[2] = atan2(T(2) * (e0 * e3 + e1 * e2), e0 * e0 + e1 * e1 - e2 * e2 - e3 * e3);
 #pragma unroll
   for (int i = 0; i < 3; i++) {
@@ -1077,7 +1115,8 @@ FW_HD int sim_step_masked(const C& c, const A& a, T* y, T* der, T* cmd, const T*
   else airspeed_vec(y, wind, tl, y + 10, va);
   const T Va_raw = sqrt(va[0] * va[0] + va[1] * va[1] + va[2] * va[2]);
   const T al = atan2(va[2], va[0]);
-  const T be = asin(va[1] / Va_raw);
+  const T sb1 = va[1] / Va_raw;  // (fp32: clamped like the pitch above; pyfly.py:1848)
+  const T be = asin(sizeof(T) == 4 ? clipv(sb1, T(-1), T(1)) : sb1);
   const T Va = cond(c, FW_V_VA, Va_raw, term);
   if (term) return term;
   der[3] = Va;

@@ -781,14 +781,17 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_sim_step(const DevCfg<T>
   int nfev = 0, nacc = 0;
   uint32_t dmask = 0;
   __shared__ V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];  // y, f (+ error sum) of the block's aircraft (pairs)
+  constexpr bool HO = Q == 1 && !RP && FW_TAIL_QUAD > 0;
+  static_assert(!HO || BLOCK == 64, "the tail handoff works per one-wave block");
+  __shared__ qd::HoSlot<T> ho[HO ? BLOCK : 1];
   int term;
   if constexpr (RP) {
     const AeroP<T> ap = aero_from<T>(c, [&](int k) { return s.prm[k * ld + i]; });
     term = sim_step_masked<Q>(c, ap, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
                               lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i}, qr);
   } else {
-    term = sim_step_masked<Q>(c, c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
-                              lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i}, qr);
+    term = sim_step_masked<Q, HO>(c, c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
+                                  lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i}, qr, ho);
   }
   if (qr != 0) return;  // the quad's other lanes hold the same result
   if (term) {  // uncommitted derived values keep their previous (history[-1]) value
@@ -823,8 +826,9 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
                                               T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
                                               int32_t* __restrict__ term_out, T* __restrict__ tobs_out,
                                               T* __restrict__ episode_out, int32_t* __restrict__ stats,
-                                              int auto_reset, int qr = 0) {
+                                              int auto_reset, int qr = 0, void* ho = nullptr) {
   const int64_t ld = s.ld;
+  constexpr bool HO = Q == 1 && !RP && FW_TAIL_QUAD > 0;  // ho: the block's qd::HoSlot<T>[64] (tail handoff)
   FW_TSTAMP(0);
 
   T y[NY], der[8], wind[3], tgt[3], a[3];
@@ -891,8 +895,8 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
     sterm = sim_step_masked<Q>(c, ap, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
                                lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i}, qr);
   } else {
-    sterm = sim_step_masked<Q>(c, c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
-                               lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i}, qr);
+    sterm = sim_step_masked<Q, HO>(c, c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
+                                   lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i}, qr, ho);
   }
   if (Q > 1 && qr != 0) return;
   if constexpr (!PREF) {
@@ -1058,8 +1062,10 @@ __global__ __launch_bounds__(BLOCK, MW > 0 ? MW : FW_WAVES(Q)) void k_env_step(c
   if (i >= s.n) return;
   const C& c = *reinterpret_cast<const C*>(cfgp);  // structural specialisation view (fw_device.hpp SpecCfg)
   __shared__ V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];  // y, f (+ error sum) of the block's aircraft (pairs)
+  static_assert(Q != 1 || RP || FW_TAIL_QUAD == 0 || BLOCK == 64, "the tail handoff works per one-wave block");
+  __shared__ qd::HoSlot<T> ho[Q == 1 && !RP ? BLOCK : 1];
   env_step_lane<T, C, RP, Q, (Q == 4 && MW <= 1)>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out,
-                                                  episode_out, stats, auto_reset, (int)(tid % Q));
+                                                  episode_out, stats, auto_reset, (int)(tid % Q), ho);
 }
 
 // One env step of k_env_rollout.  Inlined (default), the step loop's kernel spills ~230 VGPRs
@@ -1077,9 +1083,9 @@ template <typename T, typename C, bool RP, int Q>
 __device__ FW_ROLLOUT_INLINE void env_step_call(const C& c, const State<T>& s, const int64_t i, V2<T>* lds,
                                            const T* actions, T* obs_out, T* rew_out, uint8_t* done_out,
                                            int32_t* term_out, T* tobs_out, T* episode_out, int32_t* stats,
-                                           int auto_reset, int qr) {
+                                           int auto_reset, int qr, void* ho) {
   env_step_lane<T, C, RP, Q, false>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out,
-                                    stats, auto_reset, qr);  // no prefetch: this kernel spills already
+                                    stats, auto_reset, qr, ho);  // no prefetch: this kernel spills already
 }
 
 // Open-loop rollout: n_steps consecutive FixedWingAircraft.step calls per aircraft in ONE launch, actions
@@ -1101,12 +1107,13 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_env_rollout(const DevCfg
   const int qr = (int)(tid % Q);
   if (i >= s.n) return;
   __shared__ V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];
+  __shared__ qd::HoSlot<T> ho[Q == 1 && !RP ? BLOCK : 1];
   const int64_t n = s.n, ow = (int64_t)cfgp->n_obs * cfgp->obs_len;
   for (int k = 0; k < n_steps; k++) {
     const C& c = *reinterpret_cast<const C*>(cfgp);
     env_step_call<T, C, RP, Q>(c, s, i, lds, actions + k * n * 3, obs_out + k * n * ow, rew_out + k * n, done_out + k * n,
                   term_out ? term_out + k * n : nullptr, tobs_out ? tobs_out + k * n * ow : nullptr,
-                  episode_out ? episode_out + k * n * 5 : nullptr, stats ? stats + k * n : nullptr, auto_reset, qr);
+                  episode_out ? episode_out + k * n * 5 : nullptr, stats ? stats + k * n : nullptr, auto_reset, qr, ho);
   }
 }
 
@@ -1151,6 +1158,8 @@ void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
   std::memset(&d, 0, sizeof(d));
   const fw_sim_config& s = h->sim;
   const double* P = s.param;
+  d.tail_quad = std::getenv("FWSIM_TAIL_QUAD") ? std::atoi(std::getenv("FWSIM_TAIL_QUAD")) : FW_TAIL_QUAD;  // A/B switch
+  d.tail_quad = std::min(std::max(d.tail_quad, 0), 16);  // at most 16 quads in a wave
   d.t_bound = s.dt;
   d.dt = (T)s.dt;
   d.rtol = (T)s.rtol;

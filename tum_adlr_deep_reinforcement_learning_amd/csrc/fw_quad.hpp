@@ -295,41 +295,56 @@ __device__ __forceinline__ int rhs_quad(const C& c, const A& a, const QCtx<T>& Q
   return key == KEY_NONE ? 0 : FW_TERM_VAR(key_var(key));
 }
 
+// Where one aircraft's integration stands at the start of a trial step (the resumable part of the
+// state besides Y and F): what the one-lane integrator hands over (rk45 handoff, fw_device.hpp).
+struct QRun {
+  double t, t_new, h_abs, min_step;
+  int rejected, nfev, nacc;
+};
+
 // rk45() on a quad: same stage machine, step-size control and failure semantics; each lane folds
-// its 3 pairs (6 elements), norms are quad sums.  y_io: the full 19-element state on every lane of
-// the quad, in and out.
+// its 3 pairs (6 elements), norms are quad sums.  Y: this lane's slots of the accepted state (in and
+// out).  resume = false: a fresh integration from Y (R is output only); resume = true: continue at the
+// trial step R describes (begin_attempt done: t, t_new, h_abs, min_step, rejected set; F = f(t, Y)).
 template <typename T, typename C, typename A>
-__device__ __forceinline__ int rk45_quad(const C& c, const A& a, const StepCtx<T>& X, T* y_io, int& nfev, int& nacc,
-                                         int r) {
+__device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx<T>& Q, V2<T> (&Y)[3], V2<T> (&F)[3],
+                                              QRun& R, bool resume) {
   using V = V2<T>;
   using namespace dp5;
   constexpr int NQ = 3;
-  const QCtx<T> Q = qctx<T>(c, X, r);
   const T rtol = c.rtol, atol = c.atol;
   const double t_bound = c.t_bound;
   const T inv_sqrt_n = T(0.22941573387056177);  // 1 / sqrt(19)
-  V Y[NQ], F[NQ], ER[NQ], ys[NQ], K[NQ], P2v[NQ], P3[NQ], P4[NQ], P5[NQ], YB[NQ];
-  {
-    auto s3 = [r](T a0, T a1, T a2) { return r == 0 ? a0 : (r == 1 ? a1 : a2); };
-    T v[6];  // slot k of row r = y[1 + 3k + r]; lane 3: e0, 0, ...
-    v[0] = Q.row ? s3(y_io[1], y_io[2], y_io[3]) : y_io[0];
-#pragma unroll
-    for (int k = 1; k < 6; k++) v[k] = Q.row ? s3(y_io[3 * k + 1], y_io[3 * k + 2], y_io[3 * k + 3]) : T(0);
-#pragma unroll
-    for (int p = 0; p < NQ; p++) {
-      V w;
-      w.x = v[2 * p];
-      w.y = v[2 * p + 1];
-      Y[p] = w;
-      ys[p] = w;
-    }
-  }
+  V ER[NQ], ys[NQ], K[NQ], P2v[NQ], P3[NQ], P4[NQ], P5[NQ], YB[NQ];
   double t = 0.0, h_abs = 0.0, h0 = 0.0, t_new = 0.0, min_step = 0.0;
   T ht = T(0), d1 = T(0);
   bool rejected = false, active = true;
-  int result = 0;
-  nfev = 0;
-  nacc = 0;
+  int result = 0, nfev = 0, nacc = 0;
+  int stage = 0;
+#pragma unroll
+  for (int p = 0; p < NQ; p++) ys[p] = Y[p];
+  if (resume) {  // the trial step's stage-1 input and seeded accumulators (rk45 begin_attempt)
+    t = R.t;
+    t_new = R.t_new;
+    h_abs = R.h_abs;
+    min_step = R.min_step;
+    rejected = R.rejected != 0;
+    nfev = R.nfev;
+    nacc = R.nacc;
+    ht = (T)(t_new - t);
+#pragma unroll
+    for (int p = 0; p < NQ; p++) {
+      const V f = F[p];
+      ys[p] = Y[p] + (f * T(A10)) * ht;
+      P2v[p] = f * T(A20);
+      P3[p] = f * T(A30);
+      P4[p] = f * T(A40);
+      P5[p] = f * T(A50);
+      YB[p] = f * T(B0);
+      ER[p] = f * T(E0);
+    }
+    stage = 2;
+  }
   auto iscale = [&](V y) {
     V s;
     s.x = frcp(atol + fabs(y.x) * rtol);
@@ -338,7 +353,7 @@ __device__ __forceinline__ int rk45_quad(const C& c, const A& a, const StepCtx<T
   };
   auto sq2 = [](V v) { return v.x * v.x + v.y * v.y; };
 
-  for (int stage = 0;;) {
+  for (;;) {
     if (!any_lane(active)) break;
     {
       const int term = rhs_quad(c, a, Q, stage == 0, (const T*)ys, (T*)K);
@@ -494,6 +509,35 @@ __device__ __forceinline__ int rk45_quad(const C& c, const A& a, const StepCtx<T
       }
     }
   }
+  R.nfev = nfev;
+  R.nacc = nacc;
+  return result;
+}
+
+// a fresh integration of the state y_io (the full 19-element state on every lane of the quad, in and out)
+template <typename T, typename C, typename A>
+__device__ __forceinline__ int rk45_quad(const C& c, const A& a, const StepCtx<T>& X, T* y_io, int& nfev, int& nacc,
+                                         int r) {
+  using V = V2<T>;
+  constexpr int NQ = 3;
+  const QCtx<T> Q = qctx<T>(c, X, r);
+  V Y[NQ], F[NQ];
+  {
+    auto s3 = [r](T a0, T a1, T a2) { return r == 0 ? a0 : (r == 1 ? a1 : a2); };
+    T v[6];  // slot k of row r = y[1 + 3k + r]; lane 3: e0, 0, ...
+    v[0] = Q.row ? s3(y_io[1], y_io[2], y_io[3]) : y_io[0];
+#pragma unroll
+    for (int k = 1; k < 6; k++) v[k] = Q.row ? s3(y_io[3 * k + 1], y_io[3 * k + 2], y_io[3 * k + 3]) : T(0);
+#pragma unroll
+    for (int p = 0; p < NQ; p++) {
+      Y[p].x = v[2 * p];
+      Y[p].y = v[2 * p + 1];
+    }
+  }
+  QRun R;
+  const int result = rk45_quad_core(c, a, Q, Y, F, R, false);
+  nfev = R.nfev;
+  nacc = R.nacc;
   // the accepted state back on every lane of the quad
   T v[6];
 #pragma unroll
@@ -509,6 +553,75 @@ __device__ __forceinline__ int rk45_quad(const C& c, const A& a, const StepCtx<T
     y_io[3 + 3 * k] = bc<2>(v[k]);
   }
   return result;
+}
+
+// ---------------------------------------------------------------------------
+// Tail handoff (rk45 HO, fw_device.hpp): the at most 16 aircraft of a one-lane wave still integrating
+// continue on lane quads of the same wave.  Their Y / F rows stay in the one-lane integrator's LDS
+// slots (the quads read and write them in place); the step-control state and the step context go
+// through a per-wave LDS slot array.  Quad k (lanes 4k..4k+3) takes the k-th integrating lane.
+// ---------------------------------------------------------------------------
+template <typename T>
+struct HoSlot {
+  QRun R;
+  StepCtx<T> X;
+  int src, result;
+};
+
+// true on the handed-off lanes, whose R (nfev, nacc) and result are then the integration's
+template <typename T, typename C, typename A>
+__device__ __forceinline__ bool handoff(const C& c, const A& a, const StepCtx<T>& X, V2<T>* sy, V2<T>* sf, int stride,
+                                        bool active, QRun& R, int& result, void* ho) {
+  HoSlot<T>* st = (HoSlot<T>*)ho;
+  const int lane = (int)(threadIdx.x & 63);
+  const unsigned long long am = __ballot(active);
+  const int na = __popcll(am);
+  const int kk = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(am >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)am, 0u));
+  if (active) {
+    st[kk].R = R;
+    st[kk].X = X;
+    st[kk].src = lane;
+  }
+  __syncthreads();
+  const int k = lane >> 2, r = lane & 3;
+  if (k < na) {
+    const int src = st[k].src;
+    QRun Rq = st[k].R;
+    const StepCtx<T> Xs = st[k].X;
+    const QCtx<T> Q = qctx<T>(c, Xs, r);
+    V2<T>* const ysrc = sy - lane + src;
+    V2<T>* const fsrc = sf - lane + src;
+    auto el = [stride](V2<T>* base, int e) -> T& { return ((T*)(base + (e >> 1) * stride))[e & 1]; };
+    int e[6];  // element of this lane's slot m (row r of the m-th 3-vector; lane 3: e0 only)
+#pragma unroll
+    for (int m = 0; m < 6; m++) e[m] = r < 3 ? 1 + 3 * m + r : (m == 0 ? 0 : -1);
+    V2<T> Yq[3], Fq[3];
+#pragma unroll
+    for (int p = 0; p < 3; p++) {
+      Yq[p].x = e[2 * p] >= 0 ? el(ysrc, e[2 * p]) : T(0);
+      Yq[p].y = e[2 * p + 1] >= 0 ? el(ysrc, e[2 * p + 1]) : T(0);
+      Fq[p].x = e[2 * p] >= 0 ? el(fsrc, e[2 * p]) : T(0);
+      Fq[p].y = e[2 * p + 1] >= 0 ? el(fsrc, e[2 * p + 1]) : T(0);
+    }
+    const int res = rk45_quad_core(c, a, Q, Yq, Fq, Rq, true);
+#pragma unroll
+    for (int p = 0; p < 3; p++) {
+      if (e[2 * p] >= 0) el(ysrc, e[2 * p]) = Yq[p].x;
+      if (e[2 * p + 1] >= 0) el(ysrc, e[2 * p + 1]) = Yq[p].y;
+    }
+    if (r == 0) {
+      st[k].result = res;
+      st[k].R.nfev = Rq.nfev;
+      st[k].R.nacc = Rq.nacc;
+    }
+  }
+  __syncthreads();
+  if (active) {
+    result = st[kk].result;
+    R.nfev = st[kk].R.nfev;
+    R.nacc = st[kk].R.nacc;
+  }
+  return active;
 }
 
 }  // namespace qd
