@@ -4,7 +4,7 @@ Its reference parity is tested where the one-lane path's is, with both integrato
 (``test_gpu_parity.py``: reference single steps fp64 <= 1e-9 / fp32 gate, free-running reference
 trajectories; ``test_gpu_r02.py``: rollout == steps bit for bit).  Here:
 
-  lanes API ....................... auto = 4 up to FW_QUAD_AUTO_MAX aircraft, 1 above; explicit 1 / 4;
+  lanes API ....................... auto = 4 up to FW_QUAD_AUTO_MAX (16384) aircraft, 1 above; explicit 1 / 4;
                                     other values raise
   env steps fp64, quad vs 1 lane .. identical done / termination / RHS-evaluation counts, obs and reward
                                     within 1e-9 (80 steps, 1000 aircraft, auto-resets, light Dryden)
@@ -12,6 +12,9 @@ trajectories; ``test_gpu_r02.py``: rollout == steps bit for bit).  Here:
                                     can flip an RK45 accept/reject, as in the generic-vs-specialised gate)
   stragglers ...................... a wave whose aircraft need thousands of RHS evaluations (stiff
                                     sideways states) integrates them to the same states in both paths
+  tail handoff .................... one-lane kernels moving a wave's last <= 16 integrating aircraft to
+                                    quads: fp64 within 1e-9 of the handoff-off kernel (FWSIM_TAIL_QUAD=0),
+                                    same terminations; rollout == steps bit for bit above 16384 aircraft
 """
 import numpy as np
 import pytest
@@ -40,7 +43,7 @@ def test_lanes_api():
     with pytest.raises(_native.FwError):
         e.set_lanes(3)
     e.close()
-    big = _engine(spec, 40000, "float32")
+    big = _engine(spec, 20000, "float32")
     assert big.lanes == 1
     big.set_lanes(4)
     assert big.lanes == 4
@@ -147,14 +150,13 @@ def test_quad_stragglers(precision):
         assert np.median(rel) <= 1e-5 and (rel <= 1e-3).mean() >= 0.9
 
 
-def test_quad_wide_instance_equals_rollout():
-    """20000 aircraft, fp32: fw_env_step runs the 2-wave quad instance of k_env_step (register budget 256,
-    FW_QUAD_1W_MAX < N <= FW_QUAD_AUTO_MAX), fw_env_rollout the 1-wave one: the same code under another
-    register budget, equal bit for bit."""
+def test_one_lane_with_handoff_rollout_equals_steps():
+    """20037 aircraft, fp32 (above FW_QUAD_AUTO_MAX: one lane per aircraft with the tail handoff, ragged
+    last wave): fw_env_rollout equals fw_env_step launches bit for bit."""
     spec = C.EnvSpec(config_kw={"steps_max": 50}, sim_config_kw={"turbulence": True, "turbulence_intensity": "light"})
-    n, K = 20000, 60
+    n, K = 20000 + 37, 60
     a, b = _engine(spec, n, "float32"), _engine(spec, n, "float32")
-    assert a.lanes == 4
+    assert a.lanes == 1
     for e in (a, b):
         e.seed(5)
         e.reset()

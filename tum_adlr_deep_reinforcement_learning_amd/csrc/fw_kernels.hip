@@ -55,7 +55,7 @@ constexpr int BLOCK = FW_BLOCK;
 #define FW_MIN_WAVES 1  // __launch_bounds__ minimum waves per SIMD of the env-step kernels (VGPR budget 512 / this)
 #endif
 #ifndef FW_QUAD_MIN_WAVES
-#define FW_QUAD_MIN_WAVES 1  // ... of their quad (Q = 4) instances (k_env_step also has a 2-wave instance)
+#define FW_QUAD_MIN_WAVES 1  // ... of their quad (Q = 4) instances
 #endif
 #define FW_WAVES(Q) ((Q) == 4 ? FW_QUAD_MIN_WAVES : FW_MIN_WAVES)
 #ifndef FW_LDS_STATE
@@ -1048,10 +1048,8 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   FW_TSTAMP(4);
 }
 
-// MW > 0: minimum waves per SIMD instead of FW_WAVES(Q) (the 2-wave quad instance: 256 VGPRs, its
-// epilogue spills, but twice the quads fit the chip in one round)
-template <typename T, typename C, bool RP = false, int Q = 1, int MW = 0>
-__global__ __launch_bounds__(BLOCK, MW > 0 ? MW : FW_WAVES(Q)) void k_env_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
+template <typename T, typename C, bool RP = false, int Q = 1>
+__global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_env_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
                                                     const T* __restrict__ actions, T* __restrict__ obs_out,
                                                     T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
                                                     int32_t* __restrict__ term_out, T* __restrict__ tobs_out,
@@ -1064,7 +1062,7 @@ __global__ __launch_bounds__(BLOCK, MW > 0 ? MW : FW_WAVES(Q)) void k_env_step(c
   __shared__ V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];  // y, f (+ error sum) of the block's aircraft (pairs)
   static_assert(Q != 1 || RP || FW_TAIL_QUAD == 0 || BLOCK == 64, "the tail handoff works per one-wave block");
   __shared__ qd::HoSlot<T> ho[Q == 1 && !RP ? BLOCK : 1];
-  env_step_lane<T, C, RP, Q, (Q == 4 && MW <= 1)>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out,
+  env_step_lane<T, C, RP, Q, (Q == 4)>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out,
                                                   episode_out, stats, auto_reset, (int)(tid % Q), ho);
 }
 
@@ -1422,15 +1420,11 @@ int upload_cfg(fw_handle* h) {
   return FW_OK;
 }
 
-// Lanes per aircraft of the step kernels.  Automatic: the quad integrator while the aircraft fit the
-// chip in quads (its per-aircraft latency is lower), one lane each beyond (profiles/r02_quad.log):
-// up to FW_QUAD_1W_MAX aircraft one quad wave per SIMD, up to FW_QUAD_AUTO_MAX (fp32 X8 configurations)
-// the 2-wave instance of k_env_step.
+// Lanes per aircraft of the step kernels.  Automatic: the quad integrator while one quad wave per SIMD
+// holds the shard (FW_QUAD_AUTO_MAX aircraft: lower per-aircraft latency), beyond that one lane per
+// aircraft with the tail handoff to quads (rk45 HO); profiles/r02_lanes.log.
 #ifndef FW_QUAD_AUTO_MAX
-#define FW_QUAD_AUTO_MAX 32768
-#endif
-#ifndef FW_QUAD_1W_MAX
-#define FW_QUAD_1W_MAX 16384
+#define FW_QUAD_AUTO_MAX 16384
 #endif
 int lanes_of(const fw_handle* h) {
   if (!h->quad_ok) return 1;
@@ -1440,14 +1434,7 @@ int lanes_of(const fw_handle* h) {
     return e ? std::atoi(e) : 0;
   }();
   if (env_lanes == 1 || env_lanes == 4) return env_lanes;
-  if (h->n <= FW_QUAD_1W_MAX) return 4;
-  const bool wide_ok = h->precision == FW_F32 && !h->rand_active && (h->spec == 1 || h->spec == 2);
-  return wide_ok && h->n <= FW_QUAD_AUTO_MAX ? 4 : 1;
-}
-// the 2-wave quad instance of k_env_step (fp32, X8 specialisations) for shards beyond one quad wave per SIMD
-bool quad_wide(const fw_handle* h) {
-  return lanes_of(h) == 4 && h->n > FW_QUAD_1W_MAX && h->precision == FW_F32 && !h->rand_active &&
-         (h->spec == 1 || h->spec == 2);
+  return h->n <= FW_QUAD_AUTO_MAX ? 4 : 1;
 }
 
 // launch KERNEL<T, C> with C chosen by the handle's structural specialisation (G / P: the gym / pyfly
@@ -1740,22 +1727,9 @@ int fw_env_step(fw_handle* h, const void* actions_dev, void* obs_dev, void* rewa
                    (double*)reward_dev, done_dev, term_dev, (double*)terminal_obs_dev, (double*)episode_dev, stats_dev,
                    auto_reset);
   else
-    if (quad_wide(h)) {
-      const dim3 g((unsigned)((h->n * 4 + BLOCK - 1) / BLOCK)), b(BLOCK);
-      const DevCfg<float>* d = (const DevCfg<float>*)h->dcfg;
-      if (h->spec == 1)
-        hipLaunchKernelGGL((k_env_step<float, GymX8Cfg<float>, false, 4, 2>), g, b, 0, st, d, state_of<float>(h),
-                           (const float*)actions_dev, (float*)obs_dev, (float*)reward_dev, done_dev, term_dev,
-                           (float*)terminal_obs_dev, (float*)episode_dev, stats_dev, auto_reset);
-      else
-        hipLaunchKernelGGL((k_env_step<float, PyflyX8Cfg<float>, false, 4, 2>), g, b, 0, st, d, state_of<float>(h),
-                           (const float*)actions_dev, (float*)obs_dev, (float*)reward_dev, done_dev, term_dev,
-                           (float*)terminal_obs_dev, (float*)episode_dev, stats_dev, auto_reset);
-    } else {
-      FW_LAUNCH_SPEC_Q(k_env_step, float, h, st, state_of<float>(h), (const float*)actions_dev, (float*)obs_dev,
-                       (float*)reward_dev, done_dev, term_dev, (float*)terminal_obs_dev, (float*)episode_dev,
-                       stats_dev, auto_reset);
-    }
+    FW_LAUNCH_SPEC_Q(k_env_step, float, h, st, state_of<float>(h), (const float*)actions_dev, (float*)obs_dev,
+                     (float*)reward_dev, done_dev, term_dev, (float*)terminal_obs_dev, (float*)episode_dev,
+                     stats_dev, auto_reset);
   return check_launch();
 }
 
