@@ -16,6 +16,8 @@ trajectories; ``test_gpu_r02.py``: rollout == steps bit for bit).  Here:
                                     quads: fp64 within 1e-9 of the handoff-off kernel (FWSIM_TAIL_QUAD=0),
                                     same terminations; rollout == steps bit for bit above 16384 aircraft
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -32,6 +34,10 @@ def _engine(spec, n, precision, lanes=None):
     return Engine(spec.sim, spec, n, device=DEV, precision=precision, lanes=lanes)
 
 
+AUTO = pytest.mark.skipif(bool(os.environ.get("FWSIM_LANES")), reason="FWSIM_LANES overrides the automatic choice")
+
+
+@AUTO
 def test_lanes_api():
     spec = C.EnvSpec()
     e = _engine(spec, 100, "float32")
@@ -150,6 +156,7 @@ def test_quad_stragglers(precision):
         assert np.median(rel) <= 1e-5 and (rel <= 1e-3).mean() >= 0.9
 
 
+@AUTO
 def test_one_lane_with_handoff_rollout_equals_steps():
     """20037 aircraft, fp32 (above FW_QUAD_AUTO_MAX: one lane per aircraft with the tail handoff, ragged
     last wave): fw_env_rollout equals fw_env_step launches bit for bit."""

@@ -149,13 +149,15 @@ class FixedWingVecEnv(VecEnv):
 
     def __init__(self, num_envs=1, config_path=None, config_kw=None, sim_config_path=None, sim_parameter_path=None,
                  sim_config_kw=None, device=None, precision="float32", seed=None, return_tensors=False,
-                 info_target=True, curriculum_level=1, env_offset=0, record_history=False):
+                 info_target=True, curriculum_level=1, env_offset=0, record_history=False, lanes=None):
         self.spec = C.EnvSpec(config_path, config_kw, sim_config_path, sim_parameter_path, sim_config_kw,
                               curriculum_level=curriculum_level)
         obs_space = Box(self.spec.obs_low, self.spec.obs_high, dtype=np.float32)
         act_space = Box(self.spec.action_space_low, self.spec.action_space_high, dtype=np.float32)
         VecEnv.__init__(self, int(num_envs), obs_space, act_space)
-        self.engine = Engine(self.spec.sim, self.spec, self.num_envs, device=device, precision=precision)
+        # lanes: integrator (fw_set_lanes; None = automatic by num_envs); fix it when shards of different sizes
+        # must agree bit for bit
+        self.engine = Engine(self.spec.sim, self.spec, self.num_envs, device=device, precision=precision, lanes=lanes)
         self.device = self.engine.device
         self.return_tensors = return_tensors
         self.info_target = info_target
