@@ -249,9 +249,13 @@ __device__ __forceinline__ int rhs_quad(const C& c, const A& a, const QCtx<T>& Q
   const T Cm = osig * (a.Cm0 + a.Cma * alpha) + sigma * (a.Cmfp * sgna * sa * sa);
   const T mm = a.qSc * V2a * (Cm + a.kCmq * qn + a.Cmde * elev);
   const T bp = a.hb * p * iVa, br = a.hb * r * iVa;
-  const T fy = a.qS * V2a * (a.CY0 + a.CYb * beta + a.CYp * bp + a.CYr * br + a.CYda * ail);
-  const T ll = a.qSb * V2a * (a.Cl0 + a.Clb * beta + a.Clp * bp + a.Clr * br + a.Clda * ail);
-  const T nn = a.qSb * V2a * (a.Cn0 + a.Cnb * beta + a.Cnp * bp + a.Cnr * br + a.Cnda * ail);
+  // side force / roll / yaw moment: the same formula with row constants, one item per lane (lane 3
+  // repeats lane 0's), broadcast
+  auto s3c = [&Q](T x0, T x1, T x2) { return Q.r == 1 ? x1 : (Q.r == 2 ? x2 : x0); };
+  const T g2 = s3c(a.qS, a.qSb, a.qSb) * V2a *
+               (s3c(a.CY0, a.Cl0, a.Cn0) + s3c(a.CYb, a.Clb, a.Cnb) * beta + s3c(a.CYp, a.Clp, a.Cnp) * bp +
+                s3c(a.CYr, a.Clr, a.Cnr) * br + s3c(a.CYda, a.Clda, a.Cnda) * ail);
+  const T fy = bc<0>(g2), ll = bc<1>(g2), nn = bc<2>(g2);
   // Row selections below pick among values computed on every lane: selects, not divergent branches
   // (a conditional expression with work in its arms compiles to exec-masked branches here).
   const bool r0 = Q.r == 0, r1 = Q.r == 1;
@@ -291,6 +295,7 @@ __device__ __forceinline__ int rhs_quad(const C& c, const A& a, const QCtx<T>& Q
   ds[3] = Q.row ? dv : T(0);
   ds[4] = Q.row ? da : T(0);
   ds[5] = Q.row ? dd : T(0);
+  if (!any_lane(key != KEY_NONE)) return 0;  // (wave-uniform) no condition violated: the common case
   key = min4(key);
   return key == KEY_NONE ? 0 : FW_TERM_VAR(key_var(key));
 }
