@@ -206,3 +206,17 @@ def test_tail_handoff_matches_one_lane(precision, monkeypatch):
             assert close.float().mean() >= 0.99
     if precision == "float64":
         assert flips <= 0.002 * n * steps, flips
+
+
+def test_quad_refused_with_wrapped_ode_variable():
+    """The quad integrator's row conditions have no wrap: a configuration wrapping an ODE-state variable
+    runs one lane per aircraft (automatic), and asking for quads fails loudly."""
+    spec = C.EnvSpec(sim_config_kw={"turbulence": False})
+    spec.sim.vars["omega_p"].wrap = True
+    e = _engine(spec, 64, "float64")
+    assert e.lanes == 1
+    with pytest.raises(_native.FwError):
+        e.set_lanes(4)
+    e.set_lanes(1)
+    assert e.lanes == 1
+    e.close()
