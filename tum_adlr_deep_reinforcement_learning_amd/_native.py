@@ -55,26 +55,56 @@ def _build_lock(out):
             fcntl.flock(f, fcntl.LOCK_UN)
 
 
-def build(force=False, verbose=False, out=None, extra=None):
-    """Compile csrc/*.hip into lib/libfwsim.so (seconds; cross-compiles without a GPU).
+N_PARTS = 7  # fw_kernels.hip build parts (FW_PART 0..6, see the file's header)
 
-    Holds a file lock around the staleness check and the compile, and writes through a
-    per-process temporary file, so parallel callers never see a partial library."""
+
+def _jobs():
+    try:
+        return max(1, int(os.environ.get("MAX_JOBS", "")))
+    except ValueError:
+        return max(1, min(8, os.cpu_count() or 1))
+
+
+def build(force=False, verbose=False, out=None, extra=None):
+    """Compile csrc/*.hip into lib/libfwsim.so (cross-compiles without a GPU).
+
+    fw_kernels.hip is compiled as N_PARTS translation units in parallel (the step kernels' template
+    instances dominate the compile time), then linked with fw_rollout.hip.  Holds a file lock around
+    the staleness check and the compile, and writes through per-process temporary files, so parallel
+    callers never see a partial library."""
     out = out or LIB_PATH
     with _build_lock(out):
         if out == LIB_PATH and not force and not needs_build():
             return LIB_PATH
-        tmp = "%s.%d.tmp" % (out, os.getpid())
+        tag = "%d" % os.getpid()
+        tmp = "%s.%s.tmp" % (out, tag)
         flags = EXTRA_FLAGS if extra is None else extra
-        cmd = [_hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared"] + flags + ["-o", tmp] + UNITS
-        if verbose:
-            print(" ".join(cmd))
+        base = [_hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC"] + flags
+        units = [(UNITS[0], ["-DFW_PART=%d" % p]) for p in range(N_PARTS)] + [(u, []) for u in UNITS[1:]]
+        objs = ["%s.%s.%d.o" % (out, tag, k) for k in range(len(units))]
+        cmds = [base + d + ["-c", "-o", o, src] for (src, d), o in zip(units, objs)]
         try:
-            subprocess.check_call(cmd)
+            pending, running = list(cmds), []
+            while pending or running:
+                while pending and len(running) < _jobs():
+                    c = pending.pop(0)
+                    if verbose:
+                        print(" ".join(c))
+                    running.append((subprocess.Popen(c), c))
+                p, c = running.pop(0)
+                if p.wait() != 0:
+                    for q, _ in running:
+                        q.wait()
+                    raise subprocess.CalledProcessError(p.returncode, c)
+            link = [_hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs
+            if verbose:
+                print(" ".join(link))
+            subprocess.check_call(link)
             os.replace(tmp, out)
         finally:
-            if os.path.exists(tmp):
-                os.remove(tmp)
+            for f in objs + [tmp]:
+                if os.path.exists(f):
+                    os.remove(f)
     return out
 
 

@@ -25,8 +25,18 @@
 
 #include "fw_device.hpp"
 
+// Parallel build (_native.py): this file is compiled as several translation units.  FW_PART = 0 holds
+// the host code, the C ABI and the small kernels; FW_PART = 1..6 each instantiate one launch helper
+// (fwl:: below) and with it one step kernel's template instances for one precision.  FW_PART
+// undefined: everything in one unit.
+#ifndef FW_PART
+#define FW_PART -1
+#endif
+#define FW_HOST_PART (FW_PART <= 0)
+
 using namespace fw;
 
+#if FW_HOST_PART
 namespace {
 thread_local std::string g_err;
 }  // namespace
@@ -36,6 +46,7 @@ int fw::set_error(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+#endif
 
 namespace {
 
@@ -1510,6 +1521,60 @@ int check_launch() {
 
 }  // namespace
 
+// Launch helpers of the step kernels: one explicit instance per build part (FW_PART 1..6), called
+// from the C ABI in part 0.  Only plain types cross the parts.
+namespace fwl {
+template <typename T>
+int sim_step(fw_handle* h, hipStream_t st, const void* cmd, void* cmd_out, uint8_t* success, int32_t* term,
+             int32_t* stats) {
+  FW_LAUNCH_SPEC_Q(k_sim_step, T, h, st, state_of<T>(h), (const T*)cmd, (T*)cmd_out, success, term, stats);
+  return check_launch();
+}
+template <typename T>
+int env_step(fw_handle* h, hipStream_t st, const void* actions, void* obs, void* reward, uint8_t* done, int32_t* term,
+             void* tobs, void* episode, int32_t* stats, int32_t auto_reset) {
+  FW_LAUNCH_SPEC_Q(k_env_step, T, h, st, state_of<T>(h), (const T*)actions, (T*)obs, (T*)reward, done, term, (T*)tobs,
+                   (T*)episode, stats, auto_reset);
+  return check_launch();
+}
+template <typename T>
+int env_rollout(fw_handle* h, hipStream_t st, int32_t n_steps, const void* actions, void* obs, void* reward,
+                uint8_t* done, int32_t* term, void* tobs, void* episode, int32_t* stats, int32_t auto_reset) {
+  FW_LAUNCH_SPEC_Q(k_env_rollout, T, h, st, state_of<T>(h), n_steps, (const T*)actions, (T*)obs, (T*)reward, done,
+                   term, (T*)tobs, (T*)episode, stats, auto_reset);
+  return check_launch();
+}
+}  // namespace fwl
+
+#define FW_SIG_SIM(T) int fwl::sim_step<T>(fw_handle*, hipStream_t, const void*, void*, uint8_t*, int32_t*, int32_t*)
+#define FW_SIG_ENV(T)                                                                                           \
+  int fwl::env_step<T>(fw_handle*, hipStream_t, const void*, void*, void*, uint8_t*, int32_t*, void*, void*, \
+                       int32_t*, int32_t)
+#define FW_SIG_ROLL(T)                                                                                              \
+  int fwl::env_rollout<T>(fw_handle*, hipStream_t, int32_t, const void*, void*, void*, uint8_t*, int32_t*, void*, \
+                          void*, int32_t*, int32_t)
+#if FW_PART == 0
+extern template FW_SIG_SIM(float);
+extern template FW_SIG_SIM(double);
+extern template FW_SIG_ENV(float);
+extern template FW_SIG_ENV(double);
+extern template FW_SIG_ROLL(float);
+extern template FW_SIG_ROLL(double);
+#elif FW_PART == 1
+template FW_SIG_ENV(float);
+#elif FW_PART == 2
+template FW_SIG_ENV(double);
+#elif FW_PART == 3
+template FW_SIG_ROLL(float);
+#elif FW_PART == 4
+template FW_SIG_ROLL(double);
+#elif FW_PART == 5
+template FW_SIG_SIM(float);
+#elif FW_PART == 6
+template FW_SIG_SIM(double);
+#endif
+
+#if FW_HOST_PART
 extern "C" {
 
 int fw_abi_version(void) { return FWSIM_ABI_VERSION; }
@@ -1707,12 +1772,8 @@ int fw_sim_step(fw_handle* h, const void* commands_dev, void* commands_out_dev, 
   FW_HIP(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
   if (h->precision == FW_F64)
-    FW_LAUNCH_SPEC_Q(k_sim_step, double, h, st, state_of<double>(h), (const double*)commands_dev,
-                   (double*)commands_out_dev, success_dev, term_dev, stats_dev);
-  else
-    FW_LAUNCH_SPEC_Q(k_sim_step, float, h, st, state_of<float>(h), (const float*)commands_dev, (float*)commands_out_dev,
-                   success_dev, term_dev, stats_dev);
-  return check_launch();
+    return fwl::sim_step<double>(h, st, commands_dev, commands_out_dev, success_dev, term_dev, stats_dev);
+  return fwl::sim_step<float>(h, st, commands_dev, commands_out_dev, success_dev, term_dev, stats_dev);
 }
 
 int fw_env_step(fw_handle* h, const void* actions_dev, void* obs_dev, void* reward_dev, uint8_t* done_dev,
@@ -1723,14 +1784,10 @@ int fw_env_step(fw_handle* h, const void* actions_dev, void* obs_dev, void* rewa
   FW_HIP(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
   if (h->precision == FW_F64)
-    FW_LAUNCH_SPEC_Q(k_env_step, double, h, st, state_of<double>(h), (const double*)actions_dev, (double*)obs_dev,
-                   (double*)reward_dev, done_dev, term_dev, (double*)terminal_obs_dev, (double*)episode_dev, stats_dev,
-                   auto_reset);
-  else
-    FW_LAUNCH_SPEC_Q(k_env_step, float, h, st, state_of<float>(h), (const float*)actions_dev, (float*)obs_dev,
-                     (float*)reward_dev, done_dev, term_dev, (float*)terminal_obs_dev, (float*)episode_dev,
-                     stats_dev, auto_reset);
-  return check_launch();
+    return fwl::env_step<double>(h, st, actions_dev, obs_dev, reward_dev, done_dev, term_dev, terminal_obs_dev,
+                                 episode_dev, stats_dev, auto_reset);
+  return fwl::env_step<float>(h, st, actions_dev, obs_dev, reward_dev, done_dev, term_dev, terminal_obs_dev,
+                              episode_dev, stats_dev, auto_reset);
 }
 
 int fw_env_rollout(fw_handle* h, int32_t n_steps, const void* actions_dev, void* obs_dev, void* reward_dev,
@@ -1742,14 +1799,10 @@ int fw_env_rollout(fw_handle* h, int32_t n_steps, const void* actions_dev, void*
   FW_HIP(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
   if (h->precision == FW_F64)
-    FW_LAUNCH_SPEC_Q(k_env_rollout, double, h, st, state_of<double>(h), n_steps, (const double*)actions_dev,
-                   (double*)obs_dev, (double*)reward_dev, done_dev, term_dev, (double*)terminal_obs_dev,
-                   (double*)episode_dev, stats_dev, auto_reset);
-  else
-    FW_LAUNCH_SPEC_Q(k_env_rollout, float, h, st, state_of<float>(h), n_steps, (const float*)actions_dev,
-                   (float*)obs_dev, (float*)reward_dev, done_dev, term_dev, (float*)terminal_obs_dev,
-                   (float*)episode_dev, stats_dev, auto_reset);
-  return check_launch();
+    return fwl::env_rollout<double>(h, st, n_steps, actions_dev, obs_dev, reward_dev, done_dev, term_dev,
+                                    terminal_obs_dev, episode_dev, stats_dev, auto_reset);
+  return fwl::env_rollout<float>(h, st, n_steps, actions_dev, obs_dev, reward_dev, done_dev, term_dev, terminal_obs_dev,
+                                 episode_dev, stats_dev, auto_reset);
 }
 
 int fw_set_lanes(fw_handle* h, int32_t lanes) {
@@ -1820,3 +1873,4 @@ int fw_set_state(fw_handle* h, int32_t block, const void* src_dev, void* stream)
 }
 
 }  // extern "C"
+#endif  // FW_HOST_PART
