@@ -307,10 +307,220 @@ struct QRun {
   int rejected, nfev, nacc;
 };
 
-// rk45() on a quad: same stage machine, step-size control and failure semantics; each lane folds
-// its 3 pairs (6 elements), norms are quad sums.  Y: this lane's slots of the accepted state (in and
-// out).  resume = false: a fresh integration from Y (R is output only); resume = true: continue at the
+#ifndef FW_QUAD_UNROLL
+#define FW_QUAD_UNROLL 1  // 0 = the stage machine below (one RHS site per loop iteration), A/B switch
+#endif
+
+// rk45() on a quad: same step-size control and failure semantics; each lane folds its 3 pairs (6
+// elements), norms are quad sums.  Y: this lane's slots of the accepted state (in and out).
+// resume = false: a fresh integration from Y (R is output only); resume = true: continue at the
 // trial step R describes (begin_attempt done: t, t_new, h_abs, min_step, rejected set; F = f(t, Y)).
+//
+// Every lane of a wave runs the same sequence of RHS evaluations -- f0, the initial-step probe, then
+// trial steps of exactly six (K1..K5 and the FSAL f(t_new, y_new)), accepted or rejected -- so the
+// stage is wave-uniform and one trial step is written out with its six RHS sites: the accumulators
+// then have static lifetimes (the stage machine's switch merged them at the loop head with register
+// copies).  Lanes that finish or fail run on masked, as in rk45().
+#if FW_QUAD_UNROLL
+template <typename T, typename C, typename A>
+__device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx<T>& Q, V2<T> (&Y)[3], V2<T> (&F)[3],
+                                              QRun& R, bool resume) {
+  using V = V2<T>;
+  using namespace dp5;
+  constexpr int NQ = 3;
+  const T rtol = c.rtol, atol = c.atol;
+  const double t_bound = c.t_bound;
+  const T inv_sqrt_n = T(0.22941573387056177);  // 1 / sqrt(19)
+  V ER[NQ], ys[NQ], K[NQ], P2v[NQ], P3[NQ], P4[NQ], P5[NQ], YB[NQ];
+  double t = 0.0, h_abs = 0.0, t_new = 0.0, min_step = 0.0;
+  T ht = T(0);
+  bool rejected = false, active = true, begin_step = false, seeded = false;
+  int result = 0, nfev = 0, nacc = 0;
+  auto iscale = [&](V y) {
+    V s;
+    s.x = frcp(atol + fabs(y.x) * rtol);
+    s.y = frcp(atol + fabs(y.y) * rtol);
+    return s;
+  };
+  auto sq2 = [](V v) { return v.x * v.x + v.y * v.y; };
+  // K = f(ys); false once no lane of the wave integrates any more
+  auto eval = [&](bool first) {
+    const int term = rhs_quad(c, a, Q, first, (const T*)ys, (T*)K);
+    if (active) {
+      nfev++;
+      if (term) {
+        result = term;
+        active = false;
+      } else if (nfev >= c.max_nfev) {
+        result = -2;
+        active = false;
+      }
+    }
+    return any_lane(active);
+  };
+  auto seed = [&]() {  // stage-1 input and accumulators of a trial step
+#pragma unroll
+    for (int p = 0; p < NQ; p++) {
+      const V f = F[p];
+      ys[p] = Y[p] + (f * T(A10)) * ht;
+      P2v[p] = f * T(A20);
+      P3[p] = f * T(A30);
+      P4[p] = f * T(A40);
+      P5[p] = f * T(A50);
+      YB[p] = f * T(B0);
+      ER[p] = f * T(E0);
+    }
+  };
+  if (resume) {
+    t = R.t;
+    t_new = R.t_new;
+    h_abs = R.h_abs;
+    min_step = R.min_step;
+    rejected = R.rejected != 0;
+    nfev = R.nfev;
+    nacc = R.nacc;
+    ht = (T)(t_new - t);
+    seed();
+    seeded = true;
+  } else {
+#pragma unroll
+    for (int p = 0; p < NQ; p++) ys[p] = Y[p];
+    if (!eval(true)) goto done;
+    T d1;
+    double h0;
+    {  // f0; select_initial_step (common.py:68-110)
+      T d0s = T(0), d1s = T(0);
+#pragma unroll
+      for (int p = 0; p < NQ; p++) {
+        F[p] = K[p];
+        const V isc = iscale(Y[p]);
+        d0s += sq2(Y[p] * isc);
+        d1s += sq2(K[p] * isc);
+      }
+      const T d0 = fsqrt(qd::sum4(d0s)) * inv_sqrt_n;
+      d1 = fsqrt(qd::sum4(d1s)) * inv_sqrt_n;
+      h0 = (d0 < T(1e-5) || d1 < T(1e-5)) ? 1e-6 : 0.01 * (double)d0 / (double)d1;
+      if (h0 > t_bound) h0 = t_bound;
+      const T h0t = (T)h0;
+#pragma unroll
+      for (int p = 0; p < NQ; p++) ys[p] = Y[p] + h0t * F[p];
+    }
+    if (!eval(false)) goto done;
+    {  // probe; select_initial_step (common.py:111-134)
+      T d2s = T(0);
+#pragma unroll
+      for (int p = 0; p < NQ; p++) d2s += sq2((K[p] - F[p]) * iscale(Y[p]));
+      const double d2 = (double)(fsqrt(qd::sum4(d2s)) * inv_sqrt_n) / h0;
+      double h1;
+      if ((double)d1 <= 1e-15 && d2 <= 1e-15) h1 = fmax(1e-6, h0 * 1e-3);
+      else h1 = pow(0.01 / fmax((double)d1, d2), 1.0 / 5.0);
+      h_abs = fmin(fmin(100 * h0, h1), t_bound);
+      begin_step = active;
+    }
+  }
+  for (;;) {
+    if (!seeded) {
+      if (begin_step) {  // RungeKutta._step_impl entry (rk.py:111-124)
+        min_step = 10.0 * fabs(nextafter(t, 1e300) - t);
+        if (h_abs < min_step) h_abs = min_step;
+        rejected = false;
+      }
+      // one trial step (rk.py:126-137)
+      double h = h_abs;
+      t_new = t + h;
+      if (t_new - t_bound > 0) t_new = t_bound;
+      h = t_new - t;
+      h_abs = fabs(h);
+      ht = (T)h;
+      seed();
+    }
+    seeded = false;
+    if (!eval(false)) break;  // K1
+#pragma unroll
+    for (int p = 0; p < NQ; p++) {
+      ys[p] = Y[p] + (P2v[p] + K[p] * T(A21)) * ht;
+      P3[p] += K[p] * T(A31);
+      P4[p] += K[p] * T(A41);
+      P5[p] += K[p] * T(A51);
+    }
+    if (!eval(false)) break;  // K2
+#pragma unroll
+    for (int p = 0; p < NQ; p++) {
+      P3[p] += K[p] * T(A32);
+      P4[p] += K[p] * T(A42);
+      P5[p] += K[p] * T(A52);
+      YB[p] += K[p] * T(B2);
+      ER[p] += K[p] * T(E2);
+      ys[p] = Y[p] + P3[p] * ht;
+    }
+    if (!eval(false)) break;  // K3
+#pragma unroll
+    for (int p = 0; p < NQ; p++) {
+      P4[p] += K[p] * T(A43);
+      P5[p] += K[p] * T(A53);
+      YB[p] += K[p] * T(B3);
+      ER[p] += K[p] * T(E3);
+      ys[p] = Y[p] + P4[p] * ht;
+    }
+    if (!eval(false)) break;  // K4
+#pragma unroll
+    for (int p = 0; p < NQ; p++) {
+      P5[p] += K[p] * T(A54);
+      YB[p] += K[p] * T(B4);
+      ER[p] += K[p] * T(E4);
+      ys[p] = Y[p] + P5[p] * ht;
+    }
+    if (!eval(false)) break;  // K5; ys <- y_new
+#pragma unroll
+    for (int p = 0; p < NQ; p++) {
+      YB[p] += K[p] * T(B5);
+      ER[p] += K[p] * T(E5);
+      ys[p] = Y[p] + ht * YB[p];
+    }
+    if (!eval(false)) break;  // K = f(t_new, y_new): error norm + step control (rk.py:138-173)
+    T es = T(0);
+#pragma unroll
+    for (int p = 0; p < NQ; p++) {
+      const V e = (ER[p] + K[p] * T(E6)) * ht;
+      const V y0 = Y[p], y1 = ys[p];
+      V sc;
+      sc.x = frcp(atol + fmax(fabs(y0.x), fabs(y1.x)) * rtol);
+      sc.y = frcp(atol + fmax(fabs(y0.y), fabs(y1.y)) * rtol);
+      es += sq2(e * sc);
+    }
+    const T en = fsqrt(qd::sum4(es)) * inv_sqrt_n;
+    begin_step = false;
+    if (active) {
+      if (en < T(1)) {
+        double factor = (en == T(0)) ? 10.0 : fmin(10.0, 0.9 * (double)fpow(en, T(-0.2)));
+        if (rejected) factor = fmin(1.0, factor);
+        h_abs *= factor;
+        t = t_new;
+#pragma unroll
+        for (int p = 0; p < NQ; p++) {
+          Y[p] = ys[p];
+          F[p] = K[p];
+        }
+        nacc++;
+        if (t - t_bound >= 0.0) active = false;
+        else begin_step = true;
+      } else {
+        h_abs *= fmax(0.2, 0.9 * (double)fpow(en, T(-0.2)));
+        rejected = true;
+        if (!(h_abs >= min_step)) {  // TOO_SMALL_STEP (or a NaN step size): solver failure
+          result = -1;
+          active = false;
+        }
+      }
+    }
+    if (!any_lane(active)) break;
+  }
+done:
+  R.nfev = nfev;
+  R.nacc = nacc;
+  return result;
+}
+#else
 template <typename T, typename C, typename A>
 __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx<T>& Q, V2<T> (&Y)[3], V2<T> (&F)[3],
                                               QRun& R, bool resume) {
@@ -518,6 +728,7 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
   R.nacc = nacc;
   return result;
 }
+#endif  // FW_QUAD_UNROLL
 
 // a fresh integration of the state y_io (the full 19-element state on every lane of the quad, in and out)
 template <typename T, typename C, typename A>
