@@ -50,6 +50,12 @@ constexpr uint32_t DM_SOLVER_FAIL = 1u << 31;  // sim_step_masked dmask bit: RK4
 #ifndef FW_FOLD_INPLACE
 #define FW_FOLD_INPLACE 1  // stage accumulators seeded at the attempt start, every stage folds in place (-1.5..3% per RK iteration, profiles/r02_ab_fold.log)
 #endif
+#ifndef FW_RK_UNROLL
+#define FW_RK_UNROLL 1  // one-lane rk45: a trial step written out with its six RHS sites (0 = stage machine, A/B)
+#endif
+#if FW_RK_UNROLL && !FW_FOLD_INPLACE
+#error "FW_RK_UNROLL needs FW_FOLD_INPLACE"
+#endif
 #ifndef FW_RELAUNDER
 #define FW_RELAUNDER 0  // 1: re-issue config scalar loads per RHS (helped the generic kernel; -4.5% slower on the specialised one)
 #endif  // RHS evaluations per step before the step is declared a solver failure
@@ -687,6 +693,179 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
   // result, counters) are predicated.  Unpredicated folds keep the stage
   // arrays in place across the wave-uniform stage switch (no phi copies).
   bool handoff = false;
+#if FW_RK_UNROLL
+  // The stage sequence is wave-uniform (f0, probe, then trial steps of exactly six RHS evaluations,
+  // accepted or rejected; see rk45_quad_core): one trial step is written out with its six RHS sites,
+  // so the accumulators have static lifetimes instead of merging at a stage switch.
+  bool begin_step = false;
+  // K = f(ys); false once no lane of the wave integrates any more
+  auto eval = [&](bool first) {
+    const int term = rhs(c, a, X, first, (const T*)ys, (T*)K);
+    K[NP - 1].y = T(0);  // pad element
+    if (active) {
+      nfev++;
+      if (term) {
+        result = term;
+        active = false;
+      }
+      // hard bound on work per step so that no input can keep a wave spinning (scipy has
+      // none; ends the step like its TOO_SMALL_STEP failure, reported in the stats)
+      else if (nfev >= c.max_nfev) {
+        result = -2;
+        active = false;
+      }
+    }
+    return any_lane(active);
+  };
+  if (!eval(true)) goto rk_done;
+  {  // ---- f0; select_initial_step (common.py:68-110)
+    T d0s = T(0), d1s = T(0);
+#pragma unroll
+    for (int p = 0; p < NP; p++) {
+      F(p) = K[p];
+      const V isc = iscale(Y(p));
+      d0s += sq2(Y(p) * isc);
+      d1s += sq2(K[p] * isc);
+    }
+    const T d0 = fsqrt(d0s) * inv_sqrt_n;
+    d1 = fsqrt(d1s) * inv_sqrt_n;
+    h0 = (d0 < T(1e-5) || d1 < T(1e-5)) ? 1e-6 : 0.01 * (double)d0 / (double)d1;
+    if (h0 > t_bound) h0 = t_bound;
+    const T h0t = (T)h0;
+#pragma unroll
+    for (int p = 0; p < NP; p++) ys[p] = Y(p) + h0t * F(p);
+  }
+  if (!eval(false)) goto rk_done;
+  {  // ---- probe; select_initial_step (common.py:111-134)
+    T d2s = T(0);
+#pragma unroll
+    for (int p = 0; p < NP; p++) d2s += sq2((K[p] - F(p)) * iscale(Y(p)));
+    const double d2 = (double)(fsqrt(d2s) * inv_sqrt_n) / h0;
+    double h1;
+    if ((double)d1 <= 1e-15 && d2 <= 1e-15) h1 = fmax(1e-6, h0 * 1e-3);
+    else h1 = pow(0.01 / fmax((double)d1, d2), 1.0 / 5.0);
+    h_abs = fmin(fmin(100 * h0, h1), t_bound);
+    begin_step = active;
+  }
+  for (;;) {
+    if (begin_step) {  // RungeKutta._step_impl entry (rk.py:111-124)
+      min_step = 10.0 * fabs(nextafter(t, 1e300) - t);
+      if (h_abs < min_step) h_abs = min_step;
+      rejected = false;
+    }
+    {  // one trial step (rk.py:126-137); stage 1 input, accumulators seeded
+      double h = h_abs;
+      t_new = t + h;
+      if (t_new - t_bound > 0) t_new = t_bound;
+      h = t_new - t;
+      h_abs = fabs(h);
+      ht = (T)h;
+#pragma unroll
+      for (int p = 0; p < NP; p++) {
+        const V f = F(p);
+        ys[p] = Y(p) + (f * T(A10)) * ht;
+        P2v[p] = f * T(A20);
+        PA(P3, p) = f * T(A30);
+        PA(P4, p) = f * T(A40);
+        PA(P5, p) = f * T(A50);
+        PA(YB, p) = f * T(B0);
+        ERV(p) = f * T(E0);
+      }
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (HO && FW_TAIL_QUAD > 0) {  // every integrating lane is at the start of a trial step
+      const unsigned long long am = __ballot(active);
+      const int na = __popcll(am);  // (lanes of the wave's aircraft past N have returned: quads need 4 na live lanes)
+      if (na > 0 && na <= c.tail_quad && 4 * na <= __popcll(__ballot(true))) {
+        handoff = true;
+        break;
+      }
+    }
+#endif
+    if (!eval(false)) break;  // K1
+#pragma unroll
+    for (int p = 0; p < NP; p++) {
+      ys[p] = Y(p) + (P2v[p] + K[p] * T(A21)) * ht;
+      PA(P3, p) += K[p] * T(A31);
+      PA(P4, p) += K[p] * T(A41);
+      PA(P5, p) += K[p] * T(A51);
+    }
+    if (!eval(false)) break;  // K2
+#pragma unroll
+    for (int p = 0; p < NP; p++) {
+      PA(P3, p) += K[p] * T(A32);
+      PA(P4, p) += K[p] * T(A42);
+      PA(P5, p) += K[p] * T(A52);
+      PA(YB, p) += K[p] * T(B2);
+      ERV(p) += K[p] * T(E2);
+      ys[p] = Y(p) + PA(P3, p) * ht;
+    }
+    if (!eval(false)) break;  // K3
+#pragma unroll
+    for (int p = 0; p < NP; p++) {
+      PA(P4, p) += K[p] * T(A43);
+      PA(P5, p) += K[p] * T(A53);
+      PA(YB, p) += K[p] * T(B3);
+      ERV(p) += K[p] * T(E3);
+      ys[p] = Y(p) + PA(P4, p) * ht;
+    }
+    if (!eval(false)) break;  // K4
+#pragma unroll
+    for (int p = 0; p < NP; p++) {
+      PA(P5, p) += K[p] * T(A54);
+      PA(YB, p) += K[p] * T(B4);
+      ERV(p) += K[p] * T(E4);
+      ys[p] = Y(p) + PA(P5, p) * ht;
+    }
+    if (!eval(false)) break;  // K5; ys <- y_new
+#pragma unroll
+    for (int p = 0; p < NP; p++) {
+      PA(YB, p) += K[p] * T(B5);
+      ERV(p) += K[p] * T(E5);
+      ys[p] = Y(p) + ht * PA(YB, p);
+    }
+    if (!eval(false)) break;  // K = f(t_new, y_new): error norm + step control (rk.py:138-173)
+    {
+      T es = T(0);
+#pragma unroll
+      for (int p = 0; p < NP; p++) {
+        const V e = (ERV(p) + K[p] * T(E6)) * ht;
+        const V y0 = Y(p), y1 = ys[p];
+        V sc;
+        sc.x = frcp(atol + fmax(fabs(y0.x), fabs(y1.x)) * rtol);
+        sc.y = frcp(atol + fmax(fabs(y0.y), fabs(y1.y)) * rtol);
+        es += sq2(e * sc);
+      }
+      const T en = fsqrt(es) * inv_sqrt_n;
+      begin_step = false;
+      if (active) {
+        if (en < T(1)) {
+          double factor = (en == T(0)) ? 10.0 : fmin(10.0, 0.9 * (double)fpow(en, T(-0.2)));
+          if (rejected) factor = fmin(1.0, factor);
+          h_abs *= factor;
+          t = t_new;
+#pragma unroll
+          for (int p = 0; p < NP; p++) {
+            Y(p) = ys[p];
+            F(p) = K[p];
+          }
+          nacc++;
+          if (t - t_bound >= 0.0) active = false;  // OdeSolver.step: finished (base.py:203-204)
+          else begin_step = true;
+        } else {
+          h_abs *= fmax(0.2, 0.9 * (double)fpow(en, T(-0.2)));
+          rejected = true;
+          if (!(h_abs >= min_step)) {  // TOO_SMALL_STEP (or a NaN step size): solver failure
+            result = -1;
+            active = false;
+          }
+        }
+      }
+    }
+    if (!any_lane(active)) break;
+  }
+rk_done:
+#else
   for (int stage = 0;;) {
     if (!any_lane(active)) break;
 #if FW_Y_PREFETCH
@@ -881,6 +1060,7 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
     }
 #endif
   }
+#endif  // FW_RK_UNROLL
 #if defined(__HIP_DEVICE_COMPILE__)
   if constexpr (HO && FW_TAIL_QUAD > 0) {
     if (handoff) {
