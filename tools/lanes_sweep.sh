@@ -19,6 +19,9 @@ PY
 }
 for N in 8192 16384 32768 65536; do line auto_$N -- --envs $N; done
 line lanes1_8192 -- --envs 8192 --lanes 1
+line lanes1_16384 -- --envs 16384 --lanes 1
 line lanes4_32768 -- --envs 32768 --lanes 4
 line nohandoff_65536 FWSIM_TAIL_QUAD=0 -- --envs 65536
 line nohandoff_8192_lanes1 FWSIM_TAIL_QUAD=0 -- --envs 8192 --lanes 1
+line auto_131072 -- --envs 131072
+line auto_262144 -- --envs 262144
