@@ -160,13 +160,16 @@ def rollout_leg(spec, n, T, dev, rank, world, precision):
     policy = MlpActorCritic(env.observation_space.shape[0], env.action_space.shape[0]).to(dev)
     buf = RolloutBuffer(T, env.observation_space, env.action_space, device=dev, gae_lambda=0.95, gamma=0.99, n_envs=n)
     col = RolloutCollector(env, policy, buf)
+    graph = world == 1  # one captured collect step replayed per step (RolloutCollector.collect(graph=True))
     col.collect(min(T, 16))  # warm-up (kernels, allocator, RCCL communicator)
+    if graph:
+        col.collect(min(T, 16), graph=True)  # captures the step graph
     buf.all_gather()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    col.collect()
+    col.collect(graph=graph)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     gathered = buf.all_gather()
@@ -182,7 +185,7 @@ def rollout_leg(spec, n, T, dev, rank, world, precision):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     collect_s, gather_s, total_s, gae_ms = [float(x) for x in t]
     gae_bytes = (4 + 4 + 1 + 4 + 4) * T * n + (4 + 1) * n
-    out = {"horizon": T, "envs_per_gpu": n, "global_envs": n * world, "collect_s": collect_s,
+    out = {"horizon": T, "envs_per_gpu": n, "global_envs": n * world, "collect_graphed": graph, "collect_s": collect_s,
            "allgather_s": gather_s if world > 1 else 0.0, "env_steps_per_s": n * world * T / total_s,
            "gathered_bytes_per_gpu": sum(s.numel() * 4 for s in gathered.slabs),
            "gae_kernel": {"ms": gae_ms, "bytes": gae_bytes, "achieved_GBs": gae_bytes / (gae_ms * 1e-3) / 1e9,

@@ -418,6 +418,59 @@ def test_partial_collect_bootstraps_at_last_stored_row():
     env.close()
 
 
+def test_graphed_collect_equals_eager():
+    """collect(graph=True) (one captured step replayed, buffer writes by fw_replay_add) stores the same
+    rollout as the eager collect: bit for bit with a deterministic policy, over auto-resets and
+    VecNormalize updates, on two consecutive collections; with the stochastic policy the graphed
+    rollout's GAE equals the oracle's."""
+    from tum_adlr_deep_reinforcement_learning_amd.rollout import MlpActorCritic, RolloutBuffer, RolloutCollector
+    from tum_adlr_deep_reinforcement_learning_amd.vec_env import FixedWingVecEnv
+    from tum_adlr_deep_reinforcement_learning_amd.vec_normalize import VecNormalize
+
+    class Det(MlpActorCritic):
+        def forward(self, obs, deterministic=True):
+            return super().forward(obs, deterministic=True)
+
+    n, T = 4096, 48
+
+    def make(cls):
+        torch.manual_seed(5)
+        venv = FixedWingVecEnv(n, config_kw={"steps_max": 30}, sim_config_kw={"turbulence": False}, device=DEV,
+                               seed=21, return_tensors=True, info_target=False)
+        env = VecNormalize(venv)
+        policy = cls(env.observation_space.shape[0], env.action_space.shape[0]).to(DEV)
+        buf = RolloutBuffer(T, env.observation_space, env.action_space, device=DEV, gae_lambda=0.95, gamma=0.99,
+                            n_envs=n)
+        return venv, env, buf, RolloutCollector(env, policy, buf)
+
+    va, ea, ba, ca = make(Det)
+    vb, eb, bb, cb = make(Det)
+    ca.collect(8)
+    cb.collect(8)
+    for _ in range(2):
+        ca.collect()
+        cb.collect(graph=True)
+        for f in ("slab", "rewards", "dones"):
+            assert torch.equal(getattr(ba, f), getattr(bb, f)), f
+        assert torch.equal(ca.last_obs, cb.last_obs) and torch.equal(ca.last_dones, cb.last_dones)
+        assert torch.equal(ea.rms, eb.rms) and torch.equal(ea.ret, eb.ret)
+    assert bb.dones.sum() > 0  # auto-resets inside the horizon
+    va.close()
+    vb.close()
+
+    vs, es, bs, cs = make(MlpActorCritic)
+    cs.collect(8)
+    cs.collect(graph=True)
+    with torch.no_grad():
+        lv = cs.policy.predict_values(cs.last_obs).reshape(-1).cpu().numpy()
+    a_ref, r_ref = R.gae(bs.rewards.cpu().numpy(), bs.values.cpu().numpy(), bs.dones.cpu().numpy(), lv,
+                         cs.last_dones.cpu().numpy(), 0.99, 0.95)
+    assert np.array_equal(bs.advantages.cpu().numpy(), a_ref)
+    assert bool(torch.isfinite(bs.slab).all()) and float(bs.observations.abs().max()) <= 10.0
+    assert float(bs.log_probs.abs().max()) > 0
+    vs.close()
+
+
 # ---------------------------------------------------------------------------- open-loop rollout kernel
 @pytest.mark.parametrize("lanes", [1, 4])
 @pytest.mark.parametrize("precision", ["float64", "float32"])

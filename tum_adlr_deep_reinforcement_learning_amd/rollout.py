@@ -235,11 +235,17 @@ class RolloutCollector:
         self.last_dones = torch.zeros(env.num_envs, dtype=torch.uint8, device=dev)
 
     @torch.no_grad()
-    def collect(self, n_rollout_steps=None):
+    def collect(self, n_rollout_steps=None, graph=False):
+        """``graph=True``: the step body (policy forward, action clip, env step incl. VecNormalize) is
+        captured once into a HIP graph and replayed per step, with the buffer writes of a step done by
+        one ``fw_replay_add`` launch (2 launches per step instead of ~30); same kernels, same results.
+        Single-process only (a sharded VecNormalize all-gathers per step: eager path)."""
         buf, env = self.buffer, self.env
         n = n_rollout_steps or buf.buffer_size
         if self.last_obs is None:
             self.last_obs = env.reset()
+        if graph and self._graph_ok():
+            return self._collect_graphed(n)
         buf.reset()
         for t in range(n):
             obs_slot = buf.observations[t]
@@ -257,4 +263,83 @@ class RolloutCollector:
         buf.pos, buf.full = n, n == buf.buffer_size
         last_values = self.policy.predict_values(self.last_obs)
         buf.compute_returns_and_advantage(last_values, self.last_dones)
+        self._eager_done = True
         return buf
+
+    # ------------------------------------------------------------ graphed collection
+    def _graph_ok(self):
+        import torch.distributed as dist
+        buf = self.buffer
+        if buf.device.type != "cuda" or buf.n_envs % 4:  # fw_replay_add moves whole dwords
+            return False
+        return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+
+    def _capture(self):
+        """Capture one collect step on static tensors: s_obs (the observation the policy acts on, then
+        the next one), s_start (episode starts: the last dones), and the step's outputs."""
+        buf, env, dev = self.buffer, self.env, self.buffer.device
+        N, D, A = buf.n_envs, buf.obs_dim, buf.action_dim
+        self.s_obs = torch.empty(N, D, dtype=torch.float32, device=dev)
+        self.s_start = torch.empty(N, dtype=torch.uint8, device=dev)
+        self.s_act = torch.empty(N, A, dtype=torch.float32, device=dev)
+        self.s_rew = torch.empty(N, dtype=torch.float32, device=dev)
+        self.s_val = torch.empty(N, dtype=torch.float32, device=dev)
+        self.s_logp = torch.empty(N, dtype=torch.float32, device=dev)
+
+        def body():
+            actions, values, log_probs = self.policy(self.s_obs)
+            clipped = torch.max(torch.min(actions, self.high), self.low)
+            new_obs, rewards, dones, _ = env.step(clipped)
+            self.s_act.copy_(actions)
+            self.s_val.copy_(values.reshape(-1))
+            self.s_logp.copy_(log_probs)
+            self.s_rew.copy_(rewards)
+            self.s_obs.copy_(new_obs.reshape(N, D))
+            self.s_start.copy_(dones)
+
+        # kernels, the policy's BLAS handles and the allocator were warmed by an eager collect(); the
+        # capture itself records only, so no env state moves here
+        if not getattr(self, "_eager_done", False):
+            raise RuntimeError("collect(graph=True): run one eager collect() first (warms kernels outside the capture)")
+        self._graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._graph):
+            body()
+        self._segs = (_native.FwCopySeg * 6)()
+
+    def _collect_graphed(self, n):
+        buf = self.buffer
+        if getattr(self, "_graph", None) is None:
+            self._capture()
+        dev = buf.device
+        N, D, A = buf.n_envs, buf.obs_dim, buf.action_dim
+        buf.reset()
+        self.s_obs.copy_(self.last_obs.reshape(N, D))
+        self.s_start.copy_(self.last_dones)
+        lib, st = _native.load(), _stream(dev)
+        segs = self._segs
+
+        def store(t, prev):
+            """one launch: the inputs of step t (obs, episode start) and the outputs of step prev"""
+            k = 0
+            if t is not None:
+                for src, dst in ((self.s_obs, buf.observations[t]), (self.s_start, buf.dones[t])):
+                    segs[k].src, segs[k].dst, segs[k].bytes = src.data_ptr(), dst.data_ptr(), dst.numel() * dst.element_size()
+                    k += 1
+            if prev is not None:
+                for src, dst in ((self.s_act, buf.actions[prev]), (self.s_rew, buf.rewards[prev]),
+                                 (self.s_val, buf.values[prev]), (self.s_logp, buf.log_probs[prev])):
+                    segs[k].src, segs[k].dst, segs[k].bytes = src.data_ptr(), dst.data_ptr(), dst.numel() * dst.element_size()
+                    k += 1
+            _native.check(lib.fw_replay_add(segs, k, st), "fw_replay_add")
+
+        for t in range(n):
+            store(t, t - 1 if t else None)
+            self._graph.replay()
+        store(None, n - 1)
+        self.last_obs = self.s_obs.clone().reshape(self.last_obs.shape)
+        self.last_dones = self.s_start.clone()
+        buf.pos, buf.full = n, n == buf.buffer_size
+        last_values = self.policy.predict_values(self.last_obs)
+        buf.compute_returns_and_advantage(last_values, self.last_dones)
+        return buf
+
