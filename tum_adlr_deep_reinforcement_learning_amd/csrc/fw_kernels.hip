@@ -69,6 +69,9 @@ constexpr int BLOCK = FW_BLOCK;
 #define FW_QUAD_MIN_WAVES 1  // ... of their quad (Q = 4) instances
 #endif
 #define FW_WAVES(Q) ((Q) == 4 ? FW_QUAD_MIN_WAVES : FW_MIN_WAVES)
+#ifndef FW_PREF_Q1
+#define FW_PREF_Q1 0  // 1: the one-lane k_env_step instances prefetch the epilogue's loads too (A/B)
+#endif
 #ifndef FW_LDS_STATE
 #define FW_LDS_STATE 1  // 0 = y/f in VGPRs (measured: 512 VGPRs + spills, slower)
 #endif
@@ -1073,7 +1076,7 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_env_step(const DevCfg<T>
   __shared__ V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];  // y, f (+ error sum) of the block's aircraft (pairs)
   static_assert(Q != 1 || RP || FW_TAIL_QUAD == 0 || BLOCK == 64, "the tail handoff works per one-wave block");
   __shared__ qd::HoSlot<T> ho[Q == 1 && !RP ? BLOCK : 1];
-  env_step_lane<T, C, RP, Q, (Q == 4)>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out,
+  env_step_lane<T, C, RP, Q, (Q == 4 || FW_PREF_Q1)>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out,
                                                   episode_out, stats, auto_reset, (int)(tid % Q), ho);
 }
 
