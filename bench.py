@@ -398,8 +398,10 @@ def main():
     ap.add_argument("--no-open-loop", action="store_true", help="skip the open-loop rollout line (fw_env_rollout)")
     ap.add_argument("--long-window", type=int, default=1000,
                     help="after the timed steps, time this many more for the long-window steady-state line")
-    ap.add_argument("--rollout-steps", type=int, default=0,
-                    help="also run one PPO collect_rollouts of this horizon (2048 = BASELINE configs[2]/[3])")
+    ap.add_argument("--rollout-steps", type=int, default=-1,
+                    help="also run one PPO collect_rollouts of this horizon (2048 = BASELINE configs[2]/[3]); "
+                         "default: 64 on N > 1 GPUs (configs[3]: sharded collection + the RCCL all-gather), "
+                         "none on one")
     ap.add_argument("--sac-fill-steps", type=int, default=0,
                     help="also run a SAC replay-buffer fill of this many steps (BASELINE configs[4])")
     ap.add_argument("--sac-envs", type=int, default=262144, help="global envs of the SAC fill leg")
@@ -459,6 +461,8 @@ def main():
                      "source": "profiles/pmc_env_step.json (SQ_INSTS_VALU, steady-state dispatches)"}
 
     rollout = None
+    if args.rollout_steps < 0:
+        args.rollout_steps = 64 if world > 1 else 0
     if args.rollout_steps > 0:
         rollout = rollout_leg(spec, n, args.rollout_steps, dev, rank, world, args.precision)
     sac = None
