@@ -239,7 +239,9 @@ class RolloutCollector:
         """``graph=True``: the step body (policy forward, action clip, env step incl. VecNormalize) is
         captured once into a HIP graph and replayed per step, with the buffer writes of a step done by
         one ``fw_replay_add`` launch (2 launches per step instead of ~30); same kernels, same results.
-        Single-process only (a sharded VecNormalize all-gathers per step: eager path)."""
+        Single-process only (a sharded VecNormalize all-gathers per step: eager path).  The captured
+        step reads the policy's parameters in place, so optimiser steps between collections are seen;
+        a collector whose policy or env object is replaced must be rebuilt."""
         buf, env = self.buffer, self.env
         n = n_rollout_steps or buf.buffer_size
         if self.last_obs is None:
@@ -277,6 +279,10 @@ class RolloutCollector:
     def _capture(self):
         """Capture one collect step on static tensors: s_obs (the observation the policy acts on, then
         the next one), s_start (episode starts: the last dones), and the step's outputs."""
+        # kernels, the policy's BLAS handles and the allocator were warmed by an eager collect(); the
+        # capture itself records only, so no env state moves here
+        if not getattr(self, "_eager_done", False):
+            raise RuntimeError("collect(graph=True): run one eager collect() first (warms kernels outside the capture)")
         buf, env, dev = self.buffer, self.env, self.buffer.device
         N, D, A = buf.n_envs, buf.obs_dim, buf.action_dim
         self.s_obs = torch.empty(N, D, dtype=torch.float32, device=dev)
@@ -297,10 +303,6 @@ class RolloutCollector:
             self.s_obs.copy_(new_obs.reshape(N, D))
             self.s_start.copy_(dones)
 
-        # kernels, the policy's BLAS handles and the allocator were warmed by an eager collect(); the
-        # capture itself records only, so no env state moves here
-        if not getattr(self, "_eager_done", False):
-            raise RuntimeError("collect(graph=True): run one eager collect() first (warms kernels outside the capture)")
         self._graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._graph):
             body()
