@@ -40,6 +40,13 @@ from tum_adlr_deep_reinforcement_learning_amd import config as C  # noqa: E402
 from tum_adlr_deep_reinforcement_learning_amd.engine import Engine, StepGraph  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md: 8.0 TB/s spec)
+_T0 = time.time()
+
+
+def _log(msg):
+    """Progress on stderr (rank 0): the JSON line stays the only stdout output."""
+    if os.environ.get("RANK", "0") == "0":
+        print("[bench %7.1fs] %s" % (time.time() - _T0, msg), file=sys.stderr, flush=True)
 
 
 def algorithmic_bytes_per_env_step(spec, esz=4):
@@ -155,15 +162,16 @@ def rollout_leg(spec, n, T, dev, rank, world, precision):
     from tum_adlr_deep_reinforcement_learning_amd.vec_normalize import VecNormalize
     torch.manual_seed(rank)
     venv = FixedWingVecEnv(n, sim_config_kw={"turbulence": False}, device=dev, precision=precision, seed=1234,
-                           env_offset=rank * n, return_tensors=True, info_target=False)
+                           env_offset=rank * n, return_tensors=True, info_target=False, global_envs=n * world)
     env = VecNormalize(venv)
     policy = MlpActorCritic(env.observation_space.shape[0], env.action_space.shape[0]).to(dev)
     buf = RolloutBuffer(T, env.observation_space, env.action_space, device=dev, gae_lambda=0.95, gamma=0.99, n_envs=n)
     col = RolloutCollector(env, policy, buf)
-    graph = world == 1  # one captured collect step replayed per step (RolloutCollector.collect(graph=True))
+    # the collect step is replayed from HIP graphs (RolloutCollector.collect(graph=True)): one graph per step
+    # on one GPU; on N > 1 two graphs around the per-step RCCL all-gather of the VecNormalize moments
+    graph = True
     col.collect(min(T, 16))  # warm-up (kernels, allocator, RCCL communicator)
-    if graph:
-        col.collect(min(T, 16), graph=True)  # captures the step graph
+    col.collect(min(T, 16), graph=True)  # captures the step graph(s)
     buf.all_gather()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -185,7 +193,8 @@ def rollout_leg(spec, n, T, dev, rank, world, precision):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     collect_s, gather_s, total_s, gae_ms = [float(x) for x in t]
     gae_bytes = (4 + 4 + 1 + 4 + 4) * T * n + (4 + 1) * n
-    out = {"horizon": T, "envs_per_gpu": n, "global_envs": n * world, "collect_graphed": graph, "collect_s": collect_s,
+    out = {"horizon": T, "envs_per_gpu": n, "global_envs": n * world, "collect_graphed": graph,
+           "host_launches_per_step": len(col._graphs) + (1 if len(col._graphs) > 1 else 0), "collect_s": collect_s,
            "allgather_s": gather_s if world > 1 else 0.0, "env_steps_per_s": n * world * T / total_s,
            "gathered_bytes_per_gpu": sum(s.numel() * 4 for s in gathered.slabs),
            "gae_kernel": {"ms": gae_ms, "bytes": gae_bytes, "achieved_GBs": gae_bytes / (gae_ms * 1e-3) / 1e9,
@@ -205,7 +214,8 @@ def sac_fill_leg(n, K, dev, rank, world, precision):
     unit = {i: {"low": -1.0, "high": 1.0} for i in range(3)}
     env = FixedWingVecEnv(n, config_kw={"action": {"scale_space": True, "states": unit}},
                           sim_config_kw={"turbulence": True, "turbulence_intensity": "light"}, device=dev,
-                          precision=precision, seed=4321, env_offset=rank * n, return_tensors=True, info_target=False)
+                          precision=precision, seed=4321, env_offset=rank * n, return_tensors=True, info_target=False,
+                          global_envs=n * world)
     buf = ReplayBuffer(n * (K + 8), env.observation_space, env.action_space, device=dev, n_envs=n)
     col = OffPolicyCollector(env, buf, learning_starts=1 << 62, seed=7 + rank)
     col.collect(8)  # warm-up
@@ -273,43 +283,73 @@ def _pmc_record(n, args, spec):
     return None
 
 
-def timed_env_steps(n, args, spec, dev, rank, world, env_offset, early=True):
+class _Schedule:
+    """The bench's step schedule on one engine: a first eager step, then replays of a HIP graph of ``G``
+    captured ``fw_env_step`` launches (engine.StepGraph: one host call per G steps, so the box's host
+    jitter never leaves the device idle between steps) cycling over a pool of 16 action batches.
+    ``run(k)`` = k // G replays + k % G eager steps on pool[0 .. k % G - 1]; ``actions_of(k)`` lists
+    the pool index of each of those steps (the stats replay walks exactly the same sequence)."""
+    G = 16
+
+    def __init__(self, n, args, spec, dev, rank, env_offset, precision=None):
+        self.eng = Engine(spec.sim, spec, n, device=dev, precision=precision or args.precision, lanes=args.lanes)
+        self.eng.seed(1234, env_offset=env_offset)
+        self.eng.reset()
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(1 + rank)
+        self.pool = torch.rand(16, n, 3, generator=gen, device=dev, dtype=self.eng.dtype) * 2 - 1
+        self.eng.env_step(self.pool[0], stats=False)  # first step eager (kernel load outside the capture)
+        self.graph = StepGraph(self.eng, self.pool)
+        self.done = 1
+
+    def run(self, k):
+        for _ in range(k // self.G):
+            self.graph.replay()
+        for s in range(k % self.G):
+            self.eng.env_step(self.pool[s], stats=False)
+        self.done += k
+
+    def actions_of(self, k):
+        return list(range(self.G)) * (k // self.G) + list(range(k % self.G))
+
+    def close(self):
+        self.eng.close()
+        del self.graph
+
+
+def timed_env_steps(n, args, spec, dev, rank, world, env_offset, early=True, precision=None, replay=False):
     """Steady-state timing of ``args.steps`` env steps of ``n`` aircraft on this rank.
 
-    Returns (elapsed_s, kernel_ms, early_ms) with elapsed/kernel_ms max-reduced over ranks."""
-    eng = Engine(spec.sim, spec, n, device=dev, precision=args.precision, lanes=args.lanes)
+    Returns (elapsed_s, kernel_ms, early_ms, long_ms, window) with elapsed/kernel_ms max-reduced over
+    ranks; ``window`` (replay=True) = the per-launch statistics of a stats-enabled replay of the same
+    steps (window_replay)."""
+    sch = _Schedule(n, args, spec, dev, rank, env_offset, precision)
+    eng = sch.eng
+    _log("timed_env_steps: %d aircraft, %s" % (n, precision or args.precision))
     timed_env_steps.lanes = eng.lanes  # the integrator this shard size runs (fw_set_lanes)
-    eng.seed(1234, env_offset=env_offset)
-    eng.reset()
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(1 + rank)
-    pool = torch.rand(16, n, 3, generator=gen, device=dev, dtype=eng.dtype) * 2 - 1
-    # the steps are issued as replays of a HIP graph of G captured launches (engine.StepGraph): one host
-    # call per G steps, so the box's host jitter never leaves the device idle between steps
-    G = 16
-    eng.env_step(pool[0], stats=False)  # first step eager (kernel load outside the capture)
-    graph = StepGraph(eng, pool)
-    done_steps = 1
-
-    def run(k):
-        for _ in range(k // G):
-            graph.replay()
-        for s in range(k % G):
-            eng.env_step(pool[s], stats=False)
-
     stream = torch.cuda.current_stream(dev)
     early_ms = None
+    plan = []  # (phase, steps) in order, for the replay
     if early:  # early-episode regime: the first 96 steps after the global reset (no stragglers yet)
         torch.cuda.synchronize(dev)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
-        run(96)
+        sch.run(96)
         b.record(stream)
         torch.cuda.synchronize(dev)
         early_ms = a.elapsed_time(b) / 96
-        done_steps += 96
-    run(max(args.prep - done_steps, 0))  # steady-state population (DESIGN.md 5)
-    run(args.warmup)
+        plan.append(("early", 96))
+    plan.append(("prep", max(args.prep - sch.done, 0)))
+    # steady-state population (DESIGN.md 5).  Progress lines every 192 steps: chunks that are multiples
+    # of the graph length keep exactly the action sequence of one run(prep) call
+    k_prep = plan[-1][1]
+    for k in range(0, k_prep - k_prep % sch.G, 192):
+        sch.run(min(192, k_prep - k_prep % sch.G - k))
+        torch.cuda.synchronize(dev)
+        _log("  prep %d / %d" % (min(k + 192, k_prep), k_prep))
+    sch.run(k_prep % sch.G)
+    plan.append(("warmup", args.warmup))
+    sch.run(args.warmup)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -317,12 +357,15 @@ def timed_env_steps(n, args, spec, dev, rank, world, env_offset, early=True):
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    run(args.steps)
+    sch.run(args.steps)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    _log("  timed window: %.4f ms/step" % (elapsed / args.steps * 1e3))
+    plan.append(("timed", args.steps))
+    obs_after = eng.obs.clone() if replay else None
     # k_env_step device duration per launch: HIP events on the launch stream around the timed steps
     # themselves (graph replays keep the queue full, so this is kernel time plus dispatch gaps)
     kern_ms = ev0.elapsed_time(ev1) / args.steps
@@ -332,16 +375,68 @@ def timed_env_steps(n, args, spec, dev, rank, world, env_offset, early=True):
     if args.long_window > 0:
         l0, l1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         l0.record(stream)
-        run(args.long_window)
+        sch.run(args.long_window)
         l1.record(stream)
         torch.cuda.synchronize(dev)
         long_ms = l0.elapsed_time(l1) / args.long_window
+        plan.append(("long", args.long_window))
+        _log("  long window: %.4f ms/step" % long_ms)
     el = torch.tensor([elapsed, kern_ms, early_ms or 0.0, long_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    eng.close()
-    del graph
-    return float(el[0]), float(el[1]), (float(el[2]) if early else None), float(el[3])
+    sch.close()
+    window = window_replay(n, args, spec, dev, rank, env_offset, precision, plan, obs_after) if replay else None
+    return float(el[0]), float(el[1]), (float(el[2]) if early else None), float(el[3]), window
+
+
+def window_replay(n, args, spec, dev, rank, env_offset, precision, plan, obs_after):
+    """Per-launch statistics of the timed window (and of the long window), OUTSIDE the timed region: a
+    second engine with the same seeds walks the same step schedule; the untimed phases run as before,
+    the ``timed`` and ``long`` phases run eagerly with stats enabled and a HIP event pair around every
+    launch.  Per step it records the launch duration, the largest RHS-evaluation count (and its aircraft),
+    the solver failures and the max_nfev budget hits.  ``bitwise_equal_to_timed_run`` compares the
+    replay's observations after the timed window with the timed engine's."""
+    sch = _Schedule(n, args, spec, dev, rank, env_offset, precision)
+    eng = sch.eng
+    stream = torch.cuda.current_stream(dev)
+    out = {}
+    _log("window replay")
+    for phase, k in plan:
+        if phase not in ("timed", "long"):
+            sch.run(k)
+            continue
+        _log("  replay %s (%d steps)" % (phase, k))
+        rec = torch.zeros(k, 4, dtype=torch.int64, device=dev)  # max nfev, argmax, failures, budget hits
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(k)]
+        for j, ai in enumerate(sch.actions_of(k)):
+            evs[j][0].record(stream)
+            eng.env_step(sch.pool[ai], stats=True)
+            evs[j][1].record(stream)
+            st = eng.stats
+            nf = (st & 0xFFFF).to(torch.int64)
+            m, am = nf.max(0)
+            rec[j, 0], rec[j, 1] = m, am
+            rec[j, 2] = (st < 0).sum()
+            rec[j, 3] = ((st & (1 << 30)) != 0).sum()
+        torch.cuda.synchronize(dev)
+        ms = np.array([a.elapsed_time(b) for a, b in evs])
+        r = rec.cpu().numpy()
+        top = np.argsort(-ms)[:5]
+        blk = {"steps": k, "launch_ms": {"mean": float(ms.mean()), "p50": float(np.median(ms)),
+                                         "p99": float(np.percentile(ms, 99)), "max": float(ms.max()),
+                                         "sum": float(ms.sum())},
+               "max_nfev": int(r[:, 0].max()), "max_nfev_p50": float(np.median(r[:, 0])),
+               "solver_failures": int(r[:, 2].sum()), "max_nfev_budget_hits": int(r[:, 3].sum()),
+               "slowest_launches": [{"step_in_window": int(j), "launch_ms": round(float(ms[j]), 4),
+                                     "max_nfev": int(r[j, 0]), "env": int(r[j, 1]) + env_offset} for j in top]}
+        if phase == "timed" and obs_after is not None:
+            blk["bitwise_equal_to_timed_run"] = bool(torch.equal(eng.obs, obs_after))
+        out[phase] = blk
+    sch.close()
+    out["source"] = ("stats-enabled replay of the same steps (same seeds, same action sequence) outside the "
+                     "timed region, one HIP event pair per launch (eager launches: the means include each "
+                     "launch's dispatch overhead)")
+    return out
 
 
 def open_loop_leg(n, args, spec, dev, rank, world, env_offset, K=256, launches=4):
@@ -405,6 +500,11 @@ def main():
     ap.add_argument("--sac-fill-steps", type=int, default=0,
                     help="also run a SAC replay-buffer fill of this many steps (BASELINE configs[4])")
     ap.add_argument("--sac-envs", type=int, default=262144, help="global envs of the SAC fill leg")
+    ap.add_argument("--no-replay", action="store_true",
+                    help="skip the stats-enabled replay of the timed window (per-launch times, nfev, budget hits)")
+    ap.add_argument("--no-fp64", action="store_true",
+                    help="skip the secondary line at the reference's own precision (fp64 kernels)")
+    ap.add_argument("--fp64-prep", type=int, default=200, help="untimed steps before the fp64 line's window")
     ap.add_argument("--lanes", type=int, default=0,
                     help="lanes per aircraft of k_env_step: 0 = automatic by shard size, 1, or 4 (quad integrator)")
     args = ap.parse_args()
@@ -424,6 +524,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_procs)
+        _log("cpu baseline done")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -433,18 +534,36 @@ def main():
     spec = C.EnvSpec(sim_config_kw={"turbulence": bool(args.turbulence), "turbulence_intensity": "light"})
     spec.metrics_enabled = not args.no_metrics
     n = args.envs // world  # strong scaling: the global batch is split over the GPUs
-    elapsed, kern_ms, early_ms, long_ms = timed_env_steps(n, args, spec, dev, rank, world, rank * n)
+    elapsed, kern_ms, early_ms, long_ms, window = timed_env_steps(n, args, spec, dev, rank, world, rank * n,
+                                                                  replay=not args.no_replay)
     lanes = timed_env_steps.lanes
     value = args.envs * args.steps / elapsed
 
     weak = None
     if world > 1 and not args.no_weak:  # secondary: 65536 aircraft per GPU
         nw = 65536
-        w_el, w_k, _, _ = timed_env_steps(nw, args, spec, dev, rank, world, rank * nw, early=False)
+        w_el, w_k, _, _, _ = timed_env_steps(nw, args, spec, dev, rank, world, rank * nw, early=False)
         weak = {"envs_per_gpu": nw, "global_envs": nw * world, "value": nw * world * args.steps / w_el,
                 "ms_per_step": w_el / args.steps * 1e3, "kernel_ms": w_k}
 
+    _log("open-loop leg")
     open_loop = None if args.no_open_loop else open_loop_leg(n, args, spec, dev, rank, world, rank * n)
+
+    fp64 = None
+    if not args.no_fp64 and args.precision == "float32":  # secondary: the reference's own precision
+        _log("fp64 line")
+        # bounded: the fp64 kernels are 512-register instances with scratch spills whose straggler tail
+        # costs orders of magnitude more than fp32, so a 1000-step prep would take minutes
+        a64 = argparse.Namespace(**vars(args))
+        a64.prep, a64.long_window = args.fp64_prep, 0
+        f_el, f_k, f_early, _, _ = timed_env_steps(n, a64, spec, dev, rank, world, rank * n, precision="float64")
+        fp64 = {"dtype": "f64", "value": args.envs * args.steps / f_el, "ms_per_step": f_el / args.steps * 1e3,
+                "kernel_ms": f_k, "prep_steps": a64.prep, "steps": args.steps,
+                "early_regime": {"steps": 96, "kernel_ms": f_early,
+                                 "env_steps_per_s_per_gpu": n / (f_early * 1e-3)},
+                "note": "window after %d steps (not the fp32 line's 1000): the fp64 straggler tail is "
+                        "spill-bound, see DESIGN.md" % a64.prep,
+                "isa": "profiles/r03_isa_resources.txt (VGPR / spill counts per kernel instance)"}
 
     esz = 4 if args.precision == "float32" else 8
     rd, wr = algorithmic_bytes_per_env_step(spec, esz)
@@ -458,7 +577,8 @@ def main():
                      "unit": "Ginst/s (wave64 VALU issue)", "frac": valu_rate / VALU_ISSUE_PEAK,
                      "valu_insts_per_launch": pm["valu_insts_per_launch"],
                      "valu_insts_per_wave": pm["valu_insts_per_launch"] * 64.0 / n,
-                     "source": "profiles/pmc_env_step.json (SQ_INSTS_VALU, steady-state dispatches)"}
+                     "source": "SQ_INSTS_VALU per steady-state dispatch from profiles/pmc_env_step.json (a long "
+                               "window of the same workload) over this window's kernel_ms"}
 
     rollout = None
     if args.rollout_steps < 0:
@@ -496,14 +616,20 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_env_step": rd + wr, "kernel_ms": kern_ms,
+                         "traffic_source": ("profiles/pmc_env_step.json: FETCH_SIZE+WRITE_SIZE per steady-state "
+                                            "dispatch of the same workload over a long window, not this K-step "
+                                            "window" if traffic is not None else None),
                          "binding_limit": "valu issue + RK45 straggler latency (see roofline_valu, DESIGN.md 3)"},
             "roofline_valu": roof_valu,
             "early_regime": {"steps": 96, "kernel_ms": early_ms, "env_steps_per_s_per_gpu": n / (early_ms * 1e-3)},
             "long_window": ({"steps": args.long_window, "kernel_ms": long_ms,
                              "env_steps_per_s": args.envs / (long_ms * 1e-3)} if long_ms > 0 else None),
+            "window": window,
             "cpu_baseline": cpu,
             "cpu_baseline_reference": REFERENCE_CPU,
         }
+        if fp64 is not None:
+            out["fp64"] = fp64
         if open_loop is not None:
             out["open_loop_rollout"] = open_loop
         if weak is not None:

@@ -18,6 +18,8 @@
  *   fw_vecnorm_apply  VecNormalize.step_wait's normalisation + return reset
  *                     stable_baselines3/common/vec_env/vec_normalize.py:106-131, 133-169
  *   fw_replay_add     ReplayBuffer.add   stable_baselines3/common/buffers.py:222-235
+ *   fw_rollout_store  RolloutBuffer.add  stable_baselines3/common/buffers.py:335-361, with the row
+ *                     index on the device so a captured collect step stores its own row
  */
 #ifndef FWROLLOUT_H
 #define FWROLLOUT_H
@@ -79,6 +81,22 @@ typedef struct fw_copy_seg {
   int64_t bytes;
 } fw_copy_seg;
 int fw_replay_add(const fw_copy_seg* segs, int32_t n_segs, void* stream);
+
+/* RolloutBuffer.add (stable_baselines3/common/buffers.py:335-361) as a graph-capturable launch: the
+ * buffer row comes from device memory, ctrl_dev = {row, n_rows} (int32).  Segment k copies `bytes`
+ * from src to dst + (row + row_off) * stride, skipped when row + row_off is outside [0, n_rows);
+ * then, if advance != 0, ctrl_dev[0] += 1 (a second, single-thread launch on the same stream).
+ * A captured collect step replays the same launch every step and still fills row t at step t.
+ * Ranges must not overlap; bytes % 4 == 0. */
+typedef struct fw_row_seg {
+  const void* src;
+  void* dst;
+  int64_t bytes;
+  int64_t stride;
+  int32_t row_off;
+  int32_t pad;
+} fw_row_seg;
+int fw_rollout_store(const fw_row_seg* segs, int32_t n_segs, int32_t* ctrl_dev, int32_t advance, void* stream);
 
 #ifdef __cplusplus
 }

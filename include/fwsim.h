@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FWSIM_ABI_VERSION 5
+#define FWSIM_ABI_VERSION 6
 
 /* ---- error codes ---------------------------------------------------------- */
 #define FW_OK 0
@@ -119,7 +119,7 @@ typedef struct fw_sim_config {
   int32_t disabled_inputs;           /* bit0 elevator, bit1 aileron: "disabled" ControlVariables,
                                         whose .value is 0 after reset (pyfly.py:359-363) */
   int32_t wind_random;               /* 1: steady wind magnitude sampled in [mag_min, mag_max] */
-  int32_t max_nfev;                  /* RHS-evaluation budget of one step (0 = 6000).  scipy has none;
+  int32_t max_nfev;                  /* RHS-evaluation budget of one step (0 = 1000000).  scipy has none;
                                         exhausting it ends the step like solve_ivp's TOO_SMALL_STEP
                                         failure: sol.y[:, -1] (the last accepted sub-step) is committed
                                         and the step counts as a success (pyfly.py:1393-1396).       */
@@ -293,9 +293,11 @@ int fw_reset(fw_handle* h, const uint8_t* mask_dev, const void* init_dev, const 
 /* PyFly.step for all envs.  commands_dev: [N][3] in actuation-input order
  * (elevator, aileron, throttle).  Outputs (NULL = skip): commands_out_dev [N][3]
  * constrained commands, success_dev uint8[N], term_dev int32[N] (FW_TERM_*),
- * stats_dev int32[N] = nfev | (n_accepted << 16), bit 31 set when the RK45
- * integration failed (TOO_SMALL_STEP or the max_nfev budget) and the last
- * accepted sub-step was committed, as solve_ivp's sol.y[:, -1] is.           */
+ * stats_dev int32[N] = min(nfev, 0xFFFF) | (min(n_accepted, 0x3FFF) << 16);
+ * bit 31 set when the RK45 integration failed (TOO_SMALL_STEP, a NaN step or
+ * the max_nfev budget) and the last accepted sub-step was committed, as
+ * solve_ivp's sol.y[:, -1] is; bit 30 set when that failure was the budget
+ * (FW_STATS_BUDGET: a step scipy would have continued).                       */
 int fw_sim_step(fw_handle* h, const void* commands_dev, void* commands_out_dev, uint8_t* success_dev,
                 int32_t* term_dev, int32_t* stats_dev, void* stream);
 

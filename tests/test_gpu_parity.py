@@ -75,7 +75,7 @@ def _run_single_steps(d, precision, lanes=None):
         dr = eng.get_block(C.FW_BLK_DERIVED).T.cpu().numpy()
         st = eng.stats.cpu().numpy()
         for j, i in enumerate(idx):
-            out[i] = dict(y=y[j], der=dr[j], term=int(term[j]), nfev=int(st[j] & 0xFFFF), nacc=int((st[j] >> 16) & 0x7FFF),
+            out[i] = dict(y=y[j], der=dr[j], term=int(term[j]), nfev=int(st[j] & 0xFFFF), nacc=int((st[j] >> 16) & 0x3FFF),
                           cmd=eng.cmd_out[j].cpu().numpy())
         eng.close()
     return out

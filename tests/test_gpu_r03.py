@@ -1,0 +1,269 @@
+"""GPU tests of round 3, all through the C ABI.
+
+  max_nfev budget     the stats word's budget bit (bit 30) and info["solver_budget_exhausted"] are
+                      set exactly on the steps that end on fw_sim_config.max_nfev; the default budget
+                      is never reached by the bench population
+  RCCL, world 1       an in-process ``nccl`` process group on cuda:0: the VecNormalize moment
+                      all-gather and the rollout-slab all_gather_into_tensor run through RCCL, and a
+                      collection under the group (eager, and graphed as two graphs around the
+                      collective) equals the same collection without a process group, bit for bit
+  configs[3]          emulated on one GPU: eight 8192-aircraft shards at env_offset = r * 8192 collect
+                      the same rollout as one 65536-aircraft batch (slabs concatenated in rank order ==
+                      the 65536 slab, GAE included, bit for bit); eight shard VecNormalize records
+                      merged in rank order == the whole batch's statistics
+  configs[2]          65536 aircraft x the 2048-step PPO horizon, graphed collect: GAE == oracle bit for
+                      bit on a sampled subset of envs (reference: buffers.py:304-333)
+"""
+import socket
+
+import numpy as np
+import pytest
+import torch
+from torch import nn
+
+from oracle import rollout_oracle as R
+from tum_adlr_deep_reinforcement_learning_amd import config as C
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+# ---------------------------------------------------------------------------- max_nfev budget
+def test_budget_bit_surfaced_in_stats_and_info():
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
+    from tum_adlr_deep_reinforcement_learning_amd.vec_env import FixedWingVecEnv
+    n = 256
+    env = FixedWingVecEnv(n, sim_config_kw={"turbulence": False}, device=DEV, seed=5, info_target=False)
+    env.reset()
+    rng = np.random.RandomState(0)
+    # default budget: 40 steps, no step ends on it
+    for _ in range(40):
+        _, _, _, infos = env.step(rng.uniform(-1, 1, (n, 3)))
+        assert not bool(Engine.budget_hits(env.engine.stats).any())
+        assert not any("solver_budget_exhausted" in infos[i] for i in range(n))
+    # a budget of 20 RHS evaluations (a step needs 14-44): the bit marks exactly the budget failures
+    env.spec.sim.max_nfev = 20
+    env.engine.update_config(env.spec.sim, env.spec)
+    hits = 0
+    for _ in range(10):
+        _, _, _, infos = env.step(rng.uniform(-1, 1, (n, 3)))
+        st = env.engine.stats
+        nfev, _, failed = Engine.decode_stats(st)
+        bud = Engine.budget_hits(st)
+        assert torch.equal(bud, failed & (nfev >= 20))
+        assert bool((nfev <= 20).all())
+        b = bud.cpu().numpy()
+        for i in range(n):
+            assert ("solver_budget_exhausted" in infos[i]) == bool(b[i])
+        hits += int(b.sum())
+    assert hits > 0
+    env.close()
+
+
+# ---------------------------------------------------------------------------- RCCL world 1
+class _Det(nn.Module):
+    def __init__(self, d, a):
+        super().__init__()
+        from tum_adlr_deep_reinforcement_learning_amd.rollout import MlpActorCritic
+        self.m = MlpActorCritic(d, a)
+
+    def forward(self, obs):
+        return self.m(obs, deterministic=True)
+
+    def predict_values(self, obs):
+        return self.m.predict_values(obs)
+
+
+def _setup(n, T, seed=21, steps_max=30):
+    from tum_adlr_deep_reinforcement_learning_amd.rollout import RolloutBuffer, RolloutCollector
+    from tum_adlr_deep_reinforcement_learning_amd.vec_env import FixedWingVecEnv
+    from tum_adlr_deep_reinforcement_learning_amd.vec_normalize import VecNormalize
+    torch.manual_seed(5)
+    venv = FixedWingVecEnv(n, config_kw={"steps_max": steps_max}, sim_config_kw={"turbulence": False}, device=DEV,
+                           seed=seed, return_tensors=True, info_target=False)
+    env = VecNormalize(venv)
+    policy = _Det(env.observation_space.shape[0], env.action_space.shape[0]).to(DEV)
+    buf = RolloutBuffer(T, env.observation_space, env.action_space, device=DEV, gae_lambda=0.95, gamma=0.99, n_envs=n)
+    return venv, env, buf, RolloutCollector(env, policy, buf)
+
+
+def _snapshot(env, buf, col):
+    return [t.clone() for t in (buf.slab, buf.rewards, buf.dones, col.last_obs, col.last_dones, env.rms, env.ret)]
+
+
+def test_rccl_world1_collect_equals_no_group():
+    """The same collections first without a process group, then under an nccl group of size 1 on
+    cuda:0, where the VecNormalize moment exchange and the slab gather go through RCCL.  In each, an
+    eager collector and a graphed one (after the same warm-up) store the same rollouts bit for bit over
+    two consecutive collections, and the grouped run equals the group-less one bit for bit.  Under the
+    group the graphed collect is two graphs around the collective (3 host launches per step)."""
+    import torch.distributed as dist
+    n, T = 4096, 48
+    runs = []
+    for grouped in (False, True):
+        if grouped:
+            dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0, world_size=1,
+                                    device_id=torch.device(DEV))
+        try:
+            va, ea, ba, ca = _setup(n, T)
+            vb, eb, bb, cb = _setup(n, T)
+            ca.collect(8)
+            cb.collect(8)
+            snaps = []
+            for _ in range(2):
+                ca.collect()
+                cb.collect(graph=True)
+                sa, sb = _snapshot(ea, ba, ca), _snapshot(eb, bb, cb)
+                for x, y in zip(sa, sb):
+                    assert torch.equal(x, y)
+                snaps += sb
+            assert int(bb.dones.sum()) > 0 and float(bb.log_probs.abs().max()) > 0
+            snaps.append(len(cb._graphs))
+            if grouped:
+                assert dist.get_backend() == "nccl" and eb._parts.shape[0] == 1
+                g = bb.all_gather()  # one all_gather_into_tensor on RCCL
+                assert len(g.slabs) == 1 and torch.equal(g.slabs[0], bb.slab)
+            va.close()
+            vb.close()
+        finally:
+            if grouped:
+                dist.destroy_process_group()
+        runs.append(snaps)
+    a, b = runs
+    assert a[-1] == 1 and b[-1] == 2  # one graph without a group; two around the collective under one
+    for x, y in zip(a[:-1], b[:-1]):
+        assert torch.equal(x, y)
+
+
+# ---------------------------------------------------------------------------- configs[3] on one GPU
+class _Scripted(nn.Module):
+    """A policy with no cross-row arithmetic (so a shard and the whole batch compute the same bits): the
+    actions of step k are rows [off, off + n) of a pre-drawn global table; value and log-prob are
+    elementwise functions of the observation."""
+
+    def __init__(self, table, off, n):
+        super().__init__()
+        self.table, self.off, self.n, self.k = table, off, n, 0
+
+    def forward(self, obs):
+        a = self.table[self.k % self.table.shape[0], self.off:self.off + self.n]
+        self.k += 1
+        return a.clone(), (obs[:, 0] * 0.5)[:, None], obs[:, 1] * 0.25 - obs[:, 2]
+
+    def predict_values(self, obs):
+        return (obs[:, 0] * 0.5)[:, None]
+
+
+def test_configs3_eight_shards_equal_one_batch():
+    from tum_adlr_deep_reinforcement_learning_amd.rollout import GatheredRollout, RolloutBuffer, RolloutCollector
+    from tum_adlr_deep_reinforcement_learning_amd.vec_env import FixedWingVecEnv
+    W, n, T = 8, 8192, 64
+    N = W * n
+    g = torch.Generator(device=DEV)
+    g.manual_seed(3)
+    table = torch.rand(T, N, 3, generator=g, device=DEV) * 2.4 - 1.2  # some clipped by the action space
+
+    def collect(off, cnt):
+        env = FixedWingVecEnv(cnt, config_kw={"steps_max": 40}, sim_config_kw={"turbulence": False}, device=DEV,
+                              seed=99, env_offset=off, return_tensors=True, info_target=False, lanes=1)
+        buf = RolloutBuffer(T, env.observation_space, env.action_space, device=DEV, gae_lambda=0.95, gamma=0.99,
+                            n_envs=cnt)
+        col = RolloutCollector(env, _Scripted(table, off, cnt), buf)
+        col.collect()
+        out = (buf, col.last_obs.clone(), col.last_dones.clone())
+        env.close()
+        return out
+
+    whole, wobs, wdone = collect(0, N)
+    shards = [collect(r * n, n) for r in range(W)]
+    gathered = GatheredRollout([s[0].slab for s in shards], shards[0][0])  # what the all-gather returns
+    wflat = GatheredRollout([whole.slab], whole).flatten()
+    for got, want in zip(gathered.flatten(), wflat):
+        assert torch.equal(got, want)
+    assert torch.equal(torch.cat([s[0].rewards for s in shards], 1), whole.rewards)
+    assert torch.equal(torch.cat([s[0].dones for s in shards], 1), whole.dones)
+    assert torch.equal(torch.cat([s[1] for s in shards], 0), wobs)
+    assert torch.equal(torch.cat([s[2] for s in shards], 0), wdone)
+    assert int(whole.dones.sum()) > 0  # episodes end and restart inside the horizon
+
+
+def test_configs3_sharded_vecnormalize_statistics():
+    """Eight shard VecNormalize wrappers whose moment records are exchanged (stacked in rank order, as
+    the RCCL all-gather delivers them) hold the statistics of one VecNormalize over the whole batch,
+    to rounding (the records merge in a different tree), on every rank identically."""
+    from tum_adlr_deep_reinforcement_learning_amd.vec_env import FixedWingVecEnv
+    from tum_adlr_deep_reinforcement_learning_amd.vec_normalize import VecNormalize
+    W, n, steps = 8, 8192, 24
+    N = W * n
+
+    def make(off, cnt):
+        venv = FixedWingVecEnv(cnt, config_kw={"steps_max": 15}, sim_config_kw={"turbulence": False}, device=DEV,
+                               seed=7, env_offset=off, return_tensors=True, info_target=False, lanes=1)
+        return venv, VecNormalize(venv)
+
+    wv, we = make(0, N)
+    sh = [make(r * n, n) for r in range(W)]
+    for _, e in sh:
+        e._parts = torch.empty(W, e._rec.numel(), dtype=torch.float64, device=DEV)
+    we.reset()
+    for _, e in sh:  # reset updates the return statistics only: exchange those records too
+        e.venv.reset()
+        e.old_obs = e.venv.engine.obs
+    rng = torch.Generator(device=DEV)
+    rng.manual_seed(1)
+    for _ in range(steps):
+        a = torch.rand(N, 3, generator=rng, device=DEV) * 2 - 1
+        we.step(a)
+        for r, (_, e) in enumerate(sh):
+            e.step_async(a[r * n:(r + 1) * n])
+            e.step_wait_local()
+        recs = torch.stack([e._rec for _, e in sh])
+        for _, e in sh:
+            e._parts.copy_(recs)
+            e.step_wait_finish()
+    d = we.obs_dim
+    for _, e in sh:
+        assert torch.equal(e.rms, sh[0][1].rms)
+    got, want = sh[0][1].rms.cpu().numpy(), we.rms.cpu().numpy()
+    # obs mean / var and counts (the return statistics started from different reset records: skip)
+    np.testing.assert_allclose(got[:2 * d + 1], want[:2 * d + 1], rtol=1e-10, atol=1e-12)
+    for v, _ in sh:
+        v.close()
+    wv.close()
+
+
+# ---------------------------------------------------------------------------- configs[2] full horizon
+def test_configs2_full_2048_horizon_graphed():
+    from tum_adlr_deep_reinforcement_learning_amd.rollout import MlpActorCritic, RolloutBuffer, RolloutCollector
+    from tum_adlr_deep_reinforcement_learning_amd.vec_env import FixedWingVecEnv
+    from tum_adlr_deep_reinforcement_learning_amd.vec_normalize import VecNormalize
+    torch.manual_seed(0)
+    n, T = 65536, 2048
+    venv = FixedWingVecEnv(n, sim_config_kw={"turbulence": False}, device=DEV, seed=17, return_tensors=True,
+                           info_target=False)
+    env = VecNormalize(venv)
+    policy = MlpActorCritic(env.observation_space.shape[0], env.action_space.shape[0]).to(DEV)
+    buf = RolloutBuffer(T, env.observation_space, env.action_space, device=DEV, gae_lambda=0.95, gamma=0.99, n_envs=n)
+    col = RolloutCollector(env, policy, buf)
+    col.collect(16)
+    col.collect(graph=True)
+    assert buf.full and buf.pos == T
+    with torch.no_grad():
+        lv = policy.predict_values(col.last_obs).reshape(-1)
+    idx = torch.randperm(n, generator=torch.Generator().manual_seed(4))[:512].sort().values.to(DEV)
+    sub = lambda t: t[:, idx].cpu().numpy()  # noqa: E731
+    a_ref, r_ref = R.gae(sub(buf.rewards), sub(buf.values), sub(buf.dones), lv[idx].cpu().numpy(),
+                         col.last_dones[idx].cpu().numpy(), 0.99, 0.95)
+    assert np.array_equal(sub(buf.advantages), a_ref)
+    assert np.array_equal(sub(buf.returns), r_ref)
+    assert bool(torch.isfinite(buf.slab).all()) and float(buf.observations.abs().max()) <= 10.0
+    assert int(buf.dones.sum()) > 0 and float(buf.log_probs.abs().max()) > 0
+    venv.close()

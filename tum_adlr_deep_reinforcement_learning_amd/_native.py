@@ -22,7 +22,7 @@ SOURCES = UNITS + [os.path.join(CSRC, "fw_device.hpp"), os.path.join(CSRC, "fw_q
 ARCH = os.environ.get("FWSIM_ARCH", "gfx950")
 
 _lib = None
-ABI_VERSION = 5  # include/fwsim.h FWSIM_ABI_VERSION
+ABI_VERSION = 6  # include/fwsim.h FWSIM_ABI_VERSION
 
 
 class FwError(RuntimeError):
@@ -142,11 +142,16 @@ SIGNATURES = {
     "fw_vecnorm_apply": (_c.c_int, [_vp, _i64, _i32, _i64, _vp, _c.c_double, _i32, _c.c_double, _vp, _i64, _vp, _i32,
                                     _c.c_double, _vp, _vp, _vp, _vp]),
     "fw_replay_add": (_c.c_int, [_vp, _i32, _vp]),
+    "fw_rollout_store": (_c.c_int, [_vp, _i32, _vp, _i32, _vp]),
 }
 
 
 class FwCopySeg(ctypes.Structure):  # include/fwrollout.h fw_copy_seg
     _fields_ = [("src", _vp), ("dst", _vp), ("bytes", _i64)]
+
+
+class FwRowSeg(ctypes.Structure):  # include/fwrollout.h fw_row_seg
+    _fields_ = [("src", _vp), ("dst", _vp), ("bytes", _i64), ("stride", _i64), ("row_off", _i32), ("pad", _i32)]
 
 
 def load(path=None):

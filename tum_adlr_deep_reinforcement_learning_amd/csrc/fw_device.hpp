@@ -36,8 +36,18 @@ int set_error(int code, const std::string& msg);
 
 constexpr int NY = FW_NY;
 constexpr double PI_D = 3.141592653589793;
-constexpr int MAX_NFEV = 6000;  // default RHS-evaluation budget per step (fw_sim_config.max_nfev)
+// default RHS-evaluation budget per step (fw_sim_config.max_nfev): a safety net only -- scipy has no
+// budget, and the steady-state bench population never comes near it (profiles/r03_nfev_census.json)
+constexpr int MAX_NFEV = 1000000;
 constexpr uint32_t DM_SOLVER_FAIL = 1u << 31;  // sim_step_masked dmask bit: RK45 failed, last accepted sub-step kept
+constexpr uint32_t DM_BUDGET = 1u << 30;       // ... and the failure was the max_nfev budget (not TOO_SMALL_STEP)
+
+// per-aircraft stats word of fw_sim_step / fw_env_step (include/fwsim.h): saturated counts + failure bits
+FW_HD int32_t pack_stats(int nfev, int nacc, uint32_t dmask) {
+  const uint32_t nf = nfev > 0xFFFF ? 0xFFFFu : (uint32_t)nfev;
+  const uint32_t na = nacc > 0x3FFF ? 0x3FFFu : (uint32_t)nacc;
+  return (int32_t)(nf | (na << 16) | (dmask & (DM_SOLVER_FAIL | DM_BUDGET)));
+}
 #ifndef FW_Y_PREFETCH
 #define FW_Y_PREFETCH 0
 #endif
@@ -1234,7 +1244,7 @@ FW_HD int sim_step_masked(const C& c, const A& a, T* y, T* der, T* cmd, const T*
   else term = rk45<T, C, A, HO>(c, a, X, y1, sy, sf, stride, nfev, nacc, FW_ER_LDS ? sf + NP * stride : nullptr, ho);
   reload(y);
   if (term < 0) {  // solver failure: y1 = the last accepted sub-step (rk45 wrote Y back), saved as usual
-    dmask = DM_SOLVER_FAIL;
+    dmask = DM_SOLVER_FAIL | (term == -2 ? DM_BUDGET : 0u);
     term = 0;
   }
   if (term) return term;

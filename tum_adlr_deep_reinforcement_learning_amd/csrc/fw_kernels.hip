@@ -825,7 +825,7 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_sim_step(const DevCfg<T>
     for (int a = 0; a < 3; a++) cmd_out[i * 3 + a] = cmd[a];
   if (success) success[i] = term == 0;
   if (term_out) term_out[i] = term;
-  if (stats) stats[i] = (int32_t)((uint32_t)nfev | ((uint32_t)nacc << 16) | (dmask & DM_SOLVER_FAIL));
+  if (stats) stats[i] = pack_stats(nfev, nacc, dmask);
 }
 
 // FixedWingAircraft.step of aircraft i (the body of k_env_step and of one k_env_rollout step).
@@ -1007,7 +1007,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   rew_out[i] = reward;
   done_out[i] = done ? 1 : 0;
   if (term_out) term_out[i] = term;
-  if (stats) stats[i] = (int32_t)((uint32_t)nfev | ((uint32_t)nacc << 16) | (dmask & DM_SOLVER_FAIL));
+  if (stats) stats[i] = pack_stats(nfev, nacc, dmask);
 
   // Monitor episode record + the episode's final target (info["target"] of the done step)
   if (done && episode_out) {
@@ -1345,6 +1345,7 @@ int validate(const fw_sim_config* s, const fw_env_config* e) {
   for (int j = 0; j < 3; j++)
     if (s->act[j].order != 1 && s->act[j].order != 2) return set_err(FW_E_INVALID, "actuator order must be 1 or 2");
   if (s->turbulence && s->turb_len < 2) return set_err(FW_E_INVALID, "turb_len must be >= 2");
+  if (s->max_nfev < 0) return set_err(FW_E_INVALID, "max_nfev must be >= 0 (0 = default budget)");
   if (e) {
     if (e->n_obs < 1 || e->n_obs > FW_MAX_OBS) return set_err(FW_E_INVALID, "n_obs out of range");
     if (e->n_rew < 0 || e->n_rew > FW_MAX_REW) return set_err(FW_E_INVALID, "n_rew out of range");

@@ -24,9 +24,13 @@
 
 namespace qd {
 
+// bound_ctrl set and no `old` operand: the form the backend's DPP combiner folds into a single-use
+// VOP2 consumer (v_add_f32_dpp / v_mul_f32_dpp ... instead of v_mov_b32_dpp + the op).  A quad_perm never
+// reads outside the quad and the four lanes of a quad are always enabled together, so no lane takes
+// the bound_ctrl zero.
 template <int A, int B, int C, int D>
 __device__ __forceinline__ int perm_i(int x) {
-  return __builtin_amdgcn_mov_dpp(x, A | (B << 2) | (C << 4) | (D << 6), 0xF, 0xF, false);
+  return __builtin_amdgcn_update_dpp(0, x, A | (B << 2) | (C << 4) | (D << 6), 0xF, 0xF, true);
 }
 template <int A, int B, int C, int D>
 __device__ __forceinline__ float perm(float x) {

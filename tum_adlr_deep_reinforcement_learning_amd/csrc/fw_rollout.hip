@@ -301,6 +301,33 @@ __global__ __launch_bounds__(BLOCK) void k_copy_segs(CopySegs cs) {
   }
 }
 
+// RolloutBuffer.add with the row read on the device (fw_rollout_store): the same copy as k_copy_segs,
+// destinations offset by (ctrl[0] + row_off) * stride, segments outside [0, ctrl[1]) skipped.
+struct RowSegs {
+  const uint8_t* src[FW_MAX_COPY_SEGS];
+  uint8_t* dst[FW_MAX_COPY_SEGS];
+  int64_t stride[FW_MAX_COPY_SEGS];
+  int64_t start[FW_MAX_COPY_SEGS + 1];  // 4-byte units
+  int row_off[FW_MAX_COPY_SEGS];
+  int n;
+};
+
+__global__ __launch_bounds__(BLOCK) void k_store_rows(RowSegs rs, const int32_t* __restrict__ ctrl) {
+  const int row = ctrl[0], n_rows = ctrl[1];
+  const int64_t total = rs.start[rs.n];
+  for (int64_t u = (int64_t)blockIdx.x * BLOCK + threadIdx.x; u < total; u += (int64_t)gridDim.x * BLOCK) {
+    int k = 0;
+#pragma unroll
+    for (int j = 1; j < FW_MAX_COPY_SEGS; j++) k += (j < rs.n && u >= rs.start[j]) ? 1 : 0;
+    const int r = row + rs.row_off[k];
+    if (r < 0 || r >= n_rows) continue;
+    const int64_t off = u - rs.start[k];
+    reinterpret_cast<uint32_t*>(rs.dst[k] + (int64_t)r * rs.stride[k])[off] = reinterpret_cast<const uint32_t*>(rs.src[k])[off];
+  }
+}
+
+__global__ void k_row_advance(int32_t* ctrl) { ctrl[0] += 1; }
+
 unsigned grid_for(int64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
 
 int moments_parts(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(MAX_PARTS, (n + BLOCK - 1) / BLOCK)); }
@@ -390,6 +417,36 @@ int fw_replay_add(const fw_copy_seg* segs, int32_t n_segs, void* stream) {
   const unsigned grid = (unsigned)std::min<int64_t>((total + BLOCK - 1) / BLOCK, 8192);
   hipLaunchKernelGGL(k_copy_segs, dim3(grid), dim3(BLOCK), 0, (hipStream_t)stream, cs);
   FW_HIP(hipGetLastError());
+  return FW_OK;
+}
+
+int fw_rollout_store(const fw_row_seg* segs, int32_t n_segs, int32_t* ctrl_dev, int32_t advance, void* stream) {
+  if (!segs || !ctrl_dev || n_segs < 1 || n_segs > FW_MAX_COPY_SEGS)
+    return fw::set_error(FW_E_INVALID, "fw_rollout_store: 1..FW_MAX_COPY_SEGS segments and a ctrl buffer");
+  RowSegs rs{};
+  rs.n = n_segs;
+  rs.start[0] = 0;
+  for (int k = 0; k < n_segs; k++) {
+    const fw_row_seg& g = segs[k];
+    if (!g.src || !g.dst || g.bytes < 0 || g.bytes % 4 || g.stride % 4 || (uintptr_t)g.src % 4 || (uintptr_t)g.dst % 4)
+      return fw::set_error(FW_E_INVALID, "fw_rollout_store: bad segment (NULL, or not dword-aligned)");
+    rs.src[k] = (const uint8_t*)g.src;
+    rs.dst[k] = (uint8_t*)g.dst;
+    rs.stride[k] = g.stride;
+    rs.row_off[k] = g.row_off;
+    rs.start[k + 1] = rs.start[k] + g.bytes / 4;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t total = rs.start[n_segs];
+  if (total > 0) {
+    const unsigned grid = (unsigned)std::min<int64_t>((total + BLOCK - 1) / BLOCK, 8192);
+    hipLaunchKernelGGL(k_store_rows, dim3(grid), dim3(BLOCK), 0, s, rs, (const int32_t*)ctrl_dev);
+    FW_HIP(hipGetLastError());
+  }
+  if (advance) {
+    hipLaunchKernelGGL(k_row_advance, dim3(1), dim3(1), 0, s, ctrl_dev);
+    FW_HIP(hipGetLastError());
+  }
   return FW_OK;
 }
 

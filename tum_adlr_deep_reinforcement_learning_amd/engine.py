@@ -61,6 +61,7 @@ class Engine:
             self.metrics = torch.full((C.FW_NMETRIC, n), float("nan"), dtype=dt, device=dev)  # SoA
             _native.check(self.lib.fw_set_metrics_output(self.h, _ptr(self.metrics)), "fw_set_metrics_output")
         self._noise = None
+        self.config_version = 0  # bumped by every call that changes what a launch does (captured graphs check it)
         self.seed(0)
         if lanes is not None:
             self.set_lanes(lanes)
@@ -68,6 +69,7 @@ class Engine:
     def set_lanes(self, lanes):
         """Lanes per aircraft of the step kernels: 1, 4 (quad integrator) or 0 = automatic (fw_set_lanes)."""
         _native.check(self.lib.fw_set_lanes(self.h, int(lanes)), "fw_set_lanes")
+        self.config_version += 1
 
     @property
     def lanes(self):
@@ -107,6 +109,7 @@ class Engine:
         _native.check(self.lib.fw_update_config(self.h, ctypes.byref(self._sim_cfg),
                                                 ctypes.byref(self._env_cfg) if self._env_cfg is not None else None),
                       "fw_update_config")
+        self.config_version += 1
 
     def set_noise(self, noise):
         """Inject N(0,1) turbulence noise, array-like [n][4][len] or [4][len] (shared), or None."""
@@ -222,8 +225,17 @@ class Engine:
 
     @staticmethod
     def decode_stats(stats):
-        """fw_sim_step / fw_env_step stats -> (nfev, n_accepted, solver_failed) tensors."""
-        return stats & 0xFFFF, (stats >> 16) & 0x7FFF, (stats < 0)
+        """fw_sim_step / fw_env_step stats -> (nfev, n_accepted, solver_failed) tensors.
+
+        nfev saturates at 65535 and n_accepted at 16383 (include/fwsim.h); ``budget_hits`` tells the
+        failures that were the max_nfev budget apart."""
+        return stats & 0xFFFF, (stats >> 16) & 0x3FFF, (stats < 0)
+
+    @staticmethod
+    def budget_hits(stats):
+        """stats -> bool tensor: the step ended on the max_nfev budget (FW_STATS_BUDGET, bit 30), a step
+        scipy's solve_ivp would have continued (it has no budget)."""
+        return (stats & (1 << 30)) != 0
 
 
 class StepGraph:

@@ -236,12 +236,14 @@ class RolloutCollector:
 
     @torch.no_grad()
     def collect(self, n_rollout_steps=None, graph=False):
-        """``graph=True``: the step body (policy forward, action clip, env step incl. VecNormalize) is
-        captured once into a HIP graph and replayed per step, with the buffer writes of a step done by
-        one ``fw_replay_add`` launch (2 launches per step instead of ~30); same kernels, same results.
-        Single-process only (a sharded VecNormalize all-gathers per step: eager path).  The captured
-        step reads the policy's parameters in place, so optimiser steps between collections are seen;
-        a collector whose policy or env object is replaced must be rebuilt."""
+        """``graph=True``: the step body (policy forward, action clip, env step incl. VecNormalize, the
+        buffer row stores) is captured into a HIP graph and replayed per step; same kernels, same results
+        (bit for bit, tests/test_gpu_r02.py, tests/test_gpu_r03.py).  Under a process group (a sharded
+        VecNormalize exchanges its moment records every step) the step is captured as two graphs around
+        the RCCL all-gather: 3 launches per step (graph, collective, graph) instead of ~30.  The captured
+        step reads the policy's parameters in place, so optimiser steps between collections are seen; it
+        is recaptured when a host-side choice it baked in changes (``graph_key``: VecNormalize training /
+        norm flags, the engine's lanes and configuration, the buffer)."""
         buf, env = self.buffer, self.env
         n = n_rollout_steps or buf.buffer_size
         if self.last_obs is None:
@@ -270,15 +272,25 @@ class RolloutCollector:
 
     # ------------------------------------------------------------ graphed collection
     def _graph_ok(self):
-        import torch.distributed as dist
         buf = self.buffer
-        if buf.device.type != "cuda" or buf.n_envs % 4:  # fw_replay_add moves whole dwords
+        if buf.device.type != "cuda" or buf.n_envs % 4:  # fw_rollout_store moves whole dwords (uint8 rows)
             return False
-        return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+        venv = getattr(self.env, "venv", self.env)
+        return getattr(venv, "_hists", None) is None  # a history recorder syncs to the host every step
+
+    def _split(self):
+        """The env exchanges statistics between shards every step: capture around the collective."""
+        import torch.distributed as dist
+        return hasattr(self.env, "step_exchange") and dist.is_available() and dist.is_initialized()
+
+    def graph_key(self):
+        env_key = self.env.graph_key() if hasattr(self.env, "graph_key") else None
+        return (env_key, self._split(), self.buffer.slab.data_ptr(), self.buffer.buffer_size)
 
     def _capture(self):
         """Capture one collect step on static tensors: s_obs (the observation the policy acts on, then
-        the next one), s_start (episode starts: the last dones), and the step's outputs."""
+        the next one), s_start (episode starts: the last dones), and the step's outputs, which the
+        step's own fw_rollout_store launch writes into buffer row ctrl[0] (then ctrl[0] += 1)."""
         # kernels, the policy's BLAS handles and the allocator were warmed by an eager collect(); the
         # capture itself records only, so no env state moves here
         if not getattr(self, "_eager_done", False):
@@ -291,57 +303,75 @@ class RolloutCollector:
         self.s_rew = torch.empty(N, dtype=torch.float32, device=dev)
         self.s_val = torch.empty(N, dtype=torch.float32, device=dev)
         self.s_logp = torch.empty(N, dtype=torch.float32, device=dev)
+        self._ctrl = torch.zeros(2, dtype=torch.int32, device=dev)  # {row, n_rows} of fw_rollout_store
+        rows = ((self.s_obs, buf.observations, 1), (self.s_start, buf.dones, 1), (self.s_act, buf.actions, 0),
+                (self.s_rew, buf.rewards, 0), (self.s_val, buf.values, 0), (self.s_logp, buf.log_probs, 0))
+        self._rsegs = (_native.FwRowSeg * len(rows))()
+        for k, (src, dst, off) in enumerate(rows):
+            rb = dst[0].numel() * dst.element_size()
+            g = self._rsegs[k]
+            g.src, g.dst, g.bytes, g.stride, g.row_off = src.data_ptr(), dst.data_ptr(), rb, rb, off
+        lib = _native.load()
+        split = self._split()
 
-        def body():
+        def head():
             actions, values, log_probs = self.policy(self.s_obs)
             clipped = torch.max(torch.min(actions, self.high), self.low)
-            new_obs, rewards, dones, _ = env.step(clipped)
             self.s_act.copy_(actions)
             self.s_val.copy_(values.reshape(-1))
             self.s_logp.copy_(log_probs)
+            if split:
+                env.step_async(clipped)
+                env.step_wait_local()
+                return None
+            return env.step(clipped)
+
+        def tail(res):
+            new_obs, rewards, dones, _ = env.step_wait_finish() if res is None else res
             self.s_rew.copy_(rewards)
             self.s_obs.copy_(new_obs.reshape(N, D))
             self.s_start.copy_(dones)
+            # the stream is read here, inside the capture: torch.cuda.graph captures on its own side stream
+            _native.check(lib.fw_rollout_store(self._rsegs, len(rows), _p(self._ctrl), 1, _stream(dev)),
+                          "fw_rollout_store")
 
-        self._graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._graph):
-            body()
-        self._segs = (_native.FwCopySeg * 6)()
+        self._graphs = [torch.cuda.CUDAGraph()]
+        if split:
+            self._graphs.append(torch.cuda.CUDAGraph())
+            with torch.cuda.graph(self._graphs[0]):
+                head()
+            with torch.cuda.graph(self._graphs[1]):
+                tail(None)
+        else:
+            with torch.cuda.graph(self._graphs[0]):
+                tail(head())
+        self._key = self.graph_key()
 
     def _collect_graphed(self, n):
         buf = self.buffer
-        if getattr(self, "_graph", None) is None:
+        if getattr(self, "_graphs", None) is None or self._key != self.graph_key():
             self._capture()
-        dev = buf.device
-        N, D, A = buf.n_envs, buf.obs_dim, buf.action_dim
+        N, D = buf.n_envs, buf.obs_dim
         buf.reset()
         self.s_obs.copy_(self.last_obs.reshape(N, D))
         self.s_start.copy_(self.last_dones)
-        lib, st = _native.load(), _stream(dev)
-        segs = self._segs
-
-        def store(t, prev):
-            """one launch: the inputs of step t (obs, episode start) and the outputs of step prev"""
-            k = 0
-            if t is not None:
-                for src, dst in ((self.s_obs, buf.observations[t]), (self.s_start, buf.dones[t])):
-                    segs[k].src, segs[k].dst, segs[k].bytes = src.data_ptr(), dst.data_ptr(), dst.numel() * dst.element_size()
-                    k += 1
-            if prev is not None:
-                for src, dst in ((self.s_act, buf.actions[prev]), (self.s_rew, buf.rewards[prev]),
-                                 (self.s_val, buf.values[prev]), (self.s_logp, buf.log_probs[prev])):
-                    segs[k].src, segs[k].dst, segs[k].bytes = src.data_ptr(), dst.data_ptr(), dst.numel() * dst.element_size()
-                    k += 1
-            _native.check(lib.fw_replay_add(segs, k, st), "fw_replay_add")
-
-        for t in range(n):
-            store(t, t - 1 if t else None)
-            self._graph.replay()
-        store(None, n - 1)
+        buf.observations[0].copy_(self.s_obs)  # the inputs of step 0; step t stores those of t + 1
+        buf.dones[0].copy_(self.s_start)
+        self._ctrl[0] = 0
+        self._ctrl[1] = n
+        if len(self._graphs) == 1:
+            g = self._graphs[0]
+            for _ in range(n):
+                g.replay()
+        else:
+            g0, g1 = self._graphs
+            for _ in range(n):
+                g0.replay()
+                self.env.step_exchange()  # the RCCL all-gather of the moment records
+                g1.replay()
         self.last_obs = self.s_obs.clone().reshape(self.last_obs.shape)
         self.last_dones = self.s_start.clone()
         buf.pos, buf.full = n, n == buf.buffer_size
         last_values = self.policy.predict_values(self.last_obs)
         buf.compute_returns_and_advantage(last_values, self.last_dones)
         return buf
-

@@ -33,15 +33,24 @@ def shard_range(n_total, rank, world_size):
     return offset, count
 
 
-def all_gather_flat(t, group=None):
-    """Gather a contiguous tensor from every rank -> [W][t.numel()] (rank order)."""
+def all_gather_flat(t, group=None, out=None):
+    """Gather a contiguous tensor from every rank -> [W][t.numel()] (rank order).
+
+    Without a process group this is a view of ``t``.  With one (any size, also world 1) it is a real
+    collective: ``all_gather_into_tensor`` on RCCL (``nccl``), a list ``all_gather`` on gloo.  ``out``
+    (optional, [W * t.numel()] of t's dtype/device) receives the result in place, so a caller can keep
+    the destination at a fixed address (a captured graph reads it)."""
     t = t.contiguous().view(-1)
     if not (dist.is_available() and dist.is_initialized()):
+        if out is not None:
+            out.view(-1).copy_(t)
+            return out.view(1, -1)
         return t.view(1, -1)
     W = dist.get_world_size(group)
-    if W == 1:
-        return t.view(1, -1)
-    out = torch.empty(W * t.numel(), dtype=t.dtype, device=t.device)
+    if out is None:
+        out = torch.empty(W * t.numel(), dtype=t.dtype, device=t.device)
+    elif out.numel() != W * t.numel() or out.dtype != t.dtype or out.device != t.device:
+        raise ValueError("all_gather_flat: out must hold world_size * t.numel() elements of t's dtype and device")
     if dist.get_backend(group) == "nccl":
         dist.all_gather_into_tensor(out, t, group=group)
     else:

@@ -65,6 +65,20 @@ class VecEnv(_SB3VecEnv if _SB3VecEnv is not None else object):
         return indices
 
 
+QUAD_AUTO_MAX = 16384  # fw_kernels.hip FW_QUAD_AUTO_MAX: the automatic choice runs quads up to this shard size
+
+
+def auto_lanes(global_envs, world_size=None):
+    """Lanes per aircraft for every shard of ``global_envs`` envs split over ``world_size`` ranks (default:
+    the initialised process group's size, else 1): the library's automatic rule applied to the largest
+    shard (sharding.shard_range gives the remainder to the first ranks)."""
+    if world_size is None:
+        import torch.distributed as dist
+        world_size = dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
+    largest = -(-int(global_envs) // int(world_size))
+    return 4 if largest <= QUAD_AUTO_MAX else 1
+
+
 def termination_name(code, dynamics=("elevon_right", "elevon_left", "throttle")):
     """Termination code -> the reference's info["termination"] string."""
     code = int(code)
@@ -102,7 +116,7 @@ class _Infos(collections.abc.Sequence):
     the dominant host cost of the SB3 surface, and most callers touch few)."""
 
     def __init__(self, n, done, term, tobs, episode, targets, t_elapsed, dynamics, with_target, metrics=None,
-                 metric_names=()):
+                 metric_names=(), stats=None):
         self._n = n
         self._done, self._term, self._tobs, self._ep = done, term, tobs, episode
         self._tgt = targets
@@ -110,6 +124,7 @@ class _Infos(collections.abc.Sequence):
         self._dyn = dynamics
         self._with_target = with_target
         self._met, self._met_names = metrics, metric_names
+        self._stats = stats
         self._cache = {}
 
     def __len__(self):
@@ -135,6 +150,10 @@ class _Infos(collections.abc.Sequence):
             elif self._with_target:
                 t = self._tgt[:, i]
                 d["target"] = {"roll": float(t[0]), "pitch": float(t[1]), "Va": float(t[2])}
+            if self._stats is not None and (int(self._stats[i]) >> 30) & 1:
+                # the step ended on the RHS-evaluation budget (fw_sim_config.max_nfev; scipy has none): the
+                # last accepted sub-step was committed, where solve_ivp would have kept integrating
+                d["solver_budget_exhausted"] = True
             self._cache[i] = d
         return d
 
@@ -149,14 +168,18 @@ class FixedWingVecEnv(VecEnv):
 
     def __init__(self, num_envs=1, config_path=None, config_kw=None, sim_config_path=None, sim_parameter_path=None,
                  sim_config_kw=None, device=None, precision="float32", seed=None, return_tensors=False,
-                 info_target=True, curriculum_level=1, env_offset=0, record_history=False, lanes=None):
+                 info_target=True, curriculum_level=1, env_offset=0, record_history=False, lanes=None,
+                 global_envs=None):
         self.spec = C.EnvSpec(config_path, config_kw, sim_config_path, sim_parameter_path, sim_config_kw,
                               curriculum_level=curriculum_level)
         obs_space = Box(self.spec.obs_low, self.spec.obs_high, dtype=np.float32)
         act_space = Box(self.spec.action_space_low, self.spec.action_space_high, dtype=np.float32)
         VecEnv.__init__(self, int(num_envs), obs_space, act_space)
-        # lanes: integrator (fw_set_lanes; None = automatic by num_envs); fix it when shards of different sizes
-        # must agree bit for bit
+        # lanes: integrator (fw_set_lanes; None = automatic by num_envs).  A shard of a sharded batch
+        # (global_envs = the envs of all ranks) picks it from the LARGEST shard of the split, so every rank
+        # runs the same integrator (the automatic rule alone could give 16385 one lane and 16384 quads)
+        if lanes is None and global_envs is not None:
+            lanes = auto_lanes(global_envs)
         self.engine = Engine(self.spec.sim, self.spec, self.num_envs, device=device, precision=precision, lanes=lanes)
         self.device = self.engine.device
         self.return_tensors = return_tensors
@@ -209,7 +232,7 @@ class FixedWingVecEnv(VecEnv):
         25-31) and restart their histories with the reset observation."""
         from .history import step_succeeded
         eng = self.engine
-        obs, rew, done, term = eng.env_step(actions, auto_reset=False)
+        obs, rew, done, term = eng.env_step(actions, auto_reset=False, stats=True)
         dn = done.cpu().numpy().astype(bool)
         tm, r = term.cpu().numpy(), rew.double().cpu().numpy()
         o = self._shaped(obs.cpu().numpy().astype(np.float32))
@@ -241,7 +264,7 @@ class FixedWingVecEnv(VecEnv):
         if self._hists is not None:
             obs, rew, done, term = self._step_recording(self._actions)
         else:
-            obs, rew, done, term = eng.env_step(self._actions, auto_reset=True)
+            obs, rew, done, term = eng.env_step(self._actions, auto_reset=True, stats=True)
         self._actions = None
         if self.return_tensors:
             return self._shaped(obs), rew, done.bool(), self._infos_lazy_device()
@@ -275,7 +298,8 @@ class FixedWingVecEnv(VecEnv):
         tgt = eng.get_block(C.FW_BLK_TARGET).cpu().numpy() if self.info_target else None
         met = eng.metrics.cpu().numpy() if (anyd and eng.metrics is not None) else None
         return _Infos(self.num_envs, done_np, term, tobs, ep, tgt, time.time() - self._t_start, self._dyn,
-                      self.info_target, met, [m["name"] for m in self.spec.cfg.get("metrics", [])])
+                      self.info_target, met, [m["name"] for m in self.spec.cfg.get("metrics", [])],
+                      eng.stats.cpu().numpy())
 
     def _infos_lazy_device(self):
         """Device mode: infos are built only if the caller asks for them (triggers a sync)."""
@@ -299,6 +323,10 @@ class FixedWingVecEnv(VecEnv):
 
     def close(self):
         self.engine.close()
+
+    def graph_key(self):
+        """What a captured step bakes in (rollout.RolloutCollector recaptures when it changes)."""
+        return (self.engine.lanes, self.engine.config_version, self._hists is not None)
 
     def get_attr(self, attr_name, indices=None):
         idx = list(self._get_indices(indices))

@@ -23,6 +23,7 @@ import ctypes
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from . import _native
 from .sharding import all_gather_flat
@@ -82,6 +83,10 @@ class VecNormalize:
         self._ws = torch.empty(int(self.lib.fw_moments_workspace_bytes(n, d)), dtype=torch.uint8, device=dev)
         self._rec = torch.empty(1 + 2 * (d + 1), dtype=torch.float64, device=dev)
         self._rec_ret = torch.empty(3, dtype=torch.float64, device=dev)
+        # rank-ordered records of the global batch, at fixed addresses (a captured collect step reads them)
+        W = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        self._parts = torch.empty(W, self._rec.numel(), dtype=torch.float64, device=dev)
+        self._parts_ret = torch.empty(W, 3, dtype=torch.float64, device=dev)
         self._zero_rew = torch.zeros(n, dtype=torch.float32, device=dev)
         self.obs_out = torch.empty(n, d, dtype=torch.float32, device=dev)
         self.rew_out = torch.empty(n, dtype=torch.float32, device=dev)
@@ -95,9 +100,21 @@ class VecNormalize:
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     def _gather(self, rec):
-        """Rank-ordered moment records of the global batch ([W][len])."""
-        out = all_gather_flat(rec, self.group)
+        """Rank-ordered moment records of the global batch ([W][len]), into the static parts buffer."""
+        out = all_gather_flat(rec, self.group, out=self._parts if rec is self._rec else self._parts_ret)
         return out, out.shape[0]
+
+    def _moments(self, obs, rew):
+        """This shard's moment record (fw_moments) of obs and of the updated discounted return."""
+        d, n = self.obs_dim, self.num_envs
+        _native.check(self.lib.fw_moments(_p(obs), n, d, d, _p(rew), _p(self.ret), float(self.gamma), _p(self._ws),
+                                          _p(self._rec), self._s()), "fw_moments")
+
+    def _merge(self):
+        """RunningMeanStd.update_from_moments over the gathered records (rank order)."""
+        d = self.obs_dim
+        _native.check(self.lib.fw_rms_update(_p(self._parts), self._parts.shape[0], d, 1, _p(self.rms), 1, 1,
+                                             self._s()), "fw_rms_update")
 
     def _update(self, obs, rew):
         """obs_rms.update(obs) and ret = ret*gamma + rew; ret_rms.update(ret)  (training only)."""
@@ -105,10 +122,9 @@ class VecNormalize:
         L = self.lib
         s = self._s()
         if obs is not None:
-            _native.check(L.fw_moments(_p(obs), n, d, d, _p(rew), _p(self.ret), float(self.gamma), _p(self._ws),
-                                       _p(self._rec), s), "fw_moments")
-            parts, W = self._gather(self._rec)
-            _native.check(L.fw_rms_update(_p(parts), W, d, 1, _p(self.rms), 1, 1, s), "fw_rms_update")
+            self._moments(obs, rew)
+            self._gather(self._rec)
+            self._merge()
         else:  # return statistics only (reset)
             _native.check(L.fw_moments(None, n, 0, 0, _p(rew), _p(self.ret), float(self.gamma), _p(self._ws),
                                        _p(self._rec_ret), s), "fw_moments")
@@ -153,18 +169,41 @@ class VecNormalize:
 
     def step_wait(self):
         """vec_normalize.py:106-131."""
+        self.step_wait_local()
+        self.step_exchange()
+        return self.step_wait_finish()
+
+    # step_wait in three phases, for a collect step captured as HIP graphs around the collective:
+    # local (env step + this shard's moments) | exchange (RCCL all-gather of the records) | finish
+    # (update_from_moments in rank order, normalisation).  Phase 1 and 3 launch only kernels.
+    def step_wait_local(self):
         obs, rews, news, infos = self.venv.step_wait()
         obs = obs.to(torch.float32).contiguous()
         rews = rews.to(torch.float32).contiguous()
         self.old_obs, self.old_reward = obs, rews
-        done_u8 = news.to(torch.uint8).contiguous()
+        self._news, self._infos, self._done_u8 = news, infos, news.to(torch.uint8).contiguous()
         if self.training:
-            self._update(obs, rews)
-        self._apply(obs, rews, done_u8)
+            self._moments(obs, rews)
+
+    def step_exchange(self):
+        if self.training:
+            self._gather(self._rec)
+
+    def step_wait_finish(self):
+        if self.training:
+            self._merge()
+        self._apply(self.old_obs, self.old_reward, self._done_u8)
+        news, infos = self._news, self._infos
         if self.return_tensors:
             return self.obs_out, self.rew_out, news, infos
         return self.obs_out.cpu().numpy(), self.rew_out.cpu().numpy().astype(np.float64), \
             news.cpu().numpy().astype(bool), infos
+
+    def graph_key(self):
+        """Host-side choices a captured step bakes in (RolloutCollector recaptures when this changes)."""
+        inner = self.venv.graph_key() if hasattr(self.venv, "graph_key") else None
+        return (self.training, self.norm_obs, self.norm_reward, self.clip_obs, self.clip_reward, self.gamma,
+                self.epsilon, inner)
 
     def step(self, actions):
         self.step_async(actions)
