@@ -512,8 +512,15 @@ FW_HD int rhs(const C& c0, const A& a, const StepCtx<T>& X, bool first, const T*
   const T fg0 = a.mg * (T(2) * (e1 * e3 - e2 * e0));
   const T fg1 = a.mg * (T(2) * (e2 * e3 + e1 * e0));
   const T fg2 = a.mg * (e3 * e3 + e0 * e0 - e1 * e1 - e2 * e2);
-  const T ex1 = fexp(-a.M * (alpha - a.a0));
-  const T ex2 = fexp(a.M * (alpha + a.a0));
+  T ex1, ex2;
+  if constexpr (sizeof(T) == 4) {  // exp(-M (alpha - a0)), exp(M (alpha + a0)) as exp2 of one fma each
+    const T l2e = T(1.4426950408889634), k = a.M * l2e, k0 = a.M * a.a0 * l2e;
+    ex1 = __builtin_amdgcn_exp2f(fmaf(-k, alpha, k0));
+    ex2 = __builtin_amdgcn_exp2f(fmaf(k, alpha, k0));
+  } else {
+    ex1 = fexp(-a.M * (alpha - a.a0));
+    ex2 = fexp(a.M * (alpha + a.a0));
+  }
   // stall blend sigma = (1+e1+e2) / ((1+e1)(1+e2)) (pyfly.py:1541-1543).  Since
   // e1 e2 = exp(2 M a0) = C, the denominator is S + C with S = 1+e1+e2, so
   // sigma = 1 / (1 + C/S): the same value, but it never forms the ~1e38 product
@@ -521,26 +528,29 @@ FW_HD int rhs(const C& c0, const A& a, const StepCtx<T>& X, bool first, const T*
   // stall) and it is exactly 1 when an exponential overflows.
   const T sigma = frcp(T(1) + a.sig_c * frcp(T(1) + ex1 + ex2));
   const T osig = T(1) - sigma;
-  const T sgna = sgn(alpha);
+  // sgn(alpha) sin(alpha)^2 = sin(alpha) |sin(alpha)|: sin has alpha's sign on [-pi, pi] and the
+  // product is 0 where it does not (pyfly.py:1547-1579 multiply by np.sign(alpha))
+  const T ssa = sa * fabs(sa);
   const T CLlin = a.CL0 + a.CLa * alpha;
-  const T CL = osig * CLlin + sigma * (T(2) * sgna * sa * sa * ca);
+  const T CL = osig * CLlin + sigma * (T(2) * ssa * ca);
   const T iVa = frcp(Va);
   const T qn = q * iVa;  // q / Va
   // lift / drag / pitch moment per unit dynamic pressure (pyfly.py:1529-1579)
   const T flift = a.qS * V2a * (CL + a.kCLq * qn + a.CLde * elev);
-  const T CD = a.CDp + osig * (CLlin * CLlin) * a.inv_pi_e_ar + sigma * (T(2) * sgna * (sa * sa * sa));
+  const T CD = a.CDp + osig * (CLlin * CLlin) * a.inv_pi_e_ar + sigma * (T(2) * (ssa * sa));
   const T CDb = a.CDb1 * beta + a.CDb2 * beta * beta;
   const T fdrag = a.qS * V2a * (CD + CDb + a.kCDq * qn + a.CDde * elev * elev);
-  const T Cm = osig * (a.Cm0 + a.Cma * alpha) + sigma * (a.Cmfp * sgna * sa * sa);
+  const T Cm = osig * (a.Cm0 + a.Cma * alpha) + sigma * (a.Cmfp * ssa);
   const T mm = a.qSc * V2a * (Cm + a.kCmq * qn + a.Cmde * elev);
   const T bp = a.hb * p * iVa, br = a.hb * r * iVa;
   const T fy = a.qS * V2a * (a.CY0 + a.CYb * beta + a.CYp * bp + a.CYr * br + a.CYda * ail);
   const T ll = a.qSb * V2a * (a.Cl0 + a.Clb * beta + a.Clp * bp + a.Clr * br + a.Clda * ail);
   const T nn = a.qSb * V2a * (a.Cn0 + a.Cnb * beta + a.Cnp * bp + a.Cnr * br + a.Cnda * ail);
-  // f_aero = R_euler(0, alpha, beta) . [-D, Y, -L]
-  const T fa0 = ca * cb * (-fdrag) + ca * sb * fy - sa * (-flift);
-  const T fa1 = -sb * (-fdrag) + cb * fy;
-  const T fa2 = sa * cb * (-fdrag) + sa * sb * fy + ca * (-flift);
+  // f_aero = R_euler(0, alpha, beta) . [-D, Y, -L] = R_alpha . (R_beta . [-D, Y, -L])
+  const T U = cb * (-fdrag) + sb * fy;
+  const T fa0 = ca * U + sa * flift;
+  const T fa1 = sb * fdrag + cb * fy;
+  const T fa2 = sa * U - ca * flift;
   const T Vd = Va + thr * (a.kmotor - Va);
   const T fprop = a.prop_k * Vd * (Vd - Va);
   const T tprop = -a.kTP2 * (thr * thr);
@@ -626,6 +636,18 @@ constexpr double B0 = 35.0 / 384, B2 = 500.0 / 1113, B3 = 125.0 / 192, B4 = -218
 constexpr double E0 = -71.0 / 57600, E2 = 71.0 / 16695, E3 = -71.0 / 1920, E4 = 17253.0 / 339200, E5 = -22.0 / 525,
                  E6 = 1.0 / 40;
 }  // namespace dp5
+
+// scipy's min_step = 10 * np.abs(np.nextafter(t, np.inf) - t) (rk.py:116) for t in [0, t_bound]:
+// on the device from the exponent (v_frexp_exp / v_ldexp, 3 instructions) instead of libm's nextafter
+// (~25): for normal t = m 2^e, m in [0.5, 1), the spacing above t is 2^(e - 53); at t = 0 it is the
+// smallest subnormal.  t never lies in (0, 2^-1022): steps start at h0 >= ~1e-300.
+FW_HD double min_step_at(double t) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return t > 0.0 ? 10.0 * __builtin_amdgcn_ldexp(1.0, __builtin_amdgcn_frexp_exp(t) - 53) : 10.0 * 0x1p-1074;
+#else
+  return 10.0 * fabs(nextafter(t, 1e300) - t);
+#endif
+}
 
 #include "fw_quad.hpp"
 
@@ -759,7 +781,7 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
   }
   for (;;) {
     if (begin_step) {  // RungeKutta._step_impl entry (rk.py:111-124)
-      min_step = 10.0 * fabs(nextafter(t, 1e300) - t);
+      min_step = min_step_at(t);
       if (h_abs < min_step) h_abs = min_step;
       rejected = false;
     }
@@ -1031,7 +1053,7 @@ rk_done:
       stage = 2;
     }
     if (begin_step) {  // RungeKutta._step_impl entry (rk.py:111-124)
-      min_step = 10.0 * fabs(nextafter(t, 1e300) - t);
+      min_step = min_step_at(t);
       if (h_abs < min_step) h_abs = min_step;
       rejected = false;
       begin_attempt = true;

@@ -76,11 +76,15 @@ __device__ __forceinline__ int key_var(int k) {
   return k == 12 ? FW_V_AILERON : k == 13 ? FW_V_ELEVATOR : k == 14 ? FW_V_VA : k == 15 ? FW_V_ALPHA : FW_V_BETA;
 }
 
-// Per-lane constants of one step (lane r's rows; lane 3: no conditions)
+// Per-lane constants of one step (lane r's rows; lane 3: no conditions).  Lane 3 carries e0 in slot 0
+// and zeros in slots 1..5; its row coefficients are zero, so its slot-1..5 derivatives come out as 0
+// without a select (rhs_quad).
 template <typename T>
 struct QCtx {
   int r;
   bool row;
+  T rowf;                 // 1 on lanes 0..2, 0 on lane 3
+  T sgn1;                 // +1 on lane 1 (the beta chain's exponential), -1 on the others
   T w0, w1, w2;           // steady wind components r, r+1, r+2 (cyclic)
   T tl, ta, sp;           // linear / angular turbulence and actuator set-point of row r
   T elev0, ail0;          // t == 0 elevator / aileron (StepCtx)
@@ -88,8 +92,8 @@ struct QCtx {
   T om_cl, om_ch, om_vl, om_vh, pos_cl, pos_ch, vel_cl, vel_ch, vel_vl, vel_vh, act_cl, act_ch, act_vl, act_vh;
   T dmax;
   bool om_clip, vel_clip, act_clip, dclip;
-  T ac0, ac1, ac2, ac3, ac4, ac5;  // actuator coefficients of row r
-  // _f_omega_dot row r = kpq PQ + kqr QR + kpr PR + kpp (P^2 - R^2) + kt0 t0 + kt1 t1 + kt2 t2
+  T ac0, ac1, ac2, ac3, ac4, ac5;  // actuator coefficients of row r (0 on lane 3)
+  // _f_omega_dot row r = kpq PQ + kqr QR + kpr PR + kpp (P^2 - R^2) + kt0 t0 + kt1 t1 + kt2 t2 (0 on lane 3)
   T kpq, kqr, kpr, kpp, kt0, kt1, kt2;
 };
 
@@ -98,8 +102,11 @@ __device__ __forceinline__ QCtx<T> qctx(const C& c, const StepCtx<T>& X, int r) 
   QCtx<T> Q;
   auto s3 = [r](T a0, T a1, T a2) { return r == 0 ? a0 : (r == 1 ? a1 : a2); };
   const T inf = T(__builtin_inf());
+  const T z = T(0);
   Q.r = r;
   Q.row = r < 3;
+  Q.rowf = Q.row ? T(1) : z;
+  Q.sgn1 = r == 1 ? T(1) : T(-1);
   Q.w0 = s3(X.wind[0], X.wind[1], X.wind[2]);
   Q.w1 = s3(X.wind[1], X.wind[2], X.wind[0]);
   Q.w2 = s3(X.wind[2], X.wind[0], X.wind[1]);
@@ -123,8 +130,8 @@ __device__ __forceinline__ QCtx<T> qctx(const C& c, const StepCtx<T>& X, int r) 
     }
     cl = Q.row ? s3(l[0], l[1], l[2]) : -inf;
     ch = Q.row ? s3(h[0], h[1], h[2]) : inf;
-    vl = s3(a[0], a[1], a[2]);
-    vh = s3(b[0], b[1], b[2]);
+    vl = Q.row ? s3(a[0], a[1], a[2]) : -inf;  // lane 3's zero slots clip to themselves
+    vh = Q.row ? s3(b[0], b[1], b[2]) : inf;
     clip = Q.row && (r == 0 ? k[0] : (r == 1 ? k[1] : k[2]));
   };
   bool pclip;
@@ -135,22 +142,22 @@ __device__ __forceinline__ QCtx<T> qctx(const C& c, const StepCtx<T>& X, int r) 
   lim(FW_V_ACT0, Q.act_cl, Q.act_ch, Q.act_vl, Q.act_vh, Q.act_clip);
   Q.dmax = s3(c.dot_max[0], c.dot_max[1], c.dot_max[2]);
   Q.dclip = Q.row && ((c.dotmask >> (r & 3)) & 1u);
-  Q.ac0 = s3(c.ac[0][0], c.ac[1][0], c.ac[2][0]);
-  Q.ac1 = s3(c.ac[0][1], c.ac[1][1], c.ac[2][1]);
-  Q.ac2 = s3(c.ac[0][2], c.ac[1][2], c.ac[2][2]);
-  Q.ac3 = s3(c.ac[0][3], c.ac[1][3], c.ac[2][3]);
-  Q.ac4 = s3(c.ac[0][4], c.ac[1][4], c.ac[2][4]);
-  Q.ac5 = s3(c.ac[0][5], c.ac[1][5], c.ac[2][5]);
+  auto s3r = [&](T a0, T a1, T a2) { return Q.row ? s3(a0, a1, a2) : z; };
+  Q.ac0 = s3r(c.ac[0][0], c.ac[1][0], c.ac[2][0]);
+  Q.ac1 = s3r(c.ac[0][1], c.ac[1][1], c.ac[2][1]);
+  Q.ac2 = s3r(c.ac[0][2], c.ac[1][2], c.ac[2][2]);
+  Q.ac3 = s3r(c.ac[0][3], c.ac[1][3], c.ac[2][3]);
+  Q.ac4 = s3r(c.ac[0][4], c.ac[1][4], c.ac[2][4]);
+  Q.ac5 = s3r(c.ac[0][5], c.ac[1][5], c.ac[2][5]);
   // pyfly.py:1659-1683: p' = g1 PQ - g2 QR + g3 l + g4 n;  q' = g5 PR - g6 (P^2 - R^2) + m / Jy;
   //                     r' = g7 PQ - g1 QR + g4 l + g8 n
-  const T z = T(0);
-  Q.kpq = s3(c.gam[1], z, c.gam[7]);
-  Q.kqr = s3(-c.gam[2], z, -c.gam[1]);
-  Q.kpr = s3(z, c.gam[5], z);
-  Q.kpp = s3(z, -c.gam[6], z);
-  Q.kt0 = s3(c.gam[3], z, c.gam[4]);
-  Q.kt1 = s3(z, c.inv_Jy, z);
-  Q.kt2 = s3(c.gam[4], z, c.gam[8]);
+  Q.kpq = s3r(c.gam[1], z, c.gam[7]);
+  Q.kqr = s3r(-c.gam[2], z, -c.gam[1]);
+  Q.kpr = s3r(z, c.gam[5], z);
+  Q.kpp = s3r(z, -c.gam[6], z);
+  Q.kt0 = s3r(c.gam[3], z, c.gam[4]);
+  Q.kt1 = s3r(z, c.inv_Jy, z);
+  Q.kt2 = s3r(c.gam[4], z, c.gam[8]);
   return Q;
 }
 
@@ -173,17 +180,31 @@ __device__ __forceinline__ T ucond(const C& c, int v, T x, int& key, int k) {
 
 // PyFly._dynamics (pyfly.py:1450-1482) of lane Q.r's rows: s = this lane's 6 stage values,
 // ds = their derivatives.  Returns the first violated condition of the aircraft (0 = none).
+// Written for the lone-wave tail, where every VALU instruction costs its issue slot: the checks a
+// configuration does not have are compiled out (mask tests fold for the SpecCfg views), lane 3's zero
+// rows need no selects (QCtx), and the per-row force rotation shares its beta rotation.
 template <typename T, typename C, typename A>
 __device__ __forceinline__ int rhs_quad(const C& c, const A& a, const QCtx<T>& Q, bool first, const T* s, T* ds) {
   int key = KEY_NONE;
   T om = s[1], vel = s[3], av = s[4], ad = s[5];
   T elev = Q.elev0, ail = Q.ail0;
   if (!first) {  // _set_states_from_ode_solution(save=False) + Actuation.set_states (pyfly.py:479-492)
-    om = qcond(om, Q.om_cl, Q.om_ch, Q.om_vl, Q.om_vh, Q.om_clip, key, Q.r);
-    (void)qcond(s[2], Q.pos_cl, Q.pos_ch, T(0), T(0), false, key, 3 + Q.r);
-    vel = qcond(vel, Q.vel_cl, Q.vel_ch, Q.vel_vl, Q.vel_vh, Q.vel_clip, key, 6 + Q.r);
-    av = qcond(av, Q.act_cl, Q.act_ch, Q.act_vl, Q.act_vh, Q.act_clip, key, 9 + Q.r);
-    ad = Q.dclip ? clipv(ad, -Q.dmax, Q.dmax) : ad;
+    // a row variable: constraint (first violation wins) then clip.  All three rows clipping: lane 3
+    // (zeros, clip interval of row 2) clips too, without the per-lane select.
+    auto rowcond = [&](T x, int v0, T cl, T ch, T vl, T vh, bool clip, int k) {
+      if (c.cmask & (7u << v0)) {
+        const bool viol = (x < cl) | (x > ch);
+        key = (key == KEY_NONE && viol) ? k : key;
+      }
+      if (((c.clipmask >> v0) & 7u) == 7u) return clipv(x, vl, vh);
+      if (c.clipmask & (7u << v0)) return clip ? clipv(x, vl, vh) : x;
+      return x;
+    };
+    om = rowcond(om, FW_V_OMEGA_P, Q.om_cl, Q.om_ch, Q.om_vl, Q.om_vh, Q.om_clip, Q.r);
+    (void)rowcond(s[2], FW_V_POS_N, Q.pos_cl, Q.pos_ch, T(0), T(0), false, 3 + Q.r);  // checked, never clipped
+    vel = rowcond(vel, FW_V_VEL_U, Q.vel_cl, Q.vel_ch, Q.vel_vl, Q.vel_vh, Q.vel_clip, 6 + Q.r);
+    av = rowcond(av, FW_V_ACT0, Q.act_cl, Q.act_ch, Q.act_vl, Q.act_vh, Q.act_clip, 9 + Q.r);
+    if (c.dotmask) ad = Q.dclip ? clipv(ad, -Q.dmax, Q.dmax) : ad;
     const T a0 = bc<0>(av), a1 = bc<1>(av);
     if (c.elevon) {
       ail = (-a0 + a1) * T(0.5);
@@ -238,19 +259,28 @@ __device__ __forceinline__ int rhs_quad(const C& c, const A& a, const QCtx<T>& Q
     cb = rxz * iVr;
   }
   const T V2a = Va * Va;
-  const T ex = fexp(l1 ? a.M * (alpha + a.a0) : -a.M * (alpha - a.a0));
+  // lane 1: exp(M (alpha + a0)); the others: exp(-M (alpha - a0)) = exp(-M alpha + M a0)
+  T ex;
+  if constexpr (sizeof(T) == 4) {
+    const T l2e = T(1.4426950408889634);
+    ex = __builtin_amdgcn_exp2f(fmaf(Q.sgn1 * (a.M * l2e), alpha, a.M * a.a0 * l2e));
+  } else {
+    ex = fexp(l1 ? a.M * (alpha + a.a0) : -a.M * (alpha - a.a0));
+  }
   const T ex1 = bc<0>(ex), ex2 = bc<1>(ex);
   const T sigma = frcp(T(1) + a.sig_c * frcp(T(1) + ex1 + ex2));  // overflow-safe form, see rhs()
   const T osig = T(1) - sigma;
-  const T sgna = sgn(alpha);
+  // sgn(alpha) sin(alpha)^2 = sin(alpha) |sin(alpha)|: sin has alpha's sign on [-pi, pi] and the
+  // product is 0 where it does not (pyfly.py:1547-1579 multiply by np.sign(alpha))
+  const T ssa = sa * fabs(sa);
   const T CLlin = a.CL0 + a.CLa * alpha;
-  const T CL = osig * CLlin + sigma * (T(2) * sgna * sa * sa * ca);
+  const T CL = osig * CLlin + sigma * (T(2) * ssa * ca);
   const T qn = q * iVa;
   const T flift = a.qS * V2a * (CL + a.kCLq * qn + a.CLde * elev);
-  const T CD = a.CDp + osig * (CLlin * CLlin) * a.inv_pi_e_ar + sigma * (T(2) * sgna * (sa * sa * sa));
+  const T CD = a.CDp + osig * (CLlin * CLlin) * a.inv_pi_e_ar + sigma * (T(2) * (ssa * sa));
   const T CDb = a.CDb1 * beta + a.CDb2 * beta * beta;
   const T fdrag = a.qS * V2a * (CD + CDb + a.kCDq * qn + a.CDde * elev * elev);
-  const T Cm = osig * (a.Cm0 + a.Cma * alpha) + sigma * (a.Cmfp * sgna * sa * sa);
+  const T Cm = osig * (a.Cm0 + a.Cma * alpha) + sigma * (a.Cmfp * ssa);
   const T mm = a.qSc * V2a * (Cm + a.kCmq * qn + a.Cmde * elev);
   const T bp = a.hb * p * iVa, br = a.hb * r * iVa;
   // side force / roll / yaw moment: the same formula with row constants, one item per lane (lane 3
@@ -263,11 +293,11 @@ __device__ __forceinline__ int rhs_quad(const C& c, const A& a, const QCtx<T>& Q
   // Row selections below pick among values computed on every lane: selects, not divergent branches
   // (a conditional expression with work in its arms compiles to exec-masked branches here).
   const bool r0 = Q.r == 0, r1 = Q.r == 1;
-  // row r of f_aero = R_euler(0, alpha, beta) . [-D, Y, -L]
-  const T fa0 = ca * cb * (-fdrag) + ca * sb * fy - sa * (-flift);
-  const T fa1 = -sb * (-fdrag) + cb * fy;
-  const T fa2 = sa * cb * (-fdrag) + sa * sb * fy + ca * (-flift);
-  const T fa = r0 ? fa0 : (r1 ? fa1 : fa2);
+  // row r of f_aero = R_euler(0, alpha, beta) . [-D, Y, -L] = R_alpha . (R_beta . [-D, Y, -L]):
+  // U = cb (-D) + sb Y, then rows (ca U + sa L, sb D + cb Y, sa U - ca L)
+  const T U = cb * (-fdrag) + sb * fy;
+  const T fa02 = (r0 ? ca : sa) * U + (r0 ? sa : -ca) * flift;
+  const T fa = r1 ? sb * fdrag + cb * fy : fa02;
   // gravity: column 2 of R(q) (the diagonal term in the raw-quaternion form of pyfly.py:1493-1499)
   const T Dr = er * er + e0 * e0 - er1 * er1 - er2 * er2;
   const T fg = a.mg * (r0 ? Rr2 : (r1 ? Rr1 : Dr));
@@ -289,16 +319,17 @@ __device__ __forceinline__ int rhs_quad(const C& c, const A& a, const QCtx<T>& Q
   const T dp = Dr * vel + T(2) * (er * er1 - er2 * e0) * vel1 +
                T(2) * (er * er2 + er1 * e0) * vel2;
   // _f_v_dot (pyfly.py:1685-1704), row r
-  const T dv = om2 * vel1 - om1 * vel2 + fr * a.inv_mass;
+  const T dv = om2 * vel1 - om1 * vel2 + fr * (a.inv_mass * Q.rowf);
   // Actuation.rhs (pyfly.py:519-543), actuator r
   const T da = av * Q.ac0 + Q.sp * Q.ac2 + ad * Q.ac1;
   const T dd = av * Q.ac3 + Q.sp * Q.ac5 + ad * Q.ac4;
+  // lane 3: de0, then zeros -- its slots 1..5 are 0 and its coefficients (QCtx) are 0
   ds[0] = Q.row ? deps : de0;
-  ds[1] = Q.row ? dw : T(0);
-  ds[2] = Q.row ? dp : T(0);
-  ds[3] = Q.row ? dv : T(0);
-  ds[4] = Q.row ? da : T(0);
-  ds[5] = Q.row ? dd : T(0);
+  ds[1] = dw;
+  ds[2] = dp;
+  ds[3] = dv;
+  ds[4] = da;
+  ds[5] = dd;
   if (!any_lane(key != KEY_NONE)) return 0;  // (wave-uniform) no condition violated: the common case
   key = min4(key);
   return key == KEY_NONE ? 0 : FW_TERM_VAR(key_var(key));
@@ -425,7 +456,7 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
   for (;;) {
     if (!seeded) {
       if (begin_step) {  // RungeKutta._step_impl entry (rk.py:111-124)
-        min_step = 10.0 * fabs(nextafter(t, 1e300) - t);
+        min_step = min_step_at(t);
         if (h_abs < min_step) h_abs = min_step;
         rejected = false;
       }
@@ -703,7 +734,7 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
       stage = 2;
     }
     if (begin_step) {  // RungeKutta._step_impl entry (rk.py:111-124)
-      min_step = 10.0 * fabs(nextafter(t, 1e300) - t);
+      min_step = min_step_at(t);
       if (h_abs < min_step) h_abs = min_step;
       rejected = false;
       begin_attempt = true;
