@@ -262,7 +262,11 @@ enum fw_init_field {
 #define FW_BLK_STEPS 4      /* 1 row, uint32: steps_count | steps_for_current_target << 16 */
 #define FW_BLK_COMMAND 5    /* 3 rows, T: last constrained commands (input order) */
 #define FW_BLK_PARAMS 6     /* FW_NPARAM rows, T: per-aircraft parameters (only with env->n_rand > 0) */
-#define FW_NBLK 7
+#define FW_BLK_ACT_RING 7   /* window*3 rows, T: raw actions, action number k (1-based) in slot (k-1) % window,
+                               row slot*3 + component (the action-delta reward / action-window observation) */
+#define FW_BLK_CMD_RING 8   /* window*3 rows, T: constrained commands, same layout (unscaled action windows) */
+#define FW_BLK_GOAL 9       /* 4 rows, uint32: the last 128 goal-status bits ("all"), bit 0 of row 0 newest */
+#define FW_NBLK 10
 
 typedef struct fw_handle fw_handle;
 
@@ -338,6 +342,9 @@ int fw_observe(fw_handle* h, void* obs_dev, void* stream);
 
 int fw_get_state(fw_handle* h, int32_t block, void* dst_dev, void* stream);
 int fw_set_state(fw_handle* h, int32_t block, const void* src_dev, void* stream);
+/* Rows of a state block (its [rows][N] shape) on this handle; element size: uint32 for FW_BLK_STEPS and
+ * FW_BLK_GOAL, the handle's precision otherwise.  A block the handle does not hold is FW_E_INVALID. */
+int fw_block_rows(const fw_handle* h, int32_t block, int32_t* rows);
 
 /* Curriculum / config update between steps (FixedWingAircraft.set_curriculum_level
  * recomputes ranges on the host and pushes a new env/sim config).            */

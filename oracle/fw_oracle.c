@@ -921,6 +921,30 @@ int orc_env_step(const fw_sim_config* c, const fw_env_config* e, orc_env* s, con
 
 int orc_env_state_size(void) { return (int)sizeof(orc_env); }
 
+/* Teacher forcing (tests only): put an env into a mid-episode state given as the device keeps it -- ODE
+ * state, derived values (whose successful-step history[-1] equals them), steady wind, targets, step
+ * counters, the last n_act raw actions (oldest first) and the last n_goal "all" goal bits (oldest
+ * first).  The next orc_env_step is then the reference's step from exactly that state. */
+void orc_env_set_state(void* state, const double* y, const double* der, const double* wind, const double* target,
+                       int32_t steps, int32_t steps_tgt, const double* act_hist, int32_t n_act, const uint8_t* goals,
+                       int32_t n_goal) {
+  orc_env* s = (orc_env*)state;
+  for (int i = 0; i < NY; i++) s->y[i] = y[i];
+  for (int i = 0; i < 8; i++) s->der[i] = der[i];
+  for (int i = 0; i < 6; i++) s->hist[i] = der[i];
+  for (int i = 0; i < 3; i++) s->hist[6 + i] = y[4 + i];
+  for (int i = 0; i < 3; i++) s->wind[i] = wind[i];
+  for (int i = 0; i < 3; i++) s->target[i] = target[i];
+  s->steps = steps;
+  s->steps_tgt = steps_tgt;
+  s->n_act = n_act < FW_MAX_WINDOW ? n_act : FW_MAX_WINDOW;
+  for (int k = 0; k < s->n_act; k++)
+    for (int i = 0; i < 3; i++) s->act_hist[k][i] = act_hist[3 * k + i];
+  s->n_cmd = 0;
+  s->n_goal = n_goal < 2048 ? n_goal : 2048;
+  for (int k = 0; k < s->n_goal; k++) s->goal_all[k] = goals[k];
+}
+
 /* Give the env's aircraft its own parameter values (after orc_env_reset, which clears them). */
 void orc_env_set_params(void* state, const fw_sim_config* c, const double* params) {
   orc_env* s = (orc_env*)state;

@@ -52,6 +52,9 @@ def lib():
         L.orc_env_step.restype = ctypes.c_int
         L.orc_env_step.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _d, _d, ctypes.c_int64, _d, _d,
                                    _i32, _i32]
+        L.orc_env_set_state.restype = None
+        L.orc_env_set_state.argtypes = [ctypes.c_void_p, _d, _d, _d, _d, ctypes.c_int32, ctypes.c_int32, _d,
+                                        ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
         L.orc_env_observe.restype = None
         L.orc_env_observe.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, _d]
         for f in ("orc_env_state_size", "orc_sizeof_sim_config", "orc_sizeof_env_config"):
@@ -148,6 +151,17 @@ class OracleEnv:
             raise RuntimeError("reset constraint violation code %d" % t)
         self.noise = np.ascontiguousarray(noise if noise is not None else np.zeros((4, 1)), dtype=np.float64)
         return obs
+
+    def set_state(self, y, der, wind, target, steps, steps_tgt, act_hist, goals):
+        """Teacher forcing: the env continues from a device state (orc_env_set_state).  act_hist: the last
+        raw actions, oldest first ([k][3]); goals: the last "all" goal bits, oldest first."""
+        a = np.ascontiguousarray(np.asarray(act_hist, dtype=np.float64).reshape(-1, 3))
+        g = np.ascontiguousarray(np.asarray(goals, dtype=np.uint8))
+        self.L.orc_env_set_state(self.buf, _p(np.ascontiguousarray(y, dtype=np.float64)),
+                                 _p(np.ascontiguousarray(der, dtype=np.float64)),
+                                 _p(np.ascontiguousarray(wind, dtype=np.float64)),
+                                 _p(np.ascontiguousarray(target, dtype=np.float64)), int(steps), int(steps_tgt),
+                                 _p(a), a.shape[0], g.ctypes.data_as(ctypes.c_void_p), g.shape[0])
 
     def set_params(self, params):
         """This aircraft's own simulator parameters (after reset, which clears them)."""

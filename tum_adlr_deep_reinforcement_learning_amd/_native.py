@@ -132,6 +132,7 @@ SIGNATURES = {
     "fw_observe": (_c.c_int, [_vp, _vp, _vp]),
     "fw_get_state": (_c.c_int, [_vp, _i32, _vp, _vp]),
     "fw_set_state": (_c.c_int, [_vp, _i32, _vp, _vp]),
+    "fw_block_rows": (_c.c_int, [_vp, _i32, _c.POINTER(_i32)]),
     "fw_update_config": (_c.c_int, [_vp, _vp, _vp]),
     "fw_set_metrics_output": (_c.c_int, [_vp, _vp]),
     # include/fwrollout.h

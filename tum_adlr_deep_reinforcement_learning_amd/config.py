@@ -63,7 +63,8 @@ FW_MAX_OBS_LEN, FW_MAX_OBS_HIST = 16, 64
  FW_I_ACT0, FW_I_ACT0_DOT, FW_I_ACT1, FW_I_ACT1_DOT, FW_I_ACT2, FW_I_ACT2_DOT, FW_I_WIND_N, FW_I_WIND_E,
  FW_I_WIND_D, FW_NINIT) = range(22)
 
-FW_BLK_ODE, FW_BLK_DERIVED, FW_BLK_TARGET, FW_BLK_WIND, FW_BLK_STEPS, FW_BLK_COMMAND, FW_BLK_PARAMS = range(7)
+(FW_BLK_ODE, FW_BLK_DERIVED, FW_BLK_TARGET, FW_BLK_WIND, FW_BLK_STEPS, FW_BLK_COMMAND, FW_BLK_PARAMS,
+ FW_BLK_ACT_RING, FW_BLK_CMD_RING, FW_BLK_GOAL) = range(10)
 FW_DIST_GAUSSIAN, FW_DIST_UNIFORM = 0, 1
 
 # episode-metric record (include/fwsim.h FW_M_*): name -> (first column, info keys)

@@ -280,8 +280,8 @@ FW_HD float fpow(float a, float p) {  // a > 0
 FW_HD double fatan2(double y, double x) { return atan2(y, x); }
 FW_HD float fatan2(float y, float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  const float ax = fabsf(x), ay = fabsf(y);
-  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  // |x|, |y| stay source modifiers of the max / min / compare (no separate abs instructions)
+  const float mx = fmaxf(fabsf(x), fabsf(y)), mn = fminf(fabsf(x), fabsf(y));
   const float t = mn * __builtin_amdgcn_rcpf(mx);
   const float q = t * t;
   float p = 0.0029030926525592804f;
@@ -294,7 +294,7 @@ FW_HD float fatan2(float y, float x) {
   p = fmaf(p, q, -0.3333309292793274f);
   p = fmaf(p, q, 1.0f);
   float r = t * p;
-  r = ay > ax ? 1.5707963267948966f - r : r;
+  r = fabsf(y) > fabsf(x) ? 1.5707963267948966f - r : r;
   r = x < 0.0f ? 3.141592653589793f - r : r;
   r = mx == 0.0f ? 0.0f : r;
   return copysignf(r, y);

@@ -1843,8 +1843,25 @@ static int block_info(const fw_handle* h, int32_t block, size_t* off, int* rows,
     case FW_BLK_PARAMS:
       if (!h->o_prm) return set_err(FW_E_INVALID, "handle has no per-aircraft parameters (env n_rand = 0)");
       *off = h->o_prm; *rows = FW_NPARAM; *esz = T_; return FW_OK;
+    case FW_BLK_ACT_RING:
+      if (!h->has_env) return set_err(FW_E_INVALID, "handle has no env (no action ring)");
+      *off = h->o_act; *rows = 3 * h->act_window; *esz = T_; return FW_OK;
+    case FW_BLK_CMD_RING:
+      if (!h->has_env || !h->cmd_window) return set_err(FW_E_INVALID, "handle keeps no command ring");
+      *off = h->o_cmdring; *rows = 3 * h->cmd_window; *esz = T_; return FW_OK;
+    case FW_BLK_GOAL: *off = h->o_goal; *rows = 4; *esz = 4; return FW_OK;
     default: return set_err(FW_E_INVALID, "unknown state block");
   }
+}
+
+int fw_block_rows(const fw_handle* h, int32_t block, int32_t* rows) {
+  if (!h || !rows) return set_err(FW_E_INVALID, "NULL argument");
+  size_t off, esz;
+  int r;
+  const int v = block_info(h, block, &off, &r, &esz);
+  if (v) return v;
+  *rows = r;
+  return FW_OK;
 }
 
 // Blocks are exchanged densely as [rows][N].

@@ -273,15 +273,27 @@ __device__ __forceinline__ int rhs_quad(const C& c, const A& a, const QCtx<T>& Q
   // sgn(alpha) sin(alpha)^2 = sin(alpha) |sin(alpha)|: sin has alpha's sign on [-pi, pi] and the
   // product is 0 where it does not (pyfly.py:1547-1579 multiply by np.sign(alpha))
   const T ssa = sa * fabs(sa);
-  const T CLlin = a.CL0 + a.CLa * alpha;
-  const T CL = osig * CLlin + sigma * (T(2) * ssa * ca);
   const T qn = q * iVa;
-  const T flift = a.qS * V2a * (CL + a.kCLq * qn + a.CLde * elev);
-  const T CD = a.CDp + osig * (CLlin * CLlin) * a.inv_pi_e_ar + sigma * (T(2) * (ssa * sa));
-  const T CDb = a.CDb1 * beta + a.CDb2 * beta * beta;
-  const T fdrag = a.qS * V2a * (CD + CDb + a.kCDq * qn + a.CDde * elev * elev);
-  const T Cm = osig * (a.Cm0 + a.Cma * alpha) + sigma * (a.Cmfp * ssa);
-  const T mm = a.qSc * V2a * (Cm + a.kCmq * qn + a.Cmde * elev);
+  // lift / drag / pitch moment (pyfly.py:1529-1579) as ONE formula with row constants, lane r = row r
+  // (lane 3 repeats lane 0), then broadcast:
+  //   K V2a (c0 + osig (pa + pb alpha)(pg + ph alpha) + sigma ssa (mu ca + mv sa + mw)
+  //          + kq q/Va + kde elev + kde2 elev^2 + kb1 beta + kb2 beta^2)
+  //   lift:   CL0 + CLa a, stall 2 ca,  C_L_q c/2,  C_L_de elev                       (K = rho/2 S)
+  //   drag:   CDp + (CL0 + CLa a)^2 / (pi e AR), stall 2 sa, C_D_q c/2, C_D_de elev^2,
+  //           C_D_beta1 b + C_D_beta2 b^2                                            (K = rho/2 S)
+  //   moment: Cm0 + Cma a, stall C_m_fp, C_m_q b/2, C_m_de elev                        (K = rho/2 S c)
+  const int rr = Q.r == 3 ? 0 : Q.r;
+  auto s3r = [rr](T x0, T x1, T x2) { return rr == 0 ? x0 : (rr == 1 ? x1 : x2); };
+  const T z = T(0), one = T(1), two = T(2);
+  const T pa = s3r(a.CL0, a.CL0, a.Cm0), pb = s3r(a.CLa, a.CLa, a.Cma);
+  const T pg = s3r(one, a.CL0 * a.inv_pi_e_ar, one), ph = s3r(z, a.CLa * a.inv_pi_e_ar, z);
+  const T c0 = s3r(z, a.CDp, z), mu = s3r(two, z, z), mv = s3r(z, two, z), mw = s3r(z, z, a.Cmfp);
+  const T kq = s3r(a.kCLq, a.kCDq, a.kCmq), kde = s3r(a.CLde, z, a.Cmde), kde2 = s3r(z, a.CDde, z);
+  const T kb1 = s3r(z, a.CDb1, z), kb2 = s3r(z, a.CDb2, z), K = s3r(a.qS, a.qS, a.qSc);
+  const T P = (pa + pb * alpha) * (pg + ph * alpha);
+  const T Cr = c0 + osig * P + (sigma * ssa) * (mu * ca + mv * sa + mw);
+  const T Fr = K * V2a * (Cr + kq * qn + kde * elev + kde2 * (elev * elev) + kb1 * beta + kb2 * (beta * beta));
+  const T flift = bc<0>(Fr), fdrag = bc<1>(Fr), mm = bc<2>(Fr);
   const T bp = a.hb * p * iVa, br = a.hb * r * iVa;
   // side force / roll / yaw moment: the same formula with row constants, one item per lane (lane 3
   // repeats lane 0's), broadcast

@@ -202,19 +202,24 @@ class Engine:
         return self.obs
 
     # ------------------------------------------------------------------
-    _ROWS = {C.FW_BLK_ODE: C.FW_NY, C.FW_BLK_DERIVED: 8, C.FW_BLK_TARGET: 3, C.FW_BLK_WIND: 3, C.FW_BLK_STEPS: 1,
-             C.FW_BLK_COMMAND: 3, C.FW_BLK_PARAMS: C.FW_NPARAM}
+    _U32 = (C.FW_BLK_STEPS, C.FW_BLK_GOAL)
+
+    def block_rows(self, blk):
+        """Rows of a state block on this handle (fw_block_rows): [rows][n]."""
+        v = ctypes.c_int32()
+        _native.check(self.lib.fw_block_rows(self.h, int(blk), ctypes.byref(v)), "fw_block_rows")
+        return v.value
 
     def get_block(self, blk):
-        rows = self._ROWS[blk]
-        dt = torch.int32 if blk == C.FW_BLK_STEPS else self.dtype
+        rows = self.block_rows(blk)
+        dt = torch.int32 if blk in self._U32 else self.dtype
         out = torch.empty(rows, self.n, dtype=dt, device=self.device)
         _native.check(self.lib.fw_get_state(self.h, blk, _ptr(out), self.stream()), "fw_get_state")
         return out
 
     def set_block(self, blk, value):
-        rows = self._ROWS[blk]
-        dt = torch.int32 if blk == C.FW_BLK_STEPS else self.dtype
+        rows = self.block_rows(blk)
+        dt = torch.int32 if blk in self._U32 else self.dtype
         v = torch.as_tensor(value, dtype=dt).to(self.device).reshape(rows, self.n).contiguous()
         _native.check(self.lib.fw_set_state(self.h, blk, _ptr(v), self.stream()), "fw_set_state")
         torch.cuda.current_stream(self.device).synchronize()
