@@ -306,8 +306,10 @@ def test_env_step_teacher_forced(precision):
     An env-step whose RK45 evaluation count differs from the oracle's is an accept/reject flip (counted,
     bounded).  On every other env-step: done and termination identical; fp64: obs and reward within 1e-9
     (1 + |ref|); fp32: obs and reward within 1e-4 (1 + |ref|) (SURVEY 8(d) gate 2 at the env level) on
-    >= 98 % of them -- an equal count is not an equal step grid, see the gate-2 test -- and every one
-    within 2e-3 (1 + |ref|)."""
+    >= 99.9 % of them -- an equal count is not an equal step grid, see the gate-2 test -- and every one
+    within 2e-3 (1 + |ref|); flips <= 0.5 %.  The angle of attack is weighed by its conditioning 1 / |cos beta| (round 3:
+    one fp32 env-step in 49152 flew sideways and its alpha moved 0.12 rad with the reward equal to
+    1.5e-6)."""
     from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
     from oracle import oracle as O
     spec = C.EnvSpec(sim_config_kw={"turbulence": False})
@@ -320,6 +322,8 @@ def test_env_step_teacher_forced(precision):
     for _ in range(150):  # a steady-state mix: mid-episode, tumbling, freshly reset aircraft
         eng.env_step(torch.rand(n, 3, generator=gen, device=DEV, dtype=eng.dtype) * 2 - 1)
     envs = [O.OracleEnv(spec.sim.struct(), spec.struct(), spec.n_obs) for _ in range(n)]
+    names = [(o["name"], o["type"]) for o in spec.cfg["observation"]["states"]]
+    i_alpha, i_beta = names.index(("alpha", "state")), names.index(("beta", "state"))
     rng = np.random.RandomState(8)
     tight = 1e-9 if precision == "float64" else 1e-4
     total = flips = tight_ok = 0
@@ -342,6 +346,9 @@ def test_env_step_teacher_forced(precision):
             assert dd == dn[j] and tt == tm[j], (j, dd, dn[j], tt, tm[j])
             got = to[j] if dn[j] else o[j]
             eo = np.abs(got - oo) / (1 + np.abs(oo))
+            # alpha = atan2(w_r, u_r) is ill-conditioned when the aircraft flies sideways (beta near
+            # +-90 deg: the x-z airspeed Va cos(beta) is small): its error is weighed by that conditioning
+            eo[i_alpha] /= max(1.0, 1.0 / max(abs(np.cos(oo[i_beta])), 1e-12))
             err = max(float(eo.max()), abs(rr - r[j]) / (1 + abs(rr)))
             if err > worst:
                 worst = err
@@ -354,5 +361,6 @@ def test_env_step_teacher_forced(precision):
     if precision == "float64":
         assert flips <= 0.002 * total and tight_ok == same
     else:
-        assert flips <= 0.03 * total and tight_ok >= 0.98 * same and worst <= 2e-3
+        # measured (round 3): 17 flips in 49152, 99.996 % within 1e-4, worst 7.5e-4 (a sideways flyer)
+        assert flips <= 0.005 * total and tight_ok >= 0.999 * same and worst <= 2e-3
     eng.close()

@@ -277,7 +277,11 @@ class FixedWingVecEnv(VecEnv):
         fused launch (Engine.env_rollout): the SAC / TD3 warm-up with uniform actions, scripted command
         sequences.  Auto-reset as in ``step``.  Returns device tensors (obs [K, N, *obs_shape], reward
         [K][N], done [K][N] bool, termination code [K][N]); terminal observations and Monitor records of
-        the done steps are in ``engine.rollout_terminal_obs`` / ``engine.rollout_episode``."""
+        the done steps are in ``engine.rollout_terminal_obs`` / ``engine.rollout_episode``; the episode
+        metrics (``engine.metrics``) hold the last episode each env finished inside the launch."""
+        if self._hists is not None:
+            raise NotImplementedError("rollout() resets envs inside the launch, so per-env histories cannot be "
+                                      "recorded: use step() with record_history=True")
         a = torch.as_tensor(actions).to(device=self.device, dtype=self.engine.dtype)
         obs, rew, done, term = self.engine.env_rollout(a.reshape(a.shape[0], self.num_envs, -1).contiguous())
         shape = self.observation_space.shape
