@@ -577,8 +577,8 @@ def main():
                      "unit": "Ginst/s (wave64 VALU issue)", "frac": valu_rate / VALU_ISSUE_PEAK,
                      "valu_insts_per_launch": pm["valu_insts_per_launch"],
                      "valu_insts_per_wave": pm["valu_insts_per_launch"] * 64.0 / n,
-                     "source": "SQ_INSTS_VALU per steady-state dispatch from profiles/pmc_env_step.json (a long "
-                               "window of the same workload) over this window's kernel_ms"}
+                     "source": "SQ_INSTS_VALU per k_env_step dispatch from profiles/pmc_env_step.json (%s) over "
+                               "this window's kernel_ms" % pm.get("dispatches")}
 
     rollout = None
     if args.rollout_steps < 0:
@@ -616,9 +616,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_env_step": rd + wr, "kernel_ms": kern_ms,
-                         "traffic_source": ("profiles/pmc_env_step.json: FETCH_SIZE+WRITE_SIZE per steady-state "
-                                            "dispatch of the same workload over a long window, not this K-step "
-                                            "window" if traffic is not None else None),
+                         "traffic_source": ("profiles/pmc_env_step.json: calibrated FETCH_SIZE + WRITE_SIZE per "
+                                            "k_env_step dispatch, %s" % pm.get("dispatches")) if traffic is not None
+                         else None,
                          "binding_limit": "valu issue + RK45 straggler latency (see roofline_valu, DESIGN.md 3)"},
             "roofline_valu": roof_valu,
             "early_regime": {"steps": 96, "kernel_ms": early_ms, "env_steps_per_s_per_gpu": n / (early_ms * 1e-3)},

@@ -19,7 +19,7 @@ W = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 prep = int(sys.argv[4]) if len(sys.argv) > 4 else 1000
 rows = []
 for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
-    rows += [r for r in csv.DictReader(open(f)) if "k_env_step" in r["Kernel_Name"] and "IfN" in r["Kernel_Name"]]
+    rows += [r for r in csv.DictReader(open(f)) if ("k_env_step<float" in r["Kernel_Name"] or "k_env_stepIf" in r["Kernel_Name"])]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
 a = prep + W

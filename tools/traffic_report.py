@@ -60,7 +60,8 @@ def main(base):
     out = {
         "kernel": "k_env_step", "workload": "65536 aircraft fp32, turbulence off, U(-1,1) actions",
         "envs": 65536, "precision": "float32", "turbulence": False, "metrics": bool(spec.metrics_enabled),
-        "regime": "steady", "dispatches": "last %d k_env_step dispatches of the bench (its timed window)" % last,
+        "regime": "steady", "dispatches": os.environ.get("PMC_WINDOW", "last %d k_env_step dispatches of the bench "
+                                                                      "(its timed window)" % last),
         "valu_insts_per_launch": valu.get("SQ_INSTS_VALU"), "sq_counters_per_launch": valu or None,
         "fetch_size_kib_per_launch": ef, "write_size_kib_per_launch": ew, "launches": [nf, nw],
         "calibration": {"fetch_kib_k_calib_read": cf, "write_kib_k_calib_write": cw, "factor_read": f_read,
