@@ -504,7 +504,8 @@ def main():
                     help="skip the stats-enabled replay of the timed window (per-launch times, nfev, budget hits)")
     ap.add_argument("--no-fp64", action="store_true",
                     help="skip the secondary line at the reference's own precision (fp64 kernels)")
-    ap.add_argument("--fp64-prep", type=int, default=200, help="untimed steps before the fp64 line's window")
+    ap.add_argument("--fp64-prep", type=int, default=-1,
+                    help="untimed steps before the fp64 line's window (default: --prep)")
     ap.add_argument("--lanes", type=int, default=0,
                     help="lanes per aircraft of k_env_step: 0 = automatic by shard size, 1, or 4 (quad integrator)")
     args = ap.parse_args()
@@ -552,17 +553,17 @@ def main():
     fp64 = None
     if not args.no_fp64 and args.precision == "float32":  # secondary: the reference's own precision
         _log("fp64 line")
-        # bounded: the fp64 kernels are 512-register instances with scratch spills whose straggler tail
-        # costs orders of magnitude more than fp32, so a 1000-step prep would take minutes
+        # the same schedule as the fp32 line (seeds, prep, window, long window) on the fp64 kernels
         a64 = argparse.Namespace(**vars(args))
-        a64.prep, a64.long_window = args.fp64_prep, 0
-        f_el, f_k, f_early, _, _ = timed_env_steps(n, a64, spec, dev, rank, world, rank * n, precision="float64")
+        a64.prep = args.fp64_prep if args.fp64_prep >= 0 else args.prep
+        f_el, f_k, f_early, f_long, _ = timed_env_steps(n, a64, spec, dev, rank, world, rank * n,
+                                                        precision="float64")
         fp64 = {"dtype": "f64", "value": args.envs * args.steps / f_el, "ms_per_step": f_el / args.steps * 1e3,
                 "kernel_ms": f_k, "prep_steps": a64.prep, "steps": args.steps,
                 "early_regime": {"steps": 96, "kernel_ms": f_early,
                                  "env_steps_per_s_per_gpu": n / (f_early * 1e-3)},
-                "note": "window after %d steps (not the fp32 line's 1000): the fp64 straggler tail is "
-                        "spill-bound, see DESIGN.md" % a64.prep,
+                "long_window": ({"steps": args.long_window, "kernel_ms": f_long,
+                                 "env_steps_per_s": args.envs / (f_long * 1e-3)} if f_long > 0 else None),
                 "isa": "profiles/r03_isa_resources.txt (VGPR / spill counts per kernel instance)"}
 
     esz = 4 if args.precision == "float32" else 8

@@ -1122,8 +1122,13 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_env_rollout(const DevCfg
   __shared__ qd::HoSlot<T> ho[Q == 1 && !RP ? BLOCK : 1];
   const int64_t n = s.n, ow = (int64_t)cfgp->n_obs * cfgp->obs_len;
   for (int k = 0; k < n_steps; k++) {
+    // the aircraft index re-materialised per step: otherwise the backend hoists the ~70 per-lane 64-bit
+    // row addresses of the step (every SoA row at i) out of the step loop, where they stay live across
+    // the RK loop and spill (292 VGPRs, profiles/r03_isa_resources.txt); recomputed they cost an add each
+    int64_t ik = i;
+    asm volatile("" : "+v"(ik));
     const C& c = *reinterpret_cast<const C*>(cfgp);
-    env_step_call<T, C, RP, Q>(c, s, i, lds, actions + k * n * 3, obs_out + k * n * ow, rew_out + k * n, done_out + k * n,
+    env_step_call<T, C, RP, Q>(c, s, ik, lds, actions + k * n * 3, obs_out + k * n * ow, rew_out + k * n, done_out + k * n,
                   term_out ? term_out + k * n : nullptr, tobs_out ? tobs_out + k * n * ow : nullptr,
                   episode_out ? episode_out + k * n * 5 : nullptr, stats ? stats + k * n : nullptr, auto_reset, qr, ho);
   }
