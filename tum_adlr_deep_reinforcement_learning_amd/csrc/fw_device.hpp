@@ -280,8 +280,11 @@ FW_HD float fpow(float a, float p) {  // a > 0
 FW_HD double fatan2(double y, double x) { return atan2(y, x); }
 FW_HD float fatan2(float y, float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  // |x|, |y| stay source modifiers of the max / min / compare (no separate abs instructions)
-  const float mx = fmaxf(fabsf(x), fabsf(y)), mn = fminf(fabsf(x), fabsf(y));
+  // max / min of |x|, |y| as v_med3 against -+inf: the abs folds into source modifiers and, unlike
+  // fmaxf / fminf in IEEE mode, no canonicalising v_max per input is emitted
+  const float inf = __builtin_inff();
+  const float mx = __builtin_amdgcn_fmed3f(fabsf(x), fabsf(y), inf);
+  const float mn = __builtin_amdgcn_fmed3f(fabsf(x), fabsf(y), -inf);
   const float t = mn * __builtin_amdgcn_rcpf(mx);
   const float q = t * t;
   float p = 0.0029030926525592804f;
@@ -300,6 +303,48 @@ FW_HD float fatan2(float y, float x) {
   return copysignf(r, y);
 #else
   return atan2f(y, x);
+#endif
+}
+
+// Two atan2 at once (the one-lane RHS needs alpha and beta): the same function as fatan2, the
+// polynomial of both run as packed pairs (v_pk_fma_f32: one instruction per degree for the two).
+FW_HD void fatan2_2(double y0, double x0, double y1, double x1, double& r0, double& r1) {
+  r0 = atan2(y0, x0);
+  r1 = atan2(y1, x1);
+}
+FW_HD void fatan2_2(float y0, float x0, float y1, float x1, float& r0, float& r1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef float F2 __attribute__((ext_vector_type(2)));
+  const float inf = __builtin_inff();
+  const float mx0 = __builtin_amdgcn_fmed3f(fabsf(x0), fabsf(y0), inf);
+  const float mn0 = __builtin_amdgcn_fmed3f(fabsf(x0), fabsf(y0), -inf);
+  const float mx1 = __builtin_amdgcn_fmed3f(fabsf(x1), fabsf(y1), inf);
+  const float mn1 = __builtin_amdgcn_fmed3f(fabsf(x1), fabsf(y1), -inf);
+  F2 t;
+  t.x = mn0 * __builtin_amdgcn_rcpf(mx0);
+  t.y = mn1 * __builtin_amdgcn_rcpf(mx1);
+  const F2 q = t * t;
+  F2 p = q * 0.0029030926525592804f + -0.016281209886074066f;
+  p = p * q + 0.043036505579948425f;
+  p = p * q + -0.07533437758684158f;
+  p = p * q + 0.10654566437005997f;
+  p = p * q + -0.14207105338573456f;
+  p = p * q + 0.19993050396442413f;
+  p = p * q + -0.3333309292793274f;
+  p = p * q + 1.0f;
+  const F2 rr = t * p;
+  float a0 = rr.x, a1 = rr.y;
+  a0 = fabsf(y0) > fabsf(x0) ? 1.5707963267948966f - a0 : a0;
+  a1 = fabsf(y1) > fabsf(x1) ? 1.5707963267948966f - a1 : a1;
+  a0 = x0 < 0.0f ? 3.141592653589793f - a0 : a0;
+  a1 = x1 < 0.0f ? 3.141592653589793f - a1 : a1;
+  a0 = mx0 == 0.0f ? 0.0f : a0;
+  a1 = mx1 == 0.0f ? 0.0f : a1;
+  r0 = copysignf(a0, y0);
+  r1 = copysignf(a1, y1);
+#else
+  r0 = fatan2(y0, x0);
+  r1 = fatan2(y1, x1);
 #endif
 }
 
@@ -471,12 +516,8 @@ FW_HD int rhs(const C& c0, const A& a, const StepCtx<T>& X, bool first, const T*
   const T e0 = y[0], e1 = y[1], e2 = y[2], e3 = y[3];  // raw attitude (pyfly.py:1464)
 
   // ---- _forces (pyfly.py:1484-1643) ----
-  T p = om[0], q = om[1], r = om[2];
-  if (c.turbulence) {
-    p -= X.ta[0];
-    q -= X.ta[1];
-    r -= X.ta[2];
-  }
+  // angular turbulence (0 when the config has none: turbulence_at zeroes it, and x - 0 is x exactly)
+  const T p = om[0] - X.ta[0], q = om[1] - X.ta[1], r = om[2] - X.ta[2];
   T va[3];
   airspeed_vec(y, X.wind, X.tl, vel, va);
   // Va = |va|, alpha = atan2(w, u), beta = asin(v / Va) = atan2(v, sqrt(u^2 + w^2))
@@ -484,8 +525,8 @@ FW_HD int rhs(const C& c0, const A& a, const StepCtx<T>& X, bool first, const T*
   const T rxz2 = va[0] * va[0] + va[2] * va[2];
   const T rxz = fsqrt(rxz2);
   const T Va_raw = fsqrt(rxz2 + va[1] * va[1]);
-  T alpha = fatan2(va[2], va[0]);
-  T beta = fatan2(va[1], rxz);
+  T alpha, beta;
+  fatan2_2(va[2], va[0], va[1], rxz, alpha, beta);
   const T Va = cond(c, FW_V_VA, Va_raw, term);
   alpha = cond(c, FW_V_ALPHA, alpha, term);
   beta = cond(c, FW_V_BETA, beta, term);

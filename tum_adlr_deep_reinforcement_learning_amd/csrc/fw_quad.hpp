@@ -222,7 +222,7 @@ __device__ __forceinline__ int rhs_quad(const C& c, const A& a, const QCtx<T>& Q
   const T er1 = nx1(er), er2 = nx2(er);
 
   // ---- _forces (pyfly.py:1484-1643) ----
-  const T omt = c.turbulence ? om - Q.ta : om;
+  const T omt = om - Q.ta;  // angular turbulence (0 without turbulence: turbulence_at zeroes it)
   const T p = bc<0>(omt), q = bc<1>(omt), r = bc<2>(omt);
   // row r of wind_b = R(q) w + turb (_rot_b_v quaternion branch, pyfly.py:1780-1800; 1843)
   const T Rrr = T(-1) + T(2) * (e0 * e0 + er * er);
