@@ -280,7 +280,9 @@ int fw_destroy(fw_handle* h);
 int fw_num_envs(const fw_handle* h, int64_t* n);
 int fw_num_obs(const fw_handle* h, int32_t* n);
 
-/* Counter-based RNG key: env i of this handle draws from stream (seed, env_offset + i). */
+/* Counter-based RNG key: env i of this handle draws from stream (seed, env_offset + i).  Also restarts
+ * every env's episode counter, so a reset after fw_seed repeats the draws of the first reset after
+ * fw_create (gym's seed-then-reset reproducibility).  Synchronises the device; a setup call.        */
 int fw_seed(fw_handle* h, uint64_t seed, int64_t env_offset);
 
 /* Turbulence noise injection (parity mode, the turbulence_noise argument of

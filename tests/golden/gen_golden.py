@@ -898,6 +898,33 @@ def gen_curriculum():
             tgt.append([env.target["roll"], env.target["pitch"], env.target["Va"]])
         out["L%d__init" % li] = np.array(init)
         out["L%d__target" % li] = np.array(tgt)
+        if lvl in (0.25, 0.5):
+            # episodes from the reference's own sampled reset at this level (init state, target and steady
+            # wind drawn by reset()), then random actions: replayed on the device at the same level
+            rng = np.random.RandomState(300 + li)
+            env.seed(200 + li)
+            for ep in range(3):
+                obs0 = env.reset()
+                act_vals = [env.simulator.state[a].value for a in ("elevon_right", "elevon_left", "throttle")]
+                wind = np.asarray(env.simulator.wind.steady, dtype=np.float64).reshape(3)
+                init_row = np.array([env.simulator.state[k].value for k in ENV_STATE_KEYS] + act_vals + list(wind))
+                target0 = np.array([env.target["roll"], env.target["pitch"], env.target["Va"]])
+                obs, rew, done, acts = [obs0], [], [], []
+                for s in range(300):
+                    a = rng.uniform(-1.2, 1.2, size=3).astype(np.float32)
+                    o, r, dn, info = env.step(a)
+                    acts.append(np.asarray(a, dtype=np.float64))
+                    obs.append(o)
+                    rew.append(r)
+                    done.append(dn)
+                    if dn:
+                        break
+                pre = "L%d__ep%d__" % (li, ep)
+                for k, v in dict(init=init_row, target0=target0, obs=np.array(obs), rew=np.array(rew),
+                                 done=np.array(done), act=np.array(acts)).items():
+                    out[pre + k] = v
+                print("curriculum L%g ep%d: %d steps, init roll %.3f pitch %.3f u %.2f, wind %s" % (
+                    lvl, ep, len(rew), init_row[0], init_row[1], init_row[9], wind))
     out["levels"] = np.array(levels)
     out["props"] = np.array(props)
     np.savez_compressed(os.path.join(OUT, "env_curriculum.npz"), **out)

@@ -13,6 +13,10 @@
                       merged in rank order == the whole batch's statistics
   configs[2]          65536 aircraft x the 2048-step PPO horizon, graphed collect: GAE == oracle bit for
                       bit on a sampled subset of envs (reference: buffers.py:304-333)
+  curriculum          device reset draws at levels 0 / 0.25 / 0.5 / 0.75 inside the level's ranges and
+                      KS-matched to the reference's draws; the reference's episodes at levels 0.25 / 0.5
+                      (from its own sampled resets) replayed on the device in fp64 and fp32
+  facade seed         FixedWingAircraft.seed(None) draws a fresh seed (gym seeding semantics)
 """
 import socket
 
@@ -364,3 +368,104 @@ def test_env_step_teacher_forced(precision):
         # measured (round 3): 17 flips in 49152, 99.996 % within 1e-4, worst 7.5e-4 (a sideways flyer)
         assert flips <= 0.005 * total and tight_ok >= 0.999 * same and worst <= 2e-3
     eng.close()
+
+
+# ---------------------------------------------------------------------------- curriculum levels on the device
+def _curriculum_spec(lvl):
+    spec = C.EnvSpec(config_kw={"steps_max": 2000}, sim_config_kw={"turbulence": False})
+    spec.set_curriculum_level(lvl)
+    return spec
+
+
+@pytest.mark.parametrize("li", [0, 1, 2, 3])
+def test_curriculum_device_reset_draws(li):
+    """Resets the device samples at curriculum level 0 / 0.25 / 0.5 / 0.75 (set_curriculum_level,
+    fixed_wing.py:334-412; reset / sample_target, :414-481, 654-746): every draw inside the level's init
+    and target ranges, and (levels > 0) the roll / pitch / Va / velocity_u and target marginals match the
+    reference's 300 draws at the same level (env_curriculum.npz; two-sample KS, p > 1e-3).  The draws
+    themselves differ: Philox replaces gym's np_random."""
+    import _fixtures as F
+    from scipy import stats
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
+    d = F.load("env_curriculum.npz")
+    lvl = float(d["levels"][li])
+    spec = _curriculum_spec(lvl)
+    n = 8192
+    eng = Engine(spec.sim, spec, n, device=DEV, precision="float64")
+    eng.seed(31 + li)
+    eng.reset()
+    der = eng.get_block(C.FW_BLK_DERIVED).cpu().numpy()
+    y = eng.get_block(C.FW_BLK_ODE).cpu().numpy()
+    tgt = eng.get_block(C.FW_BLK_TARGET).cpu().numpy()
+    eng.close()
+    dev = np.stack([der[0], der[1], der[3], y[10]], axis=1)  # roll pitch Va u: the fixture's columns
+    for k, name in ((0, "roll"), (1, "pitch"), (3, "velocity_u")):
+        v = spec.sim.vars[name]
+        assert np.all(dev[:, k] >= v.init_min - 1e-9) and np.all(dev[:, k] <= v.init_max + 1e-9), (name, lvl)
+    for k, (lo, hi, delta) in enumerate(spec.target_sampling()):
+        cur = dev[:, k if k < 2 else 2]
+        low = np.maximum(lo, cur - delta) if delta is not None else np.full_like(cur, lo)
+        high = np.maximum(np.minimum(hi, cur + delta), low) if delta is not None else np.full_like(cur, hi)
+        assert np.all(tgt[k] >= low - 1e-9) and np.all(tgt[k] <= high + 1e-9), (k, lvl)
+    ref_init, ref_tgt = d["L%d__init" % li], d["L%d__target" % li]
+    if lvl == 0.0:  # collapsed ranges: every draw is the midpoint, as the reference's
+        for k in (0, 1, 3):
+            np.testing.assert_allclose(dev[:, k], ref_init[0, k], rtol=0, atol=1e-9)
+        return
+    for k in range(4):
+        assert stats.ks_2samp(dev[:, k], ref_init[:, k]).pvalue > 1e-3, ("init", k, lvl)
+    for k in range(3):
+        assert stats.ks_2samp(tgt[k], ref_tgt[:, k]).pvalue > 1e-3, ("target", k, lvl)
+
+
+@pytest.mark.parametrize("precision", ["float64", "float32"])
+@pytest.mark.parametrize("li", [1, 2])
+def test_curriculum_reference_episodes_replayed(li, precision):
+    """The reference's episodes at curriculum level 0.25 / 0.5, each from the reference's own sampled reset
+    (state, target and steady wind drawn by reset() at that level) under random actions, flown on the
+    device configured at the same level: fp64 obs / rewards within 1e-6 + 1e-6 per step, fp32 within
+    2e-3 (1 + |ref|) over the first 100 steps (the tolerances of the parameter-randomisation replay)."""
+    import _fixtures as F
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
+    d = F.load("env_curriculum.npz")
+    spec = _curriculum_spec(float(d["levels"][li]))
+    g = lambda ep, k: d["L%d__ep%d__%s" % (li, ep, k)]  # noqa: E731
+    eps = 3
+    eng = Engine(spec.sim, spec, eps, device=DEV, precision=precision)
+    init = np.stack([F.env_init(g(ep, "init")) for ep in range(eps)], axis=1)
+    obs0 = eng.reset(init=init, target=np.stack([g(ep, "target0") for ep in range(eps)], axis=1))
+    for ep in range(eps):
+        np.testing.assert_allclose(obs0[ep].double().cpu().numpy(), g(ep, "obs")[0], rtol=1e-5, atol=1e-5)
+    steps = max(len(g(ep, "rew")) for ep in range(eps)) if precision == "float64" else 100
+    for s in range(steps):
+        a = np.stack([g(ep, "act")[min(s, len(g(ep, "act")) - 1)] for ep in range(eps)])
+        o, r, dn, _ = eng.env_step(torch.tensor(a, dtype=eng.dtype, device=DEV), auto_reset=False)
+        o, r, dn = o.double().cpu().numpy(), r.double().cpu().numpy(), dn.cpu().numpy()
+        for ep in range(eps):
+            if s >= len(g(ep, "rew")):
+                continue
+            ref_o = eng.terminal_obs[ep].double().cpu().numpy() if dn[ep] else o[ep]
+            want_o, want_r = g(ep, "obs")[s + 1], g(ep, "rew")[s]
+            if precision == "float64":
+                tol = 1e-6 + 1e-6 * s
+                assert abs(r[ep] - want_r) <= tol, (ep, s)
+                np.testing.assert_allclose(ref_o, want_o, rtol=1e-5, atol=tol)
+            else:
+                assert abs(r[ep] - want_r) <= 2e-3 * (1 + abs(want_r)), (ep, s)
+                assert np.all(np.abs(ref_o - want_o) <= 2e-3 * (1 + np.abs(want_o))), (ep, s)
+            assert bool(dn[ep]) == bool(g(ep, "done")[s]), (ep, s)
+    eng.close()
+
+
+def test_facade_seed_none_draws_a_seed():
+    """FixedWingAircraft.seed(None) draws a fresh seed and returns it (gym seeding.np_random(None),
+    fixed_wing.py:324-332); an explicit seed is returned as given and reproduces the sampled reset."""
+    from tum_adlr_deep_reinforcement_learning_amd.fixed_wing import FixedWingAircraft
+    env = FixedWingAircraft(config_kw={"steps_max": 60}, sim_config_kw={"turbulence": False}, device=DEV)
+    a, b = env.seed(None)[0], env.seed()[0]
+    assert a != b and 0 <= a < 2 ** 64
+    assert env.seed(5) == [5]
+    o1 = env.reset()
+    env.seed(5)
+    np.testing.assert_array_equal(env.reset(), o1)
+    env.close()

@@ -1702,6 +1702,12 @@ int fw_seed(fw_handle* h, uint64_t seed, int64_t env_offset) {
   if (!h) return set_err(FW_E_INVALID, "NULL handle");
   h->seed = seed;
   h->env_offset = env_offset;
+  // a re-seed restarts every env's stream: the episode counters (the Philox counter's episode word)
+  // go back to 0, so the next reset draws what the first reset after fw_create drew
+  FW_HIP(hipSetDevice(h->device));
+  FW_HIP(hipDeviceSynchronize());
+  FW_HIP(hipMemset((char*)h->base + h->o_episode, 0, align_up((size_t)h->ld * 4, 256)));
+  FW_HIP(hipDeviceSynchronize());
   return FW_OK;
 }
 

@@ -6,6 +6,8 @@ One aircraft on the GPU, stepped with ``auto_reset=False`` so ``step`` after
 like fixed_wing.py:519-628, plus the episode metrics of ``cfg["metrics"]``
 (fixed_wing.py:1644-1736) on done.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -45,8 +47,11 @@ class FixedWingAircraft:
         return t, d[[0, 1, 3]]
 
     def seed(self, seed=None):
-        """FixedWingAircraft.seed (fixed_wing.py:324-332) -> Philox stream (seed, 0)."""
-        s = 0 if seed is None else int(seed)
+        """FixedWingAircraft.seed (fixed_wing.py:324-332) -> Philox stream (seed, 0).
+
+        ``None`` draws a fresh seed from the OS entropy pool and returns it, as gym's
+        ``seeding.np_random(None)`` does (8 bytes; the reference's stream itself is replaced by Philox)."""
+        s = int.from_bytes(os.urandom(8), "little") if seed is None else int(seed)
         self.engine.seed(s)
         return [s]
 
