@@ -11,9 +11,9 @@ done
 wait
 echo "# gfx950 resource usage per kernel instance (hipcc -Rpass-analysis=kernel-resource-usage, $(date -u +%F))"
 echo "# vgpr/agpr: registers per lane (vgpr+agpr > 256 uses the AGPR half; 512 = one wave per SIMD);"
-echo "# scratch: bytes per lane; vspill/sspill: spilled VGPRs / SGPRs"
+echo "# scratch: bytes per lane (a kernel that calls env_step_noinl includes the call frame); vspill/sspill: spilled VGPRs / SGPRs"
 cat "$W"/p*.txt | grep remark | sed -e 's/.*remark: *//; s/ \[-Rpass.*//' | \
   awk '/Function Name/{n=$3; sub(/_ZN12_GLOBAL__N_1[0-9]+/,"",n); sub(/EEvPK.*/,"",n)} /^VGPRs:/{v=$2} /^AGPRs/{a=$2}
        /ScratchSize/{s=$3} /^VGPRs Spill/{vs=$3} /^SGPRs Spill/{ss=$3} /^Occupancy/{o=$3}
-       /LDS Size/{if (n ~ /^k_/) printf "%-58s vgpr %4s agpr %4s scratch %5s vspill %4s sspill %4s occ %s\n", n, v, a, s, vs, ss, o}' | sort -u
+       /LDS Size/{if (n ~ /^k_/ || n ~ /noinl/) printf "%-58s vgpr %4s agpr %4s scratch %5s vspill %4s sspill %4s occ %s\n", n, v, a, s, vs, ss, o}' | sort -u
 rm -rf "$W"

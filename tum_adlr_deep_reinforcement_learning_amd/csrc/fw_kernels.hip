@@ -69,6 +69,11 @@ constexpr int BLOCK = FW_BLOCK;
 #define FW_QUAD_MIN_WAVES 1  // ... of their quad (Q = 4) instances
 #endif
 #define FW_WAVES(Q) ((Q) == 4 ? FW_QUAD_MIN_WAVES : FW_MIN_WAVES)
+#ifndef FW_PREF_Q4_F64
+// 1: the fp64 quad instances prefetch the epilogue's loads like the fp32 ones.  In fp64 the prefetched
+// rows spill (339 VGPRs): 8192 aircraft 0.137 -> 0.099 ms per step without it (profiles/r03_ab_pref64.log)
+#define FW_PREF_Q4_F64 0
+#endif
 #ifndef FW_PREF_Q1
 #define FW_PREF_Q1 0  // 1: the one-lane k_env_step instances prefetch the epilogue's loads too (A/B)
 #endif
@@ -1076,28 +1081,48 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_env_step(const DevCfg<T>
   __shared__ V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];  // y, f (+ error sum) of the block's aircraft (pairs)
   static_assert(Q != 1 || RP || FW_TAIL_QUAD == 0 || BLOCK == 64, "the tail handoff works per one-wave block");
   __shared__ qd::HoSlot<T> ho[Q == 1 && !RP ? BLOCK : 1];
-  env_step_lane<T, C, RP, Q, (Q == 4 || FW_PREF_Q1)>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out,
+  env_step_lane<T, C, RP, Q, ((Q == 4 && (sizeof(T) == 4 || FW_PREF_Q4_F64)) || FW_PREF_Q1)>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out,
                                                   episode_out, stats, auto_reset, (int)(tid % Q), ho);
 }
 
-// One env step of k_env_rollout.  Inlined (default), the step loop's kernel spills ~230 VGPRs
-// (values live across the RK loop into the epilogue); behind a call boundary it does not, but the call
-// costs more than the spills (tools/ab_bench.sh, profiles/r02_ab_rollout.log).
+// One env step of k_env_rollout.  fp32: inlined, and scratch-free since the step loop re-materialises
+// the aircraft index (below); behind a call boundary it ran 5 % slower (profiles/r02_ab_rollout.log).
+// fp64: inlined, the step loop spills 660-810 VGPRs (the fp64 live state does not fit 512); behind a call
+// boundary the step runs 1.39x faster (65536 aircraft, 1.86e8 -> 2.58e8 env-steps/s,
+// profiles/r03_ab_rollout64.log), so FW_ROLLOUT_CALL64 = 1 ships.
 #ifndef FW_ROLLOUT_CALL
-#define FW_ROLLOUT_CALL 0  // 1: the step behind a call (no spills, but measured 5% slower: profiles/r02_ab_rollout.log)
+#define FW_ROLLOUT_CALL 0  // 1: every instance's step behind a call
 #endif
-#if FW_ROLLOUT_CALL
-#define FW_ROLLOUT_INLINE __noinline__
-#else
-#define FW_ROLLOUT_INLINE __forceinline__
+#ifndef FW_ROLLOUT_CALL64
+#define FW_ROLLOUT_CALL64 1
 #endif
 template <typename T, typename C, bool RP, int Q>
-__device__ FW_ROLLOUT_INLINE void env_step_call(const C& c, const State<T>& s, const int64_t i, V2<T>* lds,
-                                           const T* actions, T* obs_out, T* rew_out, uint8_t* done_out,
-                                           int32_t* term_out, T* tobs_out, T* episode_out, int32_t* stats,
-                                           int auto_reset, int qr, void* ho) {
+__device__ __forceinline__ void env_step_inl(const C& c, const State<T>& s, const int64_t i, V2<T>* lds,
+                                             const T* actions, T* obs_out, T* rew_out, uint8_t* done_out,
+                                             int32_t* term_out, T* tobs_out, T* episode_out, int32_t* stats,
+                                             int auto_reset, int qr, void* ho) {
   env_step_lane<T, C, RP, Q, false>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out,
-                                    stats, auto_reset, qr, ho);  // no prefetch: this kernel spills already
+                                    stats, auto_reset, qr, ho);  // no prefetch: the open loop needs no overlap
+}
+template <typename T, typename C, bool RP, int Q>
+__device__ __noinline__ void env_step_noinl(const C& c, const State<T>& s, const int64_t i, V2<T>* lds,
+                                            const T* actions, T* obs_out, T* rew_out, uint8_t* done_out,
+                                            int32_t* term_out, T* tobs_out, T* episode_out, int32_t* stats,
+                                            int auto_reset, int qr, void* ho) {
+  env_step_inl<T, C, RP, Q>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out, stats,
+                            auto_reset, qr, ho);
+}
+template <typename T, typename C, bool RP, int Q>
+__device__ __forceinline__ void env_step_call(const C& c, const State<T>& s, const int64_t i, V2<T>* lds,
+                                              const T* actions, T* obs_out, T* rew_out, uint8_t* done_out,
+                                              int32_t* term_out, T* tobs_out, T* episode_out, int32_t* stats,
+                                              int auto_reset, int qr, void* ho) {
+  if constexpr (FW_ROLLOUT_CALL || (FW_ROLLOUT_CALL64 && sizeof(T) == 8))
+    env_step_noinl<T, C, RP, Q>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out,
+                                stats, auto_reset, qr, ho);
+  else
+    env_step_inl<T, C, RP, Q>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out, stats,
+                              auto_reset, qr, ho);
 }
 
 // Open-loop rollout: n_steps consecutive FixedWingAircraft.step calls per aircraft in ONE launch, actions

@@ -43,6 +43,24 @@ __device__ __forceinline__ double perm(double x) {
   const unsigned hi = (unsigned)perm_i<A, B, C, D>((int)(unsigned)(v >> 32));
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+// row K of every quad (lane & 3 == K) takes x_row, the others x_other: one v_cndmask against a
+// constant lane mask.  The compiler turns `r == K ? a + b : c` with work in an arm into an exec-masked
+// branch (saveexec / xor / andn2 / or, both arms issued) -- the lone-wave tail pays every instruction.
+template <int K>
+__device__ __forceinline__ float rowsel(float x_row, float x_other) {
+  float out;
+  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(out) : "v"(x_other), "v"(x_row), "s"(0x1111111111111111ull << K));
+  return out;
+}
+template <int K>
+__device__ __forceinline__ double rowsel(double x_row, double x_other) {
+  const unsigned long long a = (unsigned long long)__double_as_longlong(x_row);
+  const unsigned long long b = (unsigned long long)__double_as_longlong(x_other);
+  const float lo = rowsel<K>(__int_as_float((int)(unsigned)a), __int_as_float((int)(unsigned)b));
+  const float hi = rowsel<K>(__int_as_float((int)(unsigned)(a >> 32)), __int_as_float((int)(unsigned)(b >> 32)));
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)__float_as_int(hi) << 32) |
+                                          (unsigned)__float_as_int(lo)));
+}
 // lane K's value on all four lanes
 template <int K, typename T>
 __device__ __forceinline__ T bc(T x) {
@@ -309,7 +327,7 @@ __device__ __forceinline__ int rhs_quad(const C& c, const A& a, const QCtx<T>& Q
   // U = cb (-D) + sb Y, then rows (ca U + sa L, sb D + cb Y, sa U - ca L)
   const T U = cb * (-fdrag) + sb * fy;
   const T fa02 = (r0 ? ca : sa) * U + (r0 ? sa : -ca) * flift;
-  const T fa = r1 ? sb * fdrag + cb * fy : fa02;
+  const T fa = rowsel<1>(sb * fdrag + cb * fy, fa02);
   // gravity: column 2 of R(q) (the diagonal term in the raw-quaternion form of pyfly.py:1493-1499)
   const T Dr = er * er + e0 * e0 - er1 * er1 - er2 * er2;
   const T fg = a.mg * (r0 ? Rr2 : (r1 ? Rr1 : Dr));
