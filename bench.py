@@ -526,10 +526,18 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_procs)
         _log("cpu baseline done")
+    # FW_BENCH_ONE_DEVICE=1 / FW_BENCH_BACKEND=gloo: rehearsal of the N > 1 code path with every rank on
+    # cuda:0 (RCCL refuses two ranks on one GPU); never used for a reported line
+    if os.environ.get("FW_BENCH_ONE_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("FW_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     # pyfly_config.json defaults: random steady wind |w| <= 8 m/s; Dryden only with --turbulence
     spec = C.EnvSpec(sim_config_kw={"turbulence": bool(args.turbulence), "turbulence_intensity": "light"})
