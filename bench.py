@@ -439,10 +439,13 @@ def window_replay(n, args, spec, dev, rank, env_offset, precision, plan, obs_aft
     return out
 
 
-def open_loop_leg(n, args, spec, dev, rank, world, env_offset, K=256, launches=4):
+def open_loop_leg(n, args, spec, dev, rank, world, env_offset, K=256, launches=16):
     """The same workload through the open-loop rollout kernel (fw_env_rollout: K steps per launch,
     actions pre-generated): the rate of a SAC / TD3 warm-up fill or a scripted-command evaluation, where
-    the actions do not depend on the observations.  Steady state as above (prep steps first)."""
+    the actions do not depend on the observations.  Steady state as above (prep steps first).  A launch
+    lasts as long as its slowest wave's K steps, so one aircraft needing thousands of RHS evaluations adds
+    milliseconds to its launch: 16 launches (4096 steps) instead of round 2's 4, whose rate moved by
+    0.98e9 .. 1.26e9 with the population (profiles/r03_open_loop_probe.log)."""
     eng = Engine(spec.sim, spec, n, device=dev, precision=args.precision)
     eng.seed(1234, env_offset=env_offset)
     eng.reset()
