@@ -20,6 +20,9 @@
  *   fw_replay_add     ReplayBuffer.add   stable_baselines3/common/buffers.py:222-235
  *   fw_rollout_store  RolloutBuffer.add  stable_baselines3/common/buffers.py:335-361, with the row
  *                     index on the device so a captured collect step stores its own row
+ *   fw_policy_forward ActorCriticPolicy.forward of the default PPO MlpPolicy
+ *                     stable_baselines3/common/policies.py:539-553 (+ the action clip of
+ *                     on_policy_algorithm.py:158-161), one launch per collect step
  */
 #ifndef FWROLLOUT_H
 #define FWROLLOUT_H
@@ -97,6 +100,24 @@ typedef struct fw_row_seg {
   int32_t pad;
 } fw_row_seg;
 int fw_rollout_store(const fw_row_seg* segs, int32_t n_segs, int32_t* ctrl_dev, int32_t advance, void* stream);
+
+/* The default PPO MlpPolicy's forward for one collect step (SB3 ActorCriticPolicy.forward,
+ * stable_baselines3/common/policies.py:539-553, DiagGaussianDistribution distributions.py:143-171):
+ * two tanh MLPs [d -> hidden -> hidden] (actor, critic; nn.Linear weights [out][in], row-major),
+ * mean = act_w h + act_b, value = val_w h + val_b, action = mean + exp(log_std) * noise (noise [n][A],
+ * NULL = deterministic), log_prob = sum_a (-(action-mean)^2 / (2 std^2) - log_std - log(2 pi)/2),
+ * clipped = min(max(action, low), high) (on_policy_algorithm.py:158-161; clipped may be NULL).
+ * Parameters are read in place (device pointers), so an optimiser step is seen by the next launch.
+ * Limits: d <= 32, hidden == 64 (SB3's default net_arch [64, 64]), act_dim <= 8.  fp32 FMA arithmetic: equal to the torch module's
+ * forward within ~1e-6, not bit for bit (a different summation order than the BLAS GEMMs). */
+typedef struct fw_mlp_policy {
+  const float *pi_w0, *pi_b0, *pi_w1, *pi_b1, *act_w, *act_b;
+  const float *vf_w0, *vf_b0, *vf_w1, *vf_b1, *val_w, *val_b;
+  const float* log_std;
+  int32_t d, hidden, act_dim, pad;
+} fw_mlp_policy;
+int fw_policy_forward(const fw_mlp_policy* p, const float* obs, int64_t n, const float* noise, const float* low,
+                      const float* high, float* actions, float* clipped, float* values, float* log_probs, void* stream);
 
 #ifdef __cplusplus
 }

@@ -379,9 +379,12 @@ def test_graphed_collect_equals_eager():
     from tum_adlr_deep_reinforcement_learning_amd.vec_env import FixedWingVecEnv
     from tum_adlr_deep_reinforcement_learning_amd.vec_normalize import VecNormalize
 
-    class Det(MlpActorCritic):
+    class Det(MlpActorCritic):  # its own forward: the torch modules run the policy
         def forward(self, obs, deterministic=True):
             return super().forward(obs, deterministic=True)
+
+    class DetFused(MlpActorCritic):  # the fused fw_policy_forward launch runs the policy
+        deterministic_rollout = True
 
     n, T = 4096, 48
 
@@ -395,20 +398,22 @@ def test_graphed_collect_equals_eager():
                             n_envs=n)
         return venv, env, buf, RolloutCollector(env, policy, buf)
 
-    va, ea, ba, ca = make(Det)
-    vb, eb, bb, cb = make(Det)
-    ca.collect(8)
-    cb.collect(8)
-    for _ in range(2):
-        ca.collect()
-        cb.collect(graph=True)
-        for f in ("slab", "rewards", "dones"):
-            assert torch.equal(getattr(ba, f), getattr(bb, f)), f
-        assert torch.equal(ca.last_obs, cb.last_obs) and torch.equal(ca.last_dones, cb.last_dones)
-        assert torch.equal(ea.rms, eb.rms) and torch.equal(ea.ret, eb.ret)
-    assert bb.dones.sum() > 0  # auto-resets inside the horizon
-    va.close()
-    vb.close()
+    for cls in (Det, DetFused):
+        va, ea, ba, ca = make(cls)
+        vb, eb, bb, cb = make(cls)
+        assert ca._fused(ba.observations[0]) == (cls is DetFused)
+        ca.collect(8)
+        cb.collect(8)
+        for _ in range(2):
+            ca.collect()
+            cb.collect(graph=True)
+            for f in ("slab", "rewards", "dones"):
+                assert torch.equal(getattr(ba, f), getattr(bb, f)), (cls.__name__, f)
+            assert torch.equal(ca.last_obs, cb.last_obs) and torch.equal(ca.last_dones, cb.last_dones)
+            assert torch.equal(ea.rms, eb.rms) and torch.equal(ea.ret, eb.ret)
+        assert bb.dones.sum() > 0  # auto-resets inside the horizon
+        va.close()
+        vb.close()
 
     vs, es, bs, cs = make(MlpActorCritic)
     cs.collect(8)

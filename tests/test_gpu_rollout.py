@@ -10,6 +10,8 @@
   RolloutCollector  end to end on the real env: stored advantages == oracle GAE of the stored
                     rollout, bit for bit
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -139,3 +141,67 @@ def test_rollout_collector_end_to_end():
     flat = g.flatten()
     assert np.array_equal(flat[4].cpu().numpy().ravel(), R.swap_and_flatten(buf.advantages.cpu().numpy()).ravel())
     venv.close()
+
+
+@pytest.mark.parametrize("d", [7, 16, 32])
+def test_fused_policy_forward_vs_torch_module(d):
+    """fw_policy_forward (MlpActorCritic.collect_step: both MLPs, Gaussian sample, log-prob and clip in one
+    launch) == the torch module's forward + torch.max(torch.min(...)) on the same noise draws: fp32,
+    rel/abs 2e-5 (a different FMA order than the BLAS GEMMs; the fast tanh adds ~1e-7 absolute).  Ragged n
+    (not a multiple of the 128-env block), random (trained-like) weights, wide inputs."""
+    from tum_adlr_deep_reinforcement_learning_amd.rollout import MlpActorCritic
+    torch.manual_seed(3)
+    n, A = 5000 + d, 3
+    pol = MlpActorCritic(d, A).to(DEV)
+    with torch.no_grad():
+        for prm in pol.parameters():
+            prm.add_(0.3 * torch.randn_like(prm))
+    obs = 3 * torch.randn(n, d, device=DEV)
+    low = torch.tensor([-0.5, -1.0, 0.0], device=DEV)
+    high = torch.tensor([0.5, 1.0, 1.0], device=DEV)
+    assert pol.fused_ok(obs)
+    torch.manual_seed(11)
+    with torch.no_grad():
+        a_ref, v_ref, lp_ref = pol(obs)
+    torch.manual_seed(11)
+    a, c, v, lp = pol.collect_step(obs, low, high)
+    tol = dict(rtol=2e-5, atol=2e-5)
+    torch.testing.assert_close(a, a_ref, **tol)
+    torch.testing.assert_close(v, v_ref.reshape(-1), **tol)
+    torch.testing.assert_close(lp, lp_ref, **tol)
+    torch.testing.assert_close(c, torch.max(torch.min(a, high), low), rtol=0, atol=0)
+    pol.deterministic_rollout = True
+    a2, _, v2, lp2 = pol.collect_step(obs, low, high)
+    with torch.no_grad():
+        m_ref, _, _ = pol(obs, deterministic=True)
+    torch.testing.assert_close(a2, m_ref, **tol)
+    assert torch.equal(v2, v)  # the critic does not depend on the noise
+
+
+@pytest.mark.parametrize("n", [1, 255, 256, 70001])
+def test_moments_kernel_vs_numpy(n):
+    """fw_moments (block two-pass records + two-pass record merge) vs numpy's np.mean / np.var in fp64:
+    rel 1e-12, including a constant column (var exactly 0) and a column with a large offset."""
+    from tum_adlr_deep_reinforcement_learning_amd import _native
+    lib = _native.load()
+    d = 5
+    g = torch.Generator(device=DEV)
+    g.manual_seed(n)
+    x = torch.randn(n, d, generator=g, device=DEV)
+    x[:, 2] = 0.25
+    x[:, 3] = 1000.0 + x[:, 3]
+    rew = torch.randn(n, generator=g, device=DEV)
+    ret = torch.randn(n, generator=g, device=DEV, dtype=torch.float64)
+    ret0 = ret.clone()
+    ws = torch.empty(int(lib.fw_moments_workspace_bytes(n, d)), dtype=torch.uint8, device=DEV)
+    out = torch.empty(1 + 2 * (d + 1), dtype=torch.float64, device=DEV)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    _native.check(lib.fw_moments(P(x), n, d, d, P(rew), P(ret), 0.99, P(ws), P(out), None), "fw_moments")
+    torch.cuda.synchronize()
+    xs = np.concatenate([x.cpu().double().numpy(), (ret0.cpu().numpy() * 0.99 + rew.cpu().double().numpy())[:, None]], 1)
+    np.testing.assert_array_equal(ret.cpu().numpy(), xs[:, -1])
+    o = out.cpu().numpy()
+    assert o[0] == n
+    np.testing.assert_allclose(o[1:d + 2], xs.mean(0), rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(o[d + 2:] / n, xs.var(0), rtol=1e-12, atol=1e-13)
+    assert o[d + 2 + 2] == 0.0

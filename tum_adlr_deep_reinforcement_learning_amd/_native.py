@@ -144,6 +144,7 @@ SIGNATURES = {
                                     _c.c_double, _vp, _vp, _vp, _vp]),
     "fw_replay_add": (_c.c_int, [_vp, _i32, _vp]),
     "fw_rollout_store": (_c.c_int, [_vp, _i32, _vp, _i32, _vp]),
+    "fw_policy_forward": (_c.c_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
 }
 
 
@@ -153,6 +154,12 @@ class FwCopySeg(ctypes.Structure):  # include/fwrollout.h fw_copy_seg
 
 class FwRowSeg(ctypes.Structure):  # include/fwrollout.h fw_row_seg
     _fields_ = [("src", _vp), ("dst", _vp), ("bytes", _i64), ("stride", _i64), ("row_off", _i32), ("pad", _i32)]
+
+
+class FwMlpPolicy(ctypes.Structure):  # include/fwrollout.h fw_mlp_policy
+    _fields_ = [(k, _vp) for k in ("pi_w0", "pi_b0", "pi_w1", "pi_b1", "act_w", "act_b", "vf_w0", "vf_b0", "vf_w1",
+                                   "vf_b1", "val_w", "val_b", "log_std")] + \
+               [("d", _i32), ("hidden", _i32), ("act_dim", _i32), ("pad", _i32)]
 
 
 def load(path=None):

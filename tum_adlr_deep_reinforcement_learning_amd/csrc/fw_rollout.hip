@@ -7,7 +7,8 @@
 //                      prefetched GAE_PF steps ahead (the recurrence is serial, the loads
 //                      are not).  HBM-bound: 4+4+1 B read, 4+4 B written per (step, env).
 //   k_moments_partial  RunningMeanStd.update's batch mean/var (running_mean_std.py:20-24):
-//   k_moments_merge    per-lane Welford, Chan merges in a fixed tree -> deterministic.
+//   k_moments_merge    per-block two-pass records, then a two-pass merge of the records, every
+//                      sum in a fixed order -> deterministic.
 //   k_rms_update       update_from_moments (running_mean_std.py:26-40) over rank-ordered
 //                      moment records (the RCCL all-gather of a sharded batch).
 //   k_vecnorm_apply    VecNormalize.normalize_obs / normalize_reward + ret[news] = 0
@@ -35,7 +36,6 @@ namespace {
 constexpr int BLOCK = 256;
 constexpr int GAE_PF = 16;   // time steps loaded ahead per lane
 constexpr int MAXD = 33;     // observation dims (FW_MAX_OBS) + the return column
-constexpr int MAX_PARTS = 1024;
 
 #define FW_HIP(expr)                                                                                     \
   do {                                                                                                   \
@@ -123,83 +123,113 @@ __device__ __forceinline__ Mom chan(Mom a, Mom b) {  // parallel-variance merge,
   return r;
 }
 
-// LDS tree over BLOCK records; returns the merged record on thread 0.
-__device__ Mom block_merge(Mom m, double* sn, double* sm, double* sq) {
-  const int tid = threadIdx.x;
-  sn[tid] = m.n;
-  sm[tid] = m.mean;
-  sq[tid] = m.m2;
-  __syncthreads();
-  for (int s = BLOCK / 2; s > 0; s >>= 1) {
-    if (tid < s) {
-      const Mom r = chan(Mom{sn[tid], sm[tid], sq[tid]}, Mom{sn[tid + s], sm[tid + s], sq[tid + s]});
-      sn[tid] = r.n;
-      sm[tid] = r.mean;
-      sq[tid] = r.m2;
-    }
-    __syncthreads();
-  }
-  const Mom out{sn[0], sm[0], sq[0]};
-  __syncthreads();
-  return out;
+// Batch moments in two kernels, both exact two-pass (numpy's np.mean then np.var of the deviations):
+//   k_moments_partial  one block per MROWS rows: the rows staged column-major in LDS, the block's mean
+//                      (column sum / rows) then its M2 = sum (x - mean)^2 from LDS -> record (n_b, mean_b, M2_b)
+//   k_moments_merge    the records of the whole batch: mean = sum n_b mean_b / N, then
+//                      M2 = sum (M2_b + n_b (mean_b - mean)^2) -- sums only, no per-record division
+// Every sum runs in a fixed order (strided lane partials, then a butterfly), so results are deterministic.
+// Round 2's per-thread Welford + Chan LDS tree (a division per element, 8 barriers per column) took
+// 44 + 35 us per call at 65536 x 16 (profiles/r03_collect_kernels.csv); this is memory-bound.
+constexpr int MROWS = BLOCK;  // rows per moment record
+constexpr int MGRP = 8;       // threads per column in k_moments_partial
+
+__device__ __forceinline__ double grp_sum8(double s) {  // sum over an aligned group of 8 lanes, same bits on all
+  s += __shfl_xor(s, 1);
+  s += __shfl_xor(s, 2);
+  s += __shfl_xor(s, 4);
+  return s;
+}
+__device__ __forceinline__ double wave_sum(double s) {  // butterfly over the 64 lanes, same bits on all
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) s += __shfl_xor(s, m);
+  return s;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_moments_partial(const float* __restrict__ x, int64_t n, int d, int64_t ldx,
                                                            const float* __restrict__ rew, double* __restrict__ retv,
-                                                           double gamma, int64_t rows_per, double* __restrict__ part) {
-  __shared__ double sn[BLOCK], sm[BLOCK], sq[BLOCK];
+                                                           double gamma, double* __restrict__ part) {
+  __shared__ float sx[MAXD - 1][MROWS + 8];  // the block's rows, column-major (fp32: exact); +8: the columns a
+                                             // wave reads at once start 8 banks apart
+  __shared__ double sr[MROWS];           // the updated discounted return column
+  __shared__ double smean[MAXD];
   const int D = d + (rew ? 1 : 0);
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per;
-  const int64_t r1 = std::min(n, r0 + rows_per);
-  double cnt = 0.0, mean[MAXD], m2[MAXD];
-#pragma unroll
-  for (int j = 0; j < MAXD; j++) mean[j] = m2[j] = 0.0;
-  for (int64_t r = r0 + threadIdx.x; r < r1; r += BLOCK) {
-    cnt += 1.0;
-#pragma unroll
-    for (int j = 0; j < MAXD; j++) {
-      if (j < D) {
-        double xv;
-        if (j < d) {
-          xv = (double)x[r * ldx + j];
-        } else {  // VecNormalize._update_reward: ret = ret * gamma + reward  (vec_normalize.py:126-129)
-          xv = retv[r] * gamma + (double)rew[r];
-          retv[r] = xv;
-        }
-        const double delta = xv - mean[j];
-        mean[j] += delta / cnt;
-        m2[j] += delta * (xv - mean[j]);
+  const int64_t r0 = (int64_t)blockIdx.x * MROWS;
+  const int nb = (int)std::min<int64_t>(MROWS, n - r0);
+  if (d > 0) {
+    if (ldx == d) {  // contiguous chunk: flat coalesced reads
+      const float* src = x + r0 * d;
+      for (int f = threadIdx.x; f < nb * d; f += BLOCK) {
+        const int r = f / d;
+        sx[f - r * d][r] = src[f];
+      }
+    } else {
+      for (int f = threadIdx.x; f < nb * d; f += BLOCK) {
+        const int r = f / d, j = f - r * d;
+        sx[j][r] = x[(r0 + r) * ldx + j];
       }
     }
   }
+  if (rew && (int)threadIdx.x < nb) {  // VecNormalize._update_reward: ret = ret * gamma + reward (vec_normalize.py:126-129)
+    const int64_t r = r0 + threadIdx.x;
+    const double v = retv[r] * gamma + (double)rew[r];
+    retv[r] = v;
+    sr[threadIdx.x] = v;
+  }
+  __syncthreads();
+  const int sub = threadIdx.x % MGRP, cg = threadIdx.x / MGRP;
+  constexpr int NCG = BLOCK / MGRP;
+  const double dn = (double)nb;
+  for (int j = cg; j < D; j += NCG) {  // pass 1: column sums -> block mean
+    double s = 0.0;
+    for (int k = sub; k < nb; k += MGRP) s += j < d ? (double)sx[j][k] : sr[k];
+    s = grp_sum8(s);
+    if (sub == 0) smean[j] = s / dn;
+  }
+  __syncthreads();
   double* out = part + (int64_t)blockIdx.x * (1 + 2 * D);
-  for (int j = 0; j < D; j++) {
-    double mj = 0.0, qj = 0.0;
-#pragma unroll
-    for (int k = 0; k < MAXD; k++)
-      if (k == j) mj = mean[k], qj = m2[k];
-    const Mom m = block_merge(Mom{cnt, mj, qj}, sn, sm, sq);
-    if (threadIdx.x == 0) {
-      out[0] = m.n;
-      out[1 + j] = m.mean;
-      out[1 + D + j] = m.m2;
+  for (int j = cg; j < D; j += NCG) {  // pass 2: sum of squared deviations
+    const double m = smean[j];
+    double q = 0.0;
+    for (int k = sub; k < nb; k += MGRP) {
+      const double dv = (j < d ? (double)sx[j][k] : sr[k]) - m;
+      q += dv * dv;
+    }
+    q = grp_sum8(q);
+    if (sub == 0) {
+      out[1 + j] = m;
+      out[1 + D + j] = q;
     }
   }
+  if (threadIdx.x == 0) out[0] = dn;
 }
 
-// merges `parts` records (stride 1+2D) in a fixed order into one record
-__global__ __launch_bounds__(BLOCK) void k_moments_merge(const double* __restrict__ part, int parts, int D,
-                                                         double* __restrict__ out) {
-  __shared__ double sn[BLOCK], sm[BLOCK], sq[BLOCK];
+// merges `parts` records (stride 1+2D) into one: one wave per column (MERGE_WAVES waves, all columns
+// at once for D <= 16), lane l holds records l, l+64, ...
+constexpr int MERGE_WAVES = 16;
+__global__ __launch_bounds__(64 * MERGE_WAVES) void k_moments_merge(const double* __restrict__ part, int parts, int D,
+                                                                    double* __restrict__ out) {
   const int S = 1 + 2 * D;
-  for (int j = 0; j < D; j++) {
-    Mom m{0.0, 0.0, 0.0};
-    for (int k = threadIdx.x; k < parts; k += BLOCK) m = chan(m, Mom{part[k * S], part[k * S + 1 + j], part[k * S + 1 + D + j]});
-    const Mom r = block_merge(m, sn, sm, sq);
-    if (threadIdx.x == 0) {
-      out[0] = r.n;
-      out[1 + j] = r.mean;
-      out[1 + D + j] = r.m2;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int j = w; j < D; j += MERGE_WAVES) {
+    double cn = 0.0, cs = 0.0;
+    for (int k = lane; k < parts; k += 64) {
+      const double nk = part[(int64_t)k * S];
+      cn += nk;
+      cs += nk * part[(int64_t)k * S + 1 + j];
+    }
+    const double N = wave_sum(cn);
+    const double mean = wave_sum(cs) / N;
+    double cq = 0.0;
+    for (int k = lane; k < parts; k += 64) {
+      const double dm = part[(int64_t)k * S + 1 + j] - mean;
+      cq += part[(int64_t)k * S + 1 + D + j] + part[(int64_t)k * S] * (dm * dm);
+    }
+    const double M2 = wave_sum(cq);
+    if (lane == 0) {
+      if (j == 0) out[0] = N;
+      out[1 + j] = mean;
+      out[1 + D + j] = M2;
     }
   }
 }
@@ -328,9 +358,133 @@ __global__ __launch_bounds__(BLOCK) void k_store_rows(RowSegs rs, const int32_t*
 
 __global__ void k_row_advance(int32_t* ctrl) { ctrl[0] += 1; }
 
+
+// ---------------------------------------------------------------------------
+// The default PPO MlpPolicy forward of one collect step (SB3 ActorCriticPolicy.forward,
+// stable_baselines3/common/policies.py:539-553; DiagGaussianDistribution, distributions.py:143-171):
+//   latent_pi = tanh(W1 tanh(W0 x + b0) + b1), mean = Wa latent_pi + ba        (actor MLP)
+//   latent_vf = tanh(V1 tanh(V0 x + c0) + c1), value = Wv latent_vf + bv       (critic MLP)
+//   action = mean + exp(log_std) * noise, log_prob = sum_a N(action | mean, std), clipped = clip(action)
+// (on_policy_algorithm.py:152-161).  Two lanes per env: the even lane runs the actor MLP, the odd lane
+// the critic, both from one LDS image of the nets per block (the critic's 32 banks after the actor's,
+// so a pair's reads do not collide); hidden units stay in VGPRs.  The grid is persistent (at most
+// POL_BLOCKS_PER_CU blocks per CU): a block stages the weights once and walks env tiles of 128.
+// MACs are FMAs in input order; tanh = 1 - 2 / (exp(2x) + 1) on the hardware exp / rcp: results equal the
+// torch module to ~1e-6, not bit for bit.  Measured alternatives (65536 envs, us per launch,
+// profiles/r03_collect_kernels.csv): this layout 39 (non-persistent); weights through SGPRs 51; one net per
+// wave with packed input pairs 94; two envs per lane 100 (register-bound).
+// ---------------------------------------------------------------------------
+constexpr int POL_MAXD = 32, POL_MAXH = 64, POL_MAXA = 8;
+constexpr int POL_BLOCK = 256;  // 128 envs per tile
+constexpr int POL_BLOCKS_PER_CU = 2;
+
+__host__ __device__ inline int pol_net_floats(int d, int H, int out) { return H * d + H + H * H + H + out * H + out; }
+__host__ __device__ inline int pol_vf_offset(int d, int H, int A) { return ((pol_net_floats(d, H, A) + 63) / 64) * 64 + 32; }
+
+__device__ __forceinline__ float ftanh(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);  // exp(2x)
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+}
+
+template <int H>
+__global__ __launch_bounds__(POL_BLOCK) void k_policy_forward(fw_mlp_policy P, const float* __restrict__ obs, int64_t n,
+                                                               const float* __restrict__ noise,
+                                                               const float* __restrict__ low, const float* __restrict__ high,
+                                                               float* __restrict__ act_out, float* __restrict__ clip_out,
+                                                               float* __restrict__ val_out, float* __restrict__ logp_out) {
+  extern __shared__ float W[];  // actor image, critic image: W0^T [d][H] | b0 | W1 [H][H] | b1 | head [out][H] | head b
+  const int d = P.d, A = P.act_dim;
+  const int off_vf = pol_vf_offset(d, H, A);
+  {
+    const float* src[2][6] = {{P.pi_w0, P.pi_b0, P.pi_w1, P.pi_b1, P.act_w, P.act_b},
+                              {P.vf_w0, P.vf_b0, P.vf_w1, P.vf_b1, P.val_w, P.val_b}};
+    for (int net = 0; net < 2; net++) {
+      float* img = W + (net ? off_vf : 0);
+      const int out = net ? 1 : A;
+      for (int i = threadIdx.x; i < H * d; i += POL_BLOCK) {  // nn.Linear [H][d] -> [d][H]
+        const int r = i / d, c = i - r * d;
+        img[c * H + r] = src[net][0][i];
+      }
+      img += d * H;
+      const int len[5] = {H, H * H, H, out * H, out};
+      for (int k = 0; k < 5; k++) {
+        for (int i = threadIdx.x; i < len[k]; i += POL_BLOCK) img[i] = src[net][k + 1][i];
+        img += len[k];
+      }
+    }
+  }
+  __syncthreads();
+  const bool critic = threadIdx.x & 1;
+  const float* w0 = W + (critic ? off_vf : 0);
+  const float* b0 = w0 + H * d;
+  const float* w1 = b0 + H;
+  const float* b1 = w1 + H * H;
+  const float* wh = b1 + H;
+  const float* bh = wh + (critic ? 1 : A) * H;
+  const float half_log_2pi = 0.91893853320467274f;  // 0.5 * log(2 pi)
+  for (int64_t tile = blockIdx.x; tile * (POL_BLOCK / 2) < n; tile += gridDim.x) {
+    const int64_t env = tile * (POL_BLOCK / 2) + (threadIdx.x >> 1);
+    if (env >= n) break;
+    float h0[H], h1[H];
+#pragma unroll
+    for (int i = 0; i < H; i++) h0[i] = 0.0f;
+    for (int k = 0; k < d; k++) {  // every unit sums its inputs in order k = 0 .. d-1
+      const float xk = obs[env * d + k];
+      const float4* col = reinterpret_cast<const float4*>(w0 + k * H);
+#pragma unroll
+      for (int j = 0; j < H / 4; j++) {
+        const float4 q = col[j];
+        h0[4 * j] = fmaf(q.x, xk, h0[4 * j]);
+        h0[4 * j + 1] = fmaf(q.y, xk, h0[4 * j + 1]);
+        h0[4 * j + 2] = fmaf(q.z, xk, h0[4 * j + 2]);
+        h0[4 * j + 3] = fmaf(q.w, xk, h0[4 * j + 3]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < H; i++) h0[i] = ftanh(h0[i] + b0[i]);
+#pragma unroll
+    for (int i = 0; i < H; i++) {
+      const float4* r = reinterpret_cast<const float4*>(w1 + i * H);
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k < H / 4; k++) {
+        const float4 q = r[k];
+        acc = fmaf(q.x, h0[4 * k], acc);
+        acc = fmaf(q.y, h0[4 * k + 1], acc);
+        acc = fmaf(q.z, h0[4 * k + 2], acc);
+        acc = fmaf(q.w, h0[4 * k + 3], acc);
+      }
+      h1[i] = ftanh(acc + b1[i]);
+    }
+    if (critic) {
+      float v = 0.0f;
+#pragma unroll
+      for (int k = 0; k < H; k++) v = fmaf(wh[k], h1[k], v);
+      val_out[env] = v + bh[0];
+      continue;
+    }
+    float lp = 0.0f;
+    for (int a = 0; a < A; a++) {
+      float m = 0.0f;
+#pragma unroll
+      for (int k = 0; k < H; k++) m = fmaf(wh[a * H + k], h1[k], m);
+      m = m + bh[a];
+      const float ls = P.log_std[a];
+      const float sd = expf(ls);
+      // the module's arithmetic (rollout.py MlpActorCritic.forward): separate mul / add, as torch's kernels
+      const float act = noise ? m + sd * noise[env * A + a] : m;
+      const float dv = act - m;
+      lp = lp + (((-(dv * dv)) / ((2.0f * sd) * sd) - ls) - half_log_2pi);
+      act_out[env * A + a] = act;
+      if (clip_out) clip_out[env * A + a] = fmaxf(fminf(act, high[a]), low[a]);
+    }
+    logp_out[env] = lp;
+  }
+}
+
 unsigned grid_for(int64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
 
-int moments_parts(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(MAX_PARTS, (n + BLOCK - 1) / BLOCK)); }
+int64_t moments_parts(int64_t n) { return std::max<int64_t>(1, (n + MROWS - 1) / MROWS); }
 
 }  // namespace
 
@@ -360,15 +514,15 @@ int fw_moments(const float* x, int64_t n, int32_t d, int64_t ldx, const float* r
   if (d < 0 || d + 1 > MAXD) return fw::set_error(FW_E_INVALID, "fw_moments: d out of range");
   if ((d > 0 && (!x || ldx < d)) || !workspace || !out || (rew && !ret))
     return fw::set_error(FW_E_INVALID, "fw_moments: bad buffer / stride");
-  const int parts = moments_parts(n);
-  const int64_t rows_per = (n + parts - 1) / parts;
+  const int64_t parts = moments_parts(n);
+  if (parts > INT32_MAX / 2) return fw::set_error(FW_E_INVALID, "fw_moments: n too large");
   const int D = d + (rew ? 1 : 0);
   if (D == 0) return fw::set_error(FW_E_INVALID, "fw_moments: nothing to reduce");
   hipStream_t s = (hipStream_t)stream;
   double* part = (double*)workspace;
-  hipLaunchKernelGGL(k_moments_partial, dim3(parts), dim3(BLOCK), 0, s, x, n, d, ldx, rew, ret, gamma, rows_per, part);
+  hipLaunchKernelGGL(k_moments_partial, dim3((unsigned)parts), dim3(BLOCK), 0, s, x, n, d, ldx, rew, ret, gamma, part);
   FW_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_moments_merge, dim3(1), dim3(BLOCK), 0, s, part, parts, D, out);
+  hipLaunchKernelGGL(k_moments_merge, dim3(1), dim3(64 * std::min(D, MERGE_WAVES)), 0, s, part, (int)parts, D, out);
   FW_HIP(hipGetLastError());
   return FW_OK;
 }
@@ -443,10 +597,39 @@ int fw_rollout_store(const fw_row_seg* segs, int32_t n_segs, int32_t* ctrl_dev, 
     hipLaunchKernelGGL(k_store_rows, dim3(grid), dim3(BLOCK), 0, s, rs, (const int32_t*)ctrl_dev);
     FW_HIP(hipGetLastError());
   }
-  if (advance) {
+  if (advance) {  // a second launch: a last-block increment inside k_store_rows serialises ~5k atomics
+                  // on one address (198 vs 7 us per step, profiles/r03_collect_kernels.csv)
     hipLaunchKernelGGL(k_row_advance, dim3(1), dim3(1), 0, s, ctrl_dev);
     FW_HIP(hipGetLastError());
   }
+  return FW_OK;
+}
+
+
+int fw_policy_forward(const fw_mlp_policy* p, const float* obs, int64_t n, const float* noise, const float* low,
+                      const float* high, float* actions, float* clipped, float* values, float* log_probs, void* stream) {
+  if (!p || !obs || !actions || !values || !log_probs || n < 1)
+    return fw::set_error(FW_E_INVALID, "fw_policy_forward: NULL buffer or n < 1");
+  if (p->d < 1 || p->d > POL_MAXD || p->hidden != POL_MAXH || p->act_dim < 1 || p->act_dim > POL_MAXA)
+    return fw::set_error(FW_E_INVALID, "fw_policy_forward: d 1..32, hidden 64 (SB3's default net_arch), act_dim 1..8");
+  const void* ptrs[13] = {p->pi_w0, p->pi_b0, p->pi_w1, p->pi_b1, p->act_w, p->act_b, p->vf_w0,
+                          p->vf_b0, p->vf_w1, p->vf_b1, p->val_w, p->val_b, p->log_std};
+  for (const void* q : ptrs)
+    if (!q) return fw::set_error(FW_E_INVALID, "fw_policy_forward: NULL parameter");
+  if (clipped && (!low || !high)) return fw::set_error(FW_E_INVALID, "fw_policy_forward: clipped needs low and high");
+  const int d = p->d, H = p->hidden, A = p->act_dim;
+  const size_t lds = (size_t)(pol_vf_offset(d, H, A) + pol_net_floats(d, H, 1)) * sizeof(float);
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    FW_HIP(hipGetDevice(&dev));
+    FW_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const int64_t tiles = (n + POL_BLOCK / 2 - 1) / (POL_BLOCK / 2);
+  const unsigned grid = (unsigned)std::min<int64_t>(tiles, (int64_t)cus * POL_BLOCKS_PER_CU);
+  hipLaunchKernelGGL(k_policy_forward<POL_MAXH>, dim3(grid), dim3(POL_BLOCK), lds, (hipStream_t)stream, *p, obs, n, noise,
+                     low, high, actions, clipped, values, log_probs);
+  FW_HIP(hipGetLastError());
   return FW_OK;
 }
 

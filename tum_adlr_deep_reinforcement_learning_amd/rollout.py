@@ -205,6 +205,47 @@ class MlpActorCritic(nn.Module):
                     nn.init.orthogonal_(layer.weight, gain=g)
                     nn.init.zeros_(layer.bias)
 
+    deterministic_rollout = False  # collect_step without exploration noise (actions = mean)
+
+    def fused_ok(self, obs):
+        """collect_step can run as the fused fw_policy_forward kernel: SB3's default shapes on the device."""
+        hid = [m.out_features for m in self.pi if isinstance(m, nn.Linear)]
+        return (obs.is_cuda and obs.dtype == torch.float32 and obs.dim() == 2 and obs.shape[1] <= 32
+                and hid == [64, 64] and [m.out_features for m in self.vf if isinstance(m, nn.Linear)] == [64, 64]
+                and self.action_net.out_features <= 8 and self.log_std.dtype == torch.float32)
+
+    @torch.no_grad()
+    def collect_step(self, obs, low, high, out=None):
+        """One collect step's policy work (ActorCriticPolicy.forward, policies.py:539-553, + the action
+        clip, on_policy_algorithm.py:158-161) as ONE fw_policy_forward launch: returns (actions, clipped,
+        values [N], log_probs).  The exploration noise is torch.randn (the module's own sampler); ``out``
+        = four preallocated tensors to write into (a captured collect step).  Equal to forward() within
+        ~1e-6 (FMA order), not bit for bit."""
+        n, d = obs.shape
+        A = self.action_net.out_features
+        if out is None:
+            out = (torch.empty(n, A, device=obs.device), torch.empty(n, A, device=obs.device),
+                   torch.empty(n, device=obs.device), torch.empty(n, device=obs.device))
+        act, clip, val, logp = out
+        noise = None if self.deterministic_rollout else torch.randn(n, A, device=obs.device)
+        if not hasattr(self, "_fw_p"):
+            self._fw_p = _native.FwMlpPolicy()
+        lin = [m for m in self.pi if isinstance(m, nn.Linear)] + [self.action_net] + \
+              [m for m in self.vf if isinstance(m, nn.Linear)] + [self.value_net]
+        p = self._fw_p
+        for k, m in zip((("pi_w0", "pi_b0"), ("pi_w1", "pi_b1"), ("act_w", "act_b"), ("vf_w0", "vf_b0"),
+                         ("vf_w1", "vf_b1"), ("val_w", "val_b")), lin):
+            assert m.weight.is_contiguous() and m.bias.is_contiguous()
+            setattr(p, k[0], m.weight.data_ptr())
+            setattr(p, k[1], m.bias.data_ptr())
+        p.log_std, p.d, p.hidden, p.act_dim = self.log_std.data_ptr(), d, 64, A
+        obs = obs.contiguous()
+        lib = _native.load()
+        _native.check(lib.fw_policy_forward(ctypes.byref(p), _p(obs), n, _p(noise) if noise is not None else None,
+                                            _p(low), _p(high), _p(act), _p(clip), _p(val), _p(logp),
+                                            _stream(obs.device)), "fw_policy_forward")
+        return act, clip, val, logp
+
     def forward(self, obs, deterministic=False):
         mean = self.action_net(self.pi(obs))
         values = self.value_net(self.vf(obs))
@@ -251,11 +292,15 @@ class RolloutCollector:
         if graph and self._graph_ok():
             return self._collect_graphed(n)
         buf.reset()
+        fused = self._fused(buf.observations[0])
         for t in range(n):
             obs_slot = buf.observations[t]
             obs_slot.copy_(self.last_obs)
-            actions, values, log_probs = self.policy(obs_slot)
-            clipped = torch.max(torch.min(actions, self.high), self.low)
+            if fused:
+                actions, clipped, values, log_probs = self.policy.collect_step(obs_slot, self.low, self.high)
+            else:
+                actions, values, log_probs = self.policy(obs_slot)
+                clipped = torch.max(torch.min(actions, self.high), self.low)
             new_obs, rewards, dones, _ = env.step(clipped)
             buf.actions[t].copy_(actions)
             buf.rewards[t].copy_(rewards)
@@ -269,6 +314,13 @@ class RolloutCollector:
         buf.compute_returns_and_advantage(last_values, self.last_dones)
         self._eager_done = True
         return buf
+
+    def _fused(self, obs):
+        """The policy's step runs as one fw_policy_forward launch (MlpActorCritic with SB3's default shapes;
+        any other policy module runs its own forward)."""
+        pol = self.policy
+        return (hasattr(pol, "collect_step") and type(pol).forward is MlpActorCritic.forward and
+                self.low.dtype == torch.float32 and pol.fused_ok(obs))
 
     # ------------------------------------------------------------ graphed collection
     def _graph_ok(self):
@@ -300,26 +352,25 @@ class RolloutCollector:
         self.s_obs = torch.empty(N, D, dtype=torch.float32, device=dev)
         self.s_start = torch.empty(N, dtype=torch.uint8, device=dev)
         self.s_act = torch.empty(N, A, dtype=torch.float32, device=dev)
-        self.s_rew = torch.empty(N, dtype=torch.float32, device=dev)
+        self.s_clip = torch.empty(N, A, dtype=torch.float32, device=dev)
         self.s_val = torch.empty(N, dtype=torch.float32, device=dev)
         self.s_logp = torch.empty(N, dtype=torch.float32, device=dev)
         self._ctrl = torch.zeros(2, dtype=torch.int32, device=dev)  # {row, n_rows} of fw_rollout_store
-        rows = ((self.s_obs, buf.observations, 1), (self.s_start, buf.dones, 1), (self.s_act, buf.actions, 0),
-                (self.s_rew, buf.rewards, 0), (self.s_val, buf.values, 0), (self.s_logp, buf.log_probs, 0))
-        self._rsegs = (_native.FwRowSeg * len(rows))()
-        for k, (src, dst, off) in enumerate(rows):
-            rb = dst[0].numel() * dst.element_size()
-            g = self._rsegs[k]
-            g.src, g.dst, g.bytes, g.stride, g.row_off = src.data_ptr(), dst.data_ptr(), rb, rb, off
         lib = _native.load()
         split = self._split()
+        fused = self._fused(self.s_obs)
 
         def head():
-            actions, values, log_probs = self.policy(self.s_obs)
-            clipped = torch.max(torch.min(actions, self.high), self.low)
-            self.s_act.copy_(actions)
-            self.s_val.copy_(values.reshape(-1))
-            self.s_logp.copy_(log_probs)
+            if fused:  # one fw_policy_forward launch writes the step's outputs in place
+                self.policy.collect_step(self.s_obs, self.low, self.high,
+                                         out=(self.s_act, self.s_clip, self.s_val, self.s_logp))
+                clipped = self.s_clip
+            else:
+                actions, values, log_probs = self.policy(self.s_obs)
+                clipped = torch.max(torch.min(actions, self.high), self.low)
+                self.s_act.copy_(actions)
+                self.s_val.copy_(values.reshape(-1))
+                self.s_logp.copy_(log_probs)
             if split:
                 env.step_async(clipped)
                 env.step_wait_local()
@@ -328,9 +379,23 @@ class RolloutCollector:
 
         def tail(res):
             new_obs, rewards, dones, _ = env.step_wait_finish() if res is None else res
-            self.s_rew.copy_(rewards)
-            self.s_obs.copy_(new_obs.reshape(N, D))
+            self.s_obs.copy_(new_obs.reshape(N, D))  # the next step's policy input
             self.s_start.copy_(dones)
+            # the step's rows straight from where they were produced (the captured env outputs keep their
+            # addresses on every replay); the episode starts of row t + 1 from the static s_start
+            rew = rewards.reshape(N)
+            if rew.dtype != buf.rewards.dtype or not rew.is_contiguous():  # e.g. an fp64 env: convert once
+                self.s_rew = torch.empty(N, dtype=buf.rewards.dtype, device=dev)
+                self.s_rew.copy_(rew)
+                rew = self.s_rew
+            rows = ((self.s_obs, buf.observations, 1), (self.s_start, buf.dones, 1), (self.s_act, buf.actions, 0),
+                    (rew, buf.rewards, 0), (self.s_val, buf.values, 0), (self.s_logp, buf.log_probs, 0))
+            self._rsegs = (_native.FwRowSeg * len(rows))()
+            for k, (src, dst, off) in enumerate(rows):
+                assert src.dtype == dst.dtype and src.is_contiguous()
+                rb = dst[0].numel() * dst.element_size()
+                g = self._rsegs[k]
+                g.src, g.dst, g.bytes, g.stride, g.row_off = src.data_ptr(), dst.data_ptr(), rb, rb, off
             # the stream is read here, inside the capture: torch.cuda.graph captures on its own side stream
             _native.check(lib.fw_rollout_store(self._rsegs, len(rows), _p(self._ctrl), 1, _stream(dev)),
                           "fw_rollout_store")
