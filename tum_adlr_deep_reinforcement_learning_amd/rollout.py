@@ -380,7 +380,13 @@ class RolloutCollector:
         def tail(res):
             new_obs, rewards, dones, _ = env.step_wait_finish() if res is None else res
             self.s_obs.copy_(new_obs.reshape(N, D))  # the next step's policy input
-            self.s_start.copy_(dones)
+            d8 = dones.reshape(N)
+            if d8.dtype == torch.bool and d8.is_contiguous():
+                d8 = d8.view(torch.uint8)  # the env's done buffer itself, no conversion kernel
+            else:
+                self.s_start.copy_(d8)
+                d8 = self.s_start
+            self._dsrc = d8  # the episode starts of the next row (and, after the last step, last_dones)
             # the step's rows straight from where they were produced (the captured env outputs keep their
             # addresses on every replay); the episode starts of row t + 1 from the static s_start
             rew = rewards.reshape(N)
@@ -388,7 +394,7 @@ class RolloutCollector:
                 self.s_rew = torch.empty(N, dtype=buf.rewards.dtype, device=dev)
                 self.s_rew.copy_(rew)
                 rew = self.s_rew
-            rows = ((self.s_obs, buf.observations, 1), (self.s_start, buf.dones, 1), (self.s_act, buf.actions, 0),
+            rows = ((self.s_obs, buf.observations, 1), (d8, buf.dones, 1), (self.s_act, buf.actions, 0),
                     (rew, buf.rewards, 0), (self.s_val, buf.values, 0), (self.s_logp, buf.log_probs, 0))
             self._rsegs = (_native.FwRowSeg * len(rows))()
             for k, (src, dst, off) in enumerate(rows):
@@ -419,9 +425,8 @@ class RolloutCollector:
         N, D = buf.n_envs, buf.obs_dim
         buf.reset()
         self.s_obs.copy_(self.last_obs.reshape(N, D))
-        self.s_start.copy_(self.last_dones)
         buf.observations[0].copy_(self.s_obs)  # the inputs of step 0; step t stores those of t + 1
-        buf.dones[0].copy_(self.s_start)
+        buf.dones[0].copy_(self.last_dones)
         self._ctrl[0] = 0
         self._ctrl[1] = n
         if len(self._graphs) == 1:
@@ -435,7 +440,7 @@ class RolloutCollector:
                 self.env.step_exchange()  # the RCCL all-gather of the moment records
                 g1.replay()
         self.last_obs = self.s_obs.clone().reshape(self.last_obs.shape)
-        self.last_dones = self.s_start.clone()
+        self.last_dones = self._dsrc.clone()
         buf.pos, buf.full = n, n == buf.buffer_size
         last_values = self.policy.predict_values(self.last_obs)
         buf.compute_returns_and_advantage(last_values, self.last_dones)

@@ -267,7 +267,9 @@ class FixedWingVecEnv(VecEnv):
             obs, rew, done, term = eng.env_step(self._actions, auto_reset=True, stats=True)
         self._actions = None
         if self.return_tensors:
-            return self._shaped(obs), rew, done.bool(), self._infos_lazy_device()
+            # a bool view of the engine's uint8 done buffer (no conversion kernel); like obs and rew it is
+            # the engine's buffer, overwritten by the next step
+            return self._shaped(obs), rew, done.view(torch.bool), self._infos_lazy_device()
         done_np = done.cpu().numpy().astype(bool)
         infos = self._infos(done_np)
         return self._shaped(obs.cpu().numpy().astype(np.float32)), rew.cpu().numpy().astype(np.float32), done_np, infos

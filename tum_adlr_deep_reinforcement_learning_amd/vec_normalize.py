@@ -87,6 +87,8 @@ class VecNormalize:
         W = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
         self._parts = torch.empty(W, self._rec.numel(), dtype=torch.float64, device=dev)
         self._parts_ret = torch.empty(W, 3, dtype=torch.float64, device=dev)
+        if W == 1:  # the record is written where update_from_moments reads it (no copy per step)
+            self._rec = self._parts[0]
         self._zero_rew = torch.zeros(n, dtype=torch.float32, device=dev)
         self.obs_out = torch.empty(n, d, dtype=torch.float32, device=dev)
         self.rew_out = torch.empty(n, dtype=torch.float32, device=dev)
@@ -101,6 +103,9 @@ class VecNormalize:
 
     def _gather(self, rec):
         """Rank-ordered moment records of the global batch ([W][len]), into the static parts buffer."""
+        import torch.distributed as dist
+        if rec is self._rec and self._parts.shape[0] == 1 and not (dist.is_available() and dist.is_initialized()):
+            return self._parts, 1  # no process group: the record was written in place (_rec aliases _parts[0])
         out = all_gather_flat(rec, self.group, out=self._parts if rec is self._rec else self._parts_ret)
         return out, out.shape[0]
 
@@ -181,7 +186,8 @@ class VecNormalize:
         obs = obs.to(torch.float32).contiguous()
         rews = rews.to(torch.float32).contiguous()
         self.old_obs, self.old_reward = obs, rews
-        self._news, self._infos, self._done_u8 = news, infos, news.to(torch.uint8).contiguous()
+        u8 = news.view(torch.uint8) if (news.dtype == torch.bool and news.is_contiguous()) else news.to(torch.uint8)
+        self._news, self._infos, self._done_u8 = news, infos, u8.contiguous()
         if self.training:
             self._moments(obs, rews)
 
