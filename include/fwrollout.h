@@ -114,6 +114,9 @@ typedef struct fw_mlp_policy {
   const float *pi_w0, *pi_b0, *pi_w1, *pi_b1, *act_w, *act_b;
   const float *vf_w0, *vf_b0, *vf_w1, *vf_b1, *val_w, *val_b;
   const float* log_std;
+  /* optional device int32: the noise rows of the whole collection are in `noise` ([T][n][A]) and this
+   * launch reads row *noise_row (e.g. fw_rollout_store's ctrl[0]), so a captured step draws no RNG */
+  const int32_t* noise_row;
   int32_t d, hidden, act_dim, pad;
 } fw_mlp_policy;
 int fw_policy_forward(const fw_mlp_policy* p, const float* obs, int64_t n, const float* noise, const float* low,

@@ -371,10 +371,10 @@ def test_partial_collect_bootstraps_at_last_stored_row():
 
 
 def test_graphed_collect_equals_eager():
-    """collect(graph=True) (one captured step replayed, buffer writes by fw_replay_add) stores the same
-    rollout as the eager collect: bit for bit with a deterministic policy, over auto-resets and
-    VecNormalize updates, on two consecutive collections; with the stochastic policy the graphed
-    rollout's GAE equals the oracle's."""
+    """collect(graph=True) (one captured step replayed, buffer writes by fw_rollout_store) stores the same
+    rollout as the eager collect: bit for bit, over auto-resets and VecNormalize updates, on two
+    consecutive collections -- the torch policy (deterministic), the fused policy launch deterministic
+    and with its exploration noise; and the stochastic graphed rollout's GAE equals the oracle's."""
     from tum_adlr_deep_reinforcement_learning_amd.rollout import MlpActorCritic, RolloutBuffer, RolloutCollector
     from tum_adlr_deep_reinforcement_learning_amd.vec_env import FixedWingVecEnv
     from tum_adlr_deep_reinforcement_learning_amd.vec_normalize import VecNormalize
@@ -398,14 +398,20 @@ def test_graphed_collect_equals_eager():
                             n_envs=n)
         return venv, env, buf, RolloutCollector(env, policy, buf)
 
-    for cls in (Det, DetFused):
+    # MlpActorCritic itself: the fused launch with exploration noise, drawn once per collection (the same
+    # draws for the eager and the captured collection when the generator is seeded alike)
+    for cls in (Det, DetFused, MlpActorCritic):
         va, ea, ba, ca = make(cls)
         vb, eb, bb, cb = make(cls)
-        assert ca._fused(ba.observations[0]) == (cls is DetFused)
+        assert ca._fused(ba.observations[0]) == (cls is not Det)
+        torch.manual_seed(40)
         ca.collect(8)
+        torch.manual_seed(40)
         cb.collect(8)
-        for _ in range(2):
+        for i in range(2):
+            torch.manual_seed(41 + i)
             ca.collect()
+            torch.manual_seed(41 + i)
             cb.collect(graph=True)
             for f in ("slab", "rewards", "dones"):
                 assert torch.equal(getattr(ba, f), getattr(bb, f)), (cls.__name__, f)

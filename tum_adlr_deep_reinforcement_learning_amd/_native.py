@@ -158,7 +158,7 @@ class FwRowSeg(ctypes.Structure):  # include/fwrollout.h fw_row_seg
 
 class FwMlpPolicy(ctypes.Structure):  # include/fwrollout.h fw_mlp_policy
     _fields_ = [(k, _vp) for k in ("pi_w0", "pi_b0", "pi_w1", "pi_b1", "act_w", "act_b", "vf_w0", "vf_b0", "vf_w1",
-                                   "vf_b1", "val_w", "val_b", "log_std")] + \
+                                   "vf_b1", "val_w", "val_b", "log_std", "noise_row")] + \
                [("d", _i32), ("hidden", _i32), ("act_dim", _i32), ("pad", _i32)]
 
 

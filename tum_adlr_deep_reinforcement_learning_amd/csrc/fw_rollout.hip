@@ -53,6 +53,16 @@ constexpr int MAXD = 33;     // observation dims (FW_MAX_OBS) + the return colum
 //             last  = (f64)delta + (f64)(f32(gamma*lam)*nnt) * last   (float64)
 //   adv[t] = f32(last); ret[t] = adv[t] + v                 (float32)
 // ---------------------------------------------------------------------------
+// A product that feeds an addition goes through this barrier: the __dmul_rn / __dadd_rn (and f32) header
+// functions carry the default fp-contract flags, so after inlining the backend fused them into an FMA
+// despite the file's contract(off) -- one element in 16.7M of a 65536 x 256 rollout was 1 ulp off
+// numpy's (test_c3_rollout_collector_full_size); an opaque register keeps multiply and add separate.
+template <typename F>
+__device__ __forceinline__ F nofuse(F x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 __global__ __launch_bounds__(BLOCK) void k_gae(const float* __restrict__ rew, const float* __restrict__ val,
                                                const uint8_t* __restrict__ starts, const float* __restrict__ last_v,
                                                const uint8_t* __restrict__ last_d, int64_t T, int64_t N, float gamma_f,
@@ -64,8 +74,8 @@ __global__ __launch_bounds__(BLOCK) void k_gae(const float* __restrict__ rew, co
   {
     const double nnt = last_d[e] ? 0.0 : 1.0;
     const float a = __fmul_rn(gamma_f, last_v[e]);
-    const double delta = __dsub_rn(__dadd_rn((double)rew[t * N + e], __dmul_rn((double)a, nnt)), (double)v);
-    const double last0 = __dadd_rn(delta, __dmul_rn(__dmul_rn(gl, nnt), 0.0));
+    const double delta = __dsub_rn(__dadd_rn((double)rew[t * N + e], nofuse(__dmul_rn((double)a, nnt))), (double)v);
+    const double last0 = __dadd_rn(delta, nofuse(__dmul_rn(__dmul_rn(gl, nnt), 0.0)));
     const float af = (float)last0;
     adv[t * N + e] = af;
     ret[t * N + e] = __fadd_rn(af, v);
@@ -89,10 +99,10 @@ __global__ __launch_bounds__(BLOCK) void k_gae(const float* __restrict__ rew, co
         const int64_t tt = t0 - k;
         if (tt >= 0) {
           const float nnt = nstart ? 0.f : 1.f;
-          const float b = __fmul_rn(__fmul_rn(gamma_f, nv), nnt);
+          const float b = nofuse(__fmul_rn(__fmul_rn(gamma_f, nv), nnt));
           const float dl = __fsub_rn(__fadd_rn(rr[k], b), vv[k]);
           const float coef = __fmul_rn(gl_f, nnt);
-          last = __dadd_rn((double)dl, __dmul_rn((double)coef, last));
+          last = __dadd_rn((double)dl, nofuse(__dmul_rn((double)coef, last)));
           const float a2 = (float)last;
           adv[tt * N + e] = a2;
           ret[tt * N + e] = __fadd_rn(a2, vv[k]);
@@ -281,13 +291,16 @@ __global__ __launch_bounds__(BLOCK) void k_vecnorm_apply(const float* __restrict
                                                          const float* __restrict__ rew, int norm_rew, double clip_rew,
                                                          float* __restrict__ rew_out, const uint8_t* __restrict__ done,
                                                          double* __restrict__ retv) {
+  __shared__ double sden[MAXD];  // np.sqrt(var + eps) per column, once per block
+  if (norm_obs && (int)threadIdx.x < d) sden[threadIdx.x] = sqrt(rms[d + threadIdx.x] + eps);
+  __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (i >= n) return;
   if (obs_out) {
     for (int j = 0; j < d; j++) {
       const float o = obs[i * ldx + j];
       if (norm_obs) {  // np.clip((obs - mean) / np.sqrt(var + eps), -clip, clip).astype(float32)
-        double y = ((double)o - rms[j]) / sqrt(rms[d + j] + eps);
+        double y = ((double)o - rms[j]) / sden[j];
         y = fmin(fmax(y, -clip_obs), clip_obs);
         obs_out[i * ld_out + j] = (float)y;
       } else {
@@ -422,6 +435,7 @@ __global__ __launch_bounds__(POL_BLOCK) void k_policy_forward(fw_mlp_policy P, c
   const float* wh = b1 + H;
   const float* bh = wh + (critic ? 1 : A) * H;
   const float half_log_2pi = 0.91893853320467274f;  // 0.5 * log(2 pi)
+  if (noise && P.noise_row) noise += (int64_t)P.noise_row[0] * n * A;  // this step's row of the collection's draws
   for (int64_t tile = blockIdx.x; tile * (POL_BLOCK / 2) < n; tile += gridDim.x) {
     const int64_t env = tile * (POL_BLOCK / 2) + (threadIdx.x >> 1);
     if (env >= n) break;

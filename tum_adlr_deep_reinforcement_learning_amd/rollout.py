@@ -215,19 +215,23 @@ class MlpActorCritic(nn.Module):
                 and self.action_net.out_features <= 8 and self.log_std.dtype == torch.float32)
 
     @torch.no_grad()
-    def collect_step(self, obs, low, high, out=None):
+    def collect_step(self, obs, low, high, out=None, noise=None, noise_row=None):
         """One collect step's policy work (ActorCriticPolicy.forward, policies.py:539-553, + the action
         clip, on_policy_algorithm.py:158-161) as ONE fw_policy_forward launch: returns (actions, clipped,
-        values [N], log_probs).  The exploration noise is torch.randn (the module's own sampler); ``out``
-        = four preallocated tensors to write into (a captured collect step).  Equal to forward() within
-        ~1e-6 (FMA order), not bit for bit."""
+        values [N], log_probs).  The exploration noise is torch.randn (the module's own sampler): drawn
+        here, or given -- ``noise`` [N][A], or the whole collection's draws [T][N][A] with ``noise_row`` a
+        device int32 holding this step's row (a captured step then draws no RNG).  ``out`` = four
+        preallocated tensors to write into.  Equal to forward() within ~1e-6 (FMA order), not bit for bit."""
         n, d = obs.shape
         A = self.action_net.out_features
         if out is None:
             out = (torch.empty(n, A, device=obs.device), torch.empty(n, A, device=obs.device),
                    torch.empty(n, device=obs.device), torch.empty(n, device=obs.device))
         act, clip, val, logp = out
-        noise = None if self.deterministic_rollout else torch.randn(n, A, device=obs.device)
+        if self.deterministic_rollout:
+            noise, noise_row = None, None
+        elif noise is None:
+            noise, noise_row = torch.randn(n, A, device=obs.device), None
         if not hasattr(self, "_fw_p"):
             self._fw_p = _native.FwMlpPolicy()
         lin = [m for m in self.pi if isinstance(m, nn.Linear)] + [self.action_net] + \
@@ -239,6 +243,7 @@ class MlpActorCritic(nn.Module):
             setattr(p, k[0], m.weight.data_ptr())
             setattr(p, k[1], m.bias.data_ptr())
         p.log_std, p.d, p.hidden, p.act_dim = self.log_std.data_ptr(), d, 64, A
+        p.noise_row = noise_row.data_ptr() if noise_row is not None else None
         obs = obs.contiguous()
         lib = _native.load()
         _native.check(lib.fw_policy_forward(ctypes.byref(p), _p(obs), n, _p(noise) if noise is not None else None,
@@ -293,11 +298,13 @@ class RolloutCollector:
             return self._collect_graphed(n)
         buf.reset()
         fused = self._fused(buf.observations[0])
+        noise = self._draw_noise(n) if fused else None
         for t in range(n):
             obs_slot = buf.observations[t]
             obs_slot.copy_(self.last_obs)
             if fused:
-                actions, clipped, values, log_probs = self.policy.collect_step(obs_slot, self.low, self.high)
+                actions, clipped, values, log_probs = self.policy.collect_step(
+                    obs_slot, self.low, self.high, noise=noise[t] if noise is not None else None)
             else:
                 actions, values, log_probs = self.policy(obs_slot)
                 clipped = torch.max(torch.min(actions, self.high), self.low)
@@ -314,6 +321,20 @@ class RolloutCollector:
         buf.compute_returns_and_advantage(last_values, self.last_dones)
         self._eager_done = True
         return buf
+
+    def _draw_noise(self, n):
+        """The exploration noise of a whole fused collection in one torch.randn ([buffer_size][N][A], rows
+        0..n-1 drawn): the eager and the captured collection read the same draws, and a replayed step
+        draws nothing (torch's per-replay RNG bookkeeping costs two fill kernels + a randn per step)."""
+        if getattr(self.policy, "deterministic_rollout", False):
+            return None
+        buf = self.buffer
+        shape = (buf.buffer_size, buf.n_envs, buf.action_dim)
+        if getattr(self, "_noise", None) is None or tuple(self._noise.shape) != shape:
+            self._noise = torch.empty(shape, dtype=torch.float32, device=buf.device)
+        if n > 0:
+            self._noise[:n].normal_()
+        return self._noise
 
     def _fused(self, obs):
         """The policy's step runs as one fw_policy_forward launch (MlpActorCritic with SB3's default shapes;
@@ -362,8 +383,10 @@ class RolloutCollector:
 
         def head():
             if fused:  # one fw_policy_forward launch writes the step's outputs in place
+                noise = self._draw_noise(0)  # the buffer only; each collection draws its rows
                 self.policy.collect_step(self.s_obs, self.low, self.high,
-                                         out=(self.s_act, self.s_clip, self.s_val, self.s_logp))
+                                         out=(self.s_act, self.s_clip, self.s_val, self.s_logp),
+                                         noise=noise, noise_row=self._ctrl if noise is not None else None)
                 clipped = self.s_clip
             else:
                 actions, values, log_probs = self.policy(self.s_obs)
@@ -424,6 +447,8 @@ class RolloutCollector:
             self._capture()
         N, D = buf.n_envs, buf.obs_dim
         buf.reset()
+        if self._fused(self.s_obs):
+            self._draw_noise(n)  # into the buffer the captured policy launch reads (row = ctrl[0])
         self.s_obs.copy_(self.last_obs.reshape(N, D))
         buf.observations[0].copy_(self.s_obs)  # the inputs of step 0; step t stores those of t + 1
         buf.dones[0].copy_(self.last_dones)
