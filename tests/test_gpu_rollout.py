@@ -41,6 +41,21 @@ def test_gae_kernel_bit_exact_vs_reference(case):
     assert np.array_equal(ret, g("returns"))
 
 
+def test_gae_kernel_no_fma_contraction():
+    """One env column of a 65536 x 256 collect on which an FMA-contracted running advantage
+    (fma(coef, last, delta) in fp64) rounds 1 ulp away from numpy's separate multiply and add at step
+    190 (tests/golden/gae_fma_column.npz, captured from test_c3_rollout_collector_full_size's population):
+    the kernel must equal the oracle there bit for bit."""
+    d = F.load("gae_fma_column.npz")
+    rew, val, st = d["rewards"][:, None], d["values"][:, None], d["starts"][:, None]
+    lv, ld = np.array([d["last_value"]], np.float32), np.array([d["last_done"]], np.uint8)
+    adv, ret = _gae_dev(rew, val, st, lv, ld, 0.99, 0.95)
+    a_ref, r_ref = R.gae(rew, val, st, lv, ld, 0.99, 0.95)
+    t = int(d["t"])
+    assert adv[t, 0] == a_ref[t, 0]
+    assert np.array_equal(adv, a_ref) and np.array_equal(ret, r_ref)
+
+
 def test_gae_kernel_ppo_size_vs_oracle():
     rng = np.random.RandomState(9)
     T, N = 2048, 4099  # ragged N (not a multiple of the block)
