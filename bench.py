@@ -498,8 +498,8 @@ def main():
                     help="after the timed steps, time this many more for the long-window steady-state line")
     ap.add_argument("--rollout-steps", type=int, default=-1,
                     help="also run one PPO collect_rollouts of this horizon (2048 = BASELINE configs[2]/[3]); "
-                         "default: 64 on N > 1 GPUs (configs[3]: sharded collection + the RCCL all-gather), "
-                         "none on one")
+                         "default 64 (on N > 1 GPUs configs[3]: sharded collection + the RCCL all-gather); "
+                         "0 = skip")
     ap.add_argument("--sac-fill-steps", type=int, default=0,
                     help="also run a SAC replay-buffer fill of this many steps (BASELINE configs[4])")
     ap.add_argument("--sac-envs", type=int, default=262144, help="global envs of the SAC fill leg")
@@ -593,8 +593,8 @@ def main():
                                "this window's kernel_ms" % pm.get("dispatches")}
 
     rollout = None
-    if args.rollout_steps < 0:
-        args.rollout_steps = 64 if world > 1 else 0
+    if args.rollout_steps < 0:  # configs[2]/[3]-shaped PPO collection, short horizon by default
+        args.rollout_steps = 64
     if args.rollout_steps > 0:
         rollout = rollout_leg(spec, n, args.rollout_steps, dev, rank, world, args.precision)
     sac = None
