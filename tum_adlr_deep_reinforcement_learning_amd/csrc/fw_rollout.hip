@@ -390,6 +390,9 @@ __global__ void k_row_advance(int32_t* ctrl) { ctrl[0] += 1; }
 constexpr int POL_MAXD = 32, POL_MAXH = 64, POL_MAXA = 8;
 constexpr int POL_BLOCK = 256;  // 128 envs per tile
 constexpr int POL_BLOCKS_PER_CU = 2;
+#ifndef FW_POL_ROWPF
+#define FW_POL_ROWPF 0  // 1: hidden-layer rows and heads read whole, four partial sums per unit (A/B)
+#endif
 
 __host__ __device__ inline int pol_net_floats(int d, int H, int out) { return H * d + H + H * H + H + out * H + out; }
 __host__ __device__ inline int pol_vf_offset(int d, int H, int A) { return ((pol_net_floats(d, H, A) + 63) / 64) * 64 + 32; }
@@ -456,6 +459,56 @@ __global__ __launch_bounds__(POL_BLOCK) void k_policy_forward(fw_mlp_policy P, c
     }
 #pragma unroll
     for (int i = 0; i < H; i++) h0[i] = ftanh(h0[i] + b0[i]);
+#if FW_POL_ROWPF
+#pragma unroll
+    for (int i = 0; i < H; i++) {
+      // the whole row in flight, then four independent partial sums (inputs k mod 4, combined as
+      // (s0 + s1) + (s2 + s3)): one dependent chain per unit left each LDS read's latency exposed
+      __builtin_amdgcn_sched_barrier(0);
+      const float4* r = reinterpret_cast<const float4*>(w1 + i * H);
+      float4 rw[H / 4];
+#pragma unroll
+      for (int k = 0; k < H / 4; k++) rw[k] = r[k];
+      float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
+#pragma unroll
+      for (int k = 0; k < H / 4; k++) {
+        c0 = fmaf(rw[k].x, h0[4 * k], c0);
+        c1 = fmaf(rw[k].y, h0[4 * k + 1], c1);
+        c2 = fmaf(rw[k].z, h0[4 * k + 2], c2);
+        c3 = fmaf(rw[k].w, h0[4 * k + 3], c3);
+      }
+      h1[i] = ftanh(((c0 + c1) + (c2 + c3)) + b1[i]);
+    }
+    auto head = [&](const float* row) {  // four partial sums, as the hidden layer
+      const float4* r4 = reinterpret_cast<const float4*>(row);
+      float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
+#pragma unroll
+      for (int k = 0; k < H / 4; k++) {
+        const float4 q = r4[k];
+        c0 = fmaf(q.x, h1[4 * k], c0);
+        c1 = fmaf(q.y, h1[4 * k + 1], c1);
+        c2 = fmaf(q.z, h1[4 * k + 2], c2);
+        c3 = fmaf(q.w, h1[4 * k + 3], c3);
+      }
+      return (c0 + c1) + (c2 + c3);
+    };
+    if (critic) {
+      val_out[env] = head(wh) + bh[0];
+      continue;
+    }
+    float lp = 0.0f;
+    for (int a = 0; a < A; a++) {
+      const float m = head(wh + a * H) + bh[a];
+      const float ls = P.log_std[a];
+      const float sd = expf(ls);
+      // the module's arithmetic (rollout.py MlpActorCritic.forward): separate mul / add, as torch's kernels
+      const float act = noise ? m + sd * noise[env * A + a] : m;
+      const float dv = act - m;
+      lp = lp + (((-(dv * dv)) / ((2.0f * sd) * sd) - ls) - half_log_2pi);
+      act_out[env * A + a] = act;
+      if (clip_out) clip_out[env * A + a] = fmaxf(fminf(act, high[a]), low[a]);
+    }
+#else
 #pragma unroll
     for (int i = 0; i < H; i++) {
       const float4* r = reinterpret_cast<const float4*>(w1 + i * H);
@@ -492,6 +545,7 @@ __global__ __launch_bounds__(POL_BLOCK) void k_policy_forward(fw_mlp_policy P, c
       act_out[env * A + a] = act;
       if (clip_out) clip_out[env * A + a] = fmaxf(fminf(act, high[a]), low[a]);
     }
+#endif
     logp_out[env] = lp;
   }
 }
