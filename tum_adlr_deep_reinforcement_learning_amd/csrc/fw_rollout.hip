@@ -391,7 +391,8 @@ constexpr int POL_MAXD = 32, POL_MAXH = 64, POL_MAXA = 8;
 constexpr int POL_BLOCK = 256;  // 128 envs per tile
 constexpr int POL_BLOCKS_PER_CU = 2;
 #ifndef FW_POL_ROWPF
-#define FW_POL_ROWPF 0  // 1: hidden-layer rows and heads read whole, four partial sums per unit (A/B)
+#define FW_POL_ROWPF 0  // 1: hidden-layer rows and heads read whole, four partial sums per unit (A/B: 38.0 vs
+                        // 38.7 us, within noise, profiles/r03_collect_kernels.csv)
 #endif
 
 __host__ __device__ inline int pol_net_floats(int d, int H, int out) { return H * d + H + H * H + H + out * H + out; }
