@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FWSIM_ABI_VERSION 6
+#define FWSIM_ABI_VERSION 7
 
 /* ---- error codes ---------------------------------------------------------- */
 #define FW_OK 0
@@ -119,7 +119,8 @@ typedef struct fw_sim_config {
   int32_t disabled_inputs;           /* bit0 elevator, bit1 aileron: "disabled" ControlVariables,
                                         whose .value is 0 after reset (pyfly.py:359-363) */
   int32_t wind_random;               /* 1: steady wind magnitude sampled in [mag_min, mag_max] */
-  int32_t max_nfev;                  /* RHS-evaluation budget of one step (0 = 1000000).  scipy has none;
+  int32_t max_nfev;                  /* RHS-evaluation budget of one step (0 = 65535, the largest count the
+                                        stats word reports; 8x the census maximum).  scipy has none;
                                         exhausting it ends the step like solve_ivp's TOO_SMALL_STEP
                                         failure: sol.y[:, -1] (the last accepted sub-step) is committed
                                         and the step counts as a success (pyfly.py:1393-1396).       */
@@ -285,11 +286,21 @@ int fw_num_obs(const fw_handle* h, int32_t* n);
  * fw_create (gym's seed-then-reset reproducibility).  Synchronises the device; a setup call.        */
 int fw_seed(fw_handle* h, uint64_t seed, int64_t env_offset);
 
-/* Turbulence noise injection (parity mode, the turbulence_noise argument of
- * PyFly.reset): N(0,1) samples, SoA [4][len][N], consumed from index 0 at each
- * reset.  NULL reverts to the on-device Philox generator. The buffer must stay
- * alive while the handle uses it.                                            */
+/* Turbulence noise injection (the turbulence_noise argument of PyFly.reset, pyfly.py:1262, which
+ * Wind.reset hands to DrydenGustModel.reset, dryden.py:174-188): N(0,1) samples, SoA [4][len][N],
+ * read from index 0 at each reset; step k of an episode reads sample k mod len (dryden.py:209-236
+ * wraps a sequence shorter than the episode).  NULL reverts to the on-device Philox generator.  The
+ * buffer must stay alive while the handle uses it.                                                 */
 int fw_set_noise(fw_handle* h, const void* noise_dev, int64_t len);
+
+/* Per-env injection (env_method("reset", indices=..., turbulence_noise=...) -> FixedWingAircraft.reset
+ * (**sim_reset_kw), fixed_wing.py:414-441): env_len_dev int32[N]; env i with env_len[i] > 0 reads its
+ * first env_len[i] samples of the fw_set_noise buffer (column i, wrapped as above; env_len[i] <= the
+ * buffer's len), env_len[i] == 0 draws from Philox.  The VecEnv auto-reset of fw_env_step /
+ * fw_env_rollout zeroes env_len[i] (the SubprocVecEnv worker resets without turbulence_noise, so
+ * Dryden.reset(None) draws fresh noise); fw_reset leaves it to the caller.  NULL: every env reads the
+ * buffer (fw_set_noise alone).                                                                      */
+int fw_set_noise_lengths(fw_handle* h, int32_t* env_len_dev);
 
 /* Masked reset.  mask_dev: uint8[N] (NULL = all).  init_dev: [FW_NINIT][N] or
  * NULL (all sampled).  target_dev: [3][N] or NULL.  obs_dev: [N][n_obs] or NULL. */
@@ -338,6 +349,9 @@ int fw_env_rollout(fw_handle* h, int32_t n_steps, const void* actions_dev, void*
 #define FW_LANES_AUTO 0
 int fw_set_lanes(fw_handle* h, int32_t lanes);
 int fw_get_lanes(const fw_handle* h, int32_t* lanes);
+/* The automatic rule's threshold: FW_LANES_AUTO runs quads for N <= this (the build's FW_QUAD_AUTO_MAX).
+ * A sharded VecEnv applies the same rule to the global batch so every shard runs one integrator. */
+int64_t fw_quad_auto_max(void);
 
 /* Observation of the current state (FixedWingAircraft.get_observation). */
 int fw_observe(fw_handle* h, void* obs_dev, void* stream);

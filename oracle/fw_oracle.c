@@ -432,11 +432,14 @@ void orc_turbulence(const fw_sim_config* c, const double* noise, int64_t len, in
   if (!c->turbulence) return;
   int64_t L = c->turb_len;
   if (k % L == 0) return;
-  if (k >= len) return;
+  if (len < 1) return;
+  /* a sequence shorter than the episode wraps: simulate() reads noise[:, (t_span[0] + j) % len] in every
+   * branch of dryden.py:209-236 (slice, modulo start, concatenation, np.pad(mode="wrap")) */
+  const int64_t km1 = (k - 1) % len, k0 = k % len;
   double s = sqrt(PI_ / (double)L);
   static const int chan[6] = {0, 1, 2, 3, 1, 2}; /* dryden.py:238-252 */
   for (int f = 0; f < 6; f++) {
-    double um1 = s * noise[chan[f] * len + k - 1], u0 = s * noise[chan[f] * len + k];
+    double um1 = s * noise[chan[f] * len + km1], u0 = s * noise[chan[f] * len + k0];
     turb[f] = c->dryden_g0[f] * um1 + c->dryden_g1[f] * u0;
   }
 }

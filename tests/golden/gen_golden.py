@@ -18,6 +18,7 @@ Fixtures (all float64 unless noted):
   pyfly_single_step.npz   teacher-forced single PyFly.step cases (turbulence off/on)
   pyfly_traj.npz          free-running PyFly trajectories (PID + random commands)
   dryden.npz              Dryden FIR coefficients + raw filter outputs
+  dryden_wrap.npz         Dryden outputs for a turbulence_noise sequence shorter than the span (wraps)
   env_seq.npz             FixedWingAircraft reset/step sequences (obs, reward, done, term)
   env_pid_set.npz         PID replay of a synthetic 40-scenario evaluation set
   env_metrics.npz         episode metrics + histories for metric scenarios
@@ -506,6 +507,25 @@ def gen_dryden():
             out["L%d_%s__vel_ang" % (L, inten)] = dm.vel_ang[:, keep]
     np.savez_compressed(os.path.join(OUT, "dryden.npz"), **out)
     print("dryden done")
+
+
+def gen_dryden_wrap():
+    """A turbulence_noise sequence SHORTER than the simulated span (DrydenGustModel.simulate wraps it,
+    dryden.py:209-236): lengths 170 (wraps inside chunk 1 and again in chunk 2) and 450 (inside chunk 2)."""
+    out = {}
+    rng = np.random.RandomState(11)
+    L = 300
+    for n in (170, 450):
+        dm = DrydenGustModel(L, 0.01, 2.1, intensity="moderate")
+        noise = rng.standard_normal((4, n))
+        dm.reset(noise)
+        dm.simulate(L)
+        dm.simulate(L)
+        out["n%d__noise" % n] = noise
+        out["n%d__vel_lin" % n] = dm.vel_lin
+        out["n%d__vel_ang" % n] = dm.vel_ang
+    np.savez_compressed(os.path.join(OUT, "dryden_wrap.npz"), **out)
+    print("dryden_wrap done")
 
 
 # ---------------------------------------------------------------------------
@@ -1028,7 +1048,7 @@ def gen_history():
     np.savez_compressed(os.path.join(OUT, "env_history.npz"), **out)
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["single", "traj", "envelope", "dryden", "env", "pidset", "metrics", "obshist",
+    which = sys.argv[1:] or ["single", "traj", "envelope", "dryden", "dryden_wrap", "env", "pidset", "metrics", "obshist",
                              "solverfail", "energy", "curriculum", "randparams", "history"]
     if "envelope" in which and "traj" not in which:
         gen_envelope()
@@ -1042,6 +1062,8 @@ if __name__ == "__main__":
             gen_envelope()
     if "dryden" in which:
         gen_dryden()
+    if "dryden_wrap" in which:
+        gen_dryden_wrap()
     if "env" in which:
         gen_env_seq()
     if "pidset" in which:

@@ -23,7 +23,7 @@ HEADERS = [os.path.join(ROOT, "include", h) for h in ("fwsim.h", "fwrollout.h")]
 def _declared():
     names = set()
     for h in HEADERS:
-        names |= set(re.findall(r"^(?:int|size_t)\s+(fw_\w+)\s*\(", open(h).read(), re.M))
+        names |= set(re.findall(r"^(?:int|int64_t|size_t)\s+(fw_\w+)\s*\(", open(h).read(), re.M))
     return sorted(names)
 
 

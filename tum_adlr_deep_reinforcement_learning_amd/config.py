@@ -351,7 +351,7 @@ class SimSpec:
     def __init__(self, cfg, params):
         self.cfg = cfg
         self.params = params
-        # RHS-evaluation budget of one RK45 step (fw_sim_config.max_nfev; 0 = the library default 1000000, a safety net: scipy has none).
+        # RHS-evaluation budget of one RK45 step (fw_sim_config.max_nfev; 0 = the library default 65535, a safety net: scipy has none).
         # scipy has none; exhausting it is handled like solve_ivp's TOO_SMALL_STEP failure.
         self.max_nfev = 0
         self.vars = {}

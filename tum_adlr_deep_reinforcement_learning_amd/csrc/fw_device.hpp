@@ -37,8 +37,10 @@ int set_error(int code, const std::string& msg);
 constexpr int NY = FW_NY;
 constexpr double PI_D = 3.141592653589793;
 // default RHS-evaluation budget per step (fw_sim_config.max_nfev): a safety net only -- scipy has no
-// budget, and the steady-state bench population never comes near it (profiles/r03_nfev_census.json)
-constexpr int MAX_NFEV = 1000000;
+// budget, and the steady-state bench population never comes near it (profiles/r03_nfev_census.json:
+// maximum 6686 in 2.6e8 aircraft-steps).  65535 = the largest count the stats word reports, so a
+// saturated nfev field and a budget hit coincide; it bounds one launch at ~30 ms of lone-aircraft work.
+constexpr int MAX_NFEV = 65535;
 constexpr uint32_t DM_SOLVER_FAIL = 1u << 31;  // sim_step_masked dmask bit: RK45 failed, last accepted sub-step kept
 constexpr uint32_t DM_BUDGET = 1u << 30;       // ... and the failure was the max_nfev budget (not TOO_SMALL_STEP)
 

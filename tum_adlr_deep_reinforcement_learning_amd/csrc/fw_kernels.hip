@@ -101,6 +101,7 @@ struct State {
   uint32_t* episode;  // [ld]
   const T* noise;     // injected N(0,1) turbulence noise [4][noise_len][ld] or null
   int64_t noise_len;
+  int32_t* noise_env_len;  // [ld] per-env injected length (0: Philox; zeroed by the auto-reset) or null: all
   uint32_t key0, key1;  // Philox key = seed
   uint32_t env_offset;
   T* met;             // [MT_ROWS][ld] streaming episode-metric sums (null: metrics off)
@@ -149,17 +150,19 @@ __device__ __forceinline__ void st_(T* p, int64_t row, int64_t ld, int64_t i, T 
   p[row * ld + i] = v;
 }
 
-// N(0,1) turbulence noise sample (4 channels) of step index k of the current episode
+// N(0,1) turbulence noise sample (4 channels) of step index k of the current episode.  Injected noise
+// shorter than the episode wraps: DrydenGustModel.simulate reads noise[:, (t_span[0] + j) % len] in every
+// branch of dryden.py:209-236 (slice, modulo start, concatenation, np.pad(mode="wrap")).
 template <typename T>
 __device__ __forceinline__ void noise4(const State<T>& s, int64_t i, uint32_t episode, int k, T u[4]) {
   if (s.noise) {
-    if (k < s.noise_len) {
+    const int64_t len = s.noise_env_len ? (int64_t)s.noise_env_len[i] : s.noise_len;
+    if (len > 0) {
+      const int64_t kk = (int64_t)((uint32_t)k % (uint32_t)len);  // len < 2^31 (fw_set_noise)
 #pragma unroll
-      for (int ch = 0; ch < 4; ch++) u[ch] = s.noise[((int64_t)ch * s.noise_len + k) * s.ld + i];
-    } else {
-      u[0] = u[1] = u[2] = u[3] = T(0);
+      for (int ch = 0; ch < 4; ch++) u[ch] = s.noise[((int64_t)ch * s.noise_len + kk) * s.ld + i];
+      return;
     }
-    return;
   }
   uint32_t r[4];
   philox(s.key0, s.key1, s.env_offset + (uint32_t)i, episode, 1u, (uint32_t)k, r);
@@ -1037,6 +1040,8 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   if (__ballot(do_reset)) {
     if (do_reset) {
       T yr[NY], dr[8], wr[3], tr[3];
+      // the worker's env.reset() passes no turbulence_noise: Dryden.reset(None) (dryden.py:184-188)
+      if (s.noise_env_len) s.noise_env_len[i] = 0;
       reset_lane(c, s, i, (const T*)nullptr, (const T*)nullptr, yr, dr, wr, tr);
       store_env_fresh(c, s, i, yr, dr, wr, tr);
 #ifndef FW_MET_SKIP_INIT
@@ -1179,6 +1184,7 @@ struct fw_handle {
   int64_t env_offset = 0;
   const void* noise = nullptr;
   int64_t noise_len = 0;
+  int32_t* noise_env_len = nullptr;
   int spec = 0;  // 0 = generic DevCfg kernels, 1 = GymX8Cfg, 2 = PyflyX8Cfg (structure matched at upload)
   int metrics = 0;          // streaming episode-metric state allocated (env->metrics at create)
   void* met_out = nullptr;  // [FW_NMETRIC][N] done-episode records (fw_set_metrics_output)
@@ -1534,6 +1540,7 @@ State<T> state_of(const fw_handle* h) {
   s.episode = (uint32_t*)(b + h->o_episode);
   s.noise = (const T*)h->noise;
   s.noise_len = h->noise_len;
+  s.noise_env_len = h->noise_env_len;
   s.key0 = (uint32_t)(h->seed & 0xFFFFFFFFu);
   s.key1 = (uint32_t)(h->seed >> 32);
   s.env_offset = (uint32_t)h->env_offset;
@@ -1739,8 +1746,17 @@ int fw_seed(fw_handle* h, uint64_t seed, int64_t env_offset) {
 int fw_set_noise(fw_handle* h, const void* noise_dev, int64_t len) {
   if (!h) return set_err(FW_E_INVALID, "NULL handle");
   if (noise_dev && len < 1) return set_err(FW_E_INVALID, "noise length must be >= 1");
+  if (len > INT32_MAX) return set_err(FW_E_INVALID, "noise length must be < 2^31");
   h->noise = noise_dev;
   h->noise_len = noise_dev ? len : 0;
+  if (!noise_dev) h->noise_env_len = nullptr;
+  return FW_OK;
+}
+
+int fw_set_noise_lengths(fw_handle* h, int32_t* env_len_dev) {
+  if (!h) return set_err(FW_E_INVALID, "NULL handle");
+  if (env_len_dev && !h->noise) return set_err(FW_E_INVALID, "fw_set_noise_lengths: set the noise buffer first");
+  h->noise_env_len = env_len_dev;
   return FW_OK;
 }
 
@@ -1859,6 +1875,8 @@ int fw_get_lanes(const fw_handle* h, int32_t* lanes) {
   *lanes = lanes_of(h);
   return FW_OK;
 }
+
+int64_t fw_quad_auto_max(void) { return FW_QUAD_AUTO_MAX; }
 
 int fw_set_metrics_output(fw_handle* h, void* metrics_dev) {
   if (!h) return set_err(FW_E_INVALID, "NULL handle");

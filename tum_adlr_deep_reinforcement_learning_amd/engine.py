@@ -112,7 +112,9 @@ class Engine:
         self.config_version += 1
 
     def set_noise(self, noise):
-        """Inject N(0,1) turbulence noise, array-like [n][4][len] or [4][len] (shared), or None."""
+        """Inject N(0,1) turbulence noise for every env, array-like [n][4][len] or [4][len] (shared), or None.
+        Step k of an episode reads sample k mod len (dryden.py:209-236)."""
+        self._env_len = None
         if noise is None:
             self._noise = None
             _native.check(self.lib.fw_set_noise(self.h, None, 0), "fw_set_noise")
@@ -128,6 +130,36 @@ class Engine:
         buf[:, :, :self.n] = a.permute(1, 2, 0).to(self.device)
         self._noise = buf
         _native.check(self.lib.fw_set_noise(self.h, _ptr(buf), L), "fw_set_noise")
+
+    def set_env_noise(self, indices, noise):
+        """Per-env injection (PyFly.reset(turbulence_noise=...) of the envs in ``indices``, pyfly.py:1262):
+        ``noise`` [4][len] N(0,1) samples for all of them, or None = those envs draw from Philox again.
+        The other envs keep what they had; an env's injection ends at its next VecEnv auto-reset
+        (fw_set_noise_lengths).  Applies to the envs' next reset (call before ``reset(mask=...)``)."""
+        idx = torch.as_tensor(np.asarray(list(indices), dtype=np.int64))
+        if getattr(self, "_env_len", None) is None:
+            if noise is None:
+                return
+            self._env_len = torch.zeros(self.n, dtype=torch.int32, device=self.device)
+            self._noise = torch.zeros(4, 1, (self.n + 63) // 64 * 64, dtype=self.dtype, device=self.device)
+        if noise is None:
+            self._env_len[idx.to(self.device)] = 0
+        else:
+            a = torch.as_tensor(np.asarray(noise), dtype=self.dtype)
+            if a.dim() != 2 or a.shape[0] != 4 or a.shape[1] < 1:
+                raise ValueError("turbulence_noise must be [4][len] with len >= 1")
+            L = a.shape[1]
+            if L > self._noise.shape[1]:  # grow the buffer, keeping the other envs' samples
+                grown = torch.zeros(4, L, self._noise.shape[2], dtype=self.dtype, device=self.device)
+                grown[:, :self._noise.shape[1]] = self._noise
+                self._noise = grown
+            cols = idx.to(self.device)
+            self._noise[:, :L, cols] = a.to(self.device)[:, :, None]
+            self._env_len[cols] = L
+        torch.cuda.current_stream(self.device).synchronize()  # host -> device copies of the pageable input
+        _native.check(self.lib.fw_set_noise(self.h, _ptr(self._noise), self._noise.shape[1]), "fw_set_noise")
+        _native.check(self.lib.fw_set_noise_lengths(self.h, _ptr(self._env_len)), "fw_set_noise_lengths")
+        self.config_version += 1
 
     # ------------------------------------------------------------------
     def reset(self, mask=None, init=None, target=None, want_obs=True):

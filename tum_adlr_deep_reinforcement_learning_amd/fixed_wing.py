@@ -71,8 +71,7 @@ class FixedWingAircraft:
 
     def reset(self, state=None, target=None, turbulence_noise=None):
         """FixedWingAircraft.reset (fixed_wing.py:414-481)."""
-        if turbulence_noise is not None:
-            self.engine.set_noise(turbulence_noise)
+        self.engine.set_noise(turbulence_noise)  # Dryden.reset(noise): None draws fresh noise (dryden.py:174-188)
         init = C.init_array(state, 1, self.spec.sim) if state is not None else None
         tgt = None
         if target is not None:

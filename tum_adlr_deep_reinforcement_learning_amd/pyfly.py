@@ -119,8 +119,7 @@ class PyFly(SimulatorView):
     def reset(self, state=None, turbulence_noise=None):
         """PyFly.reset (pyfly.py:1262-1311).  ``state`` is the reference's dict (NaN / missing = sample)."""
         n = self.engine.n
-        if turbulence_noise is not None:
-            self.engine.set_noise(turbulence_noise)
+        self.engine.set_noise(turbulence_noise)  # Dryden.reset(noise): None draws fresh noise (dryden.py:174-188)
         init = C.init_array(state, n, self.engine.sim_spec) if state is not None else None
         self.engine.reset(init=init, want_obs=False)
 

@@ -357,8 +357,14 @@ class RolloutCollector:
         return hasattr(self.env, "step_exchange") and dist.is_available() and dist.is_initialized()
 
     def graph_key(self):
+        """Everything a captured step bakes in: the env's host-side choices, the split around the collective,
+        the buffer, and the policy -- which module, where its parameters live (the launch reads them in
+        place, so optimiser steps are seen but a replaced tensor is not), whether it explores."""
         env_key = self.env.graph_key() if hasattr(self.env, "graph_key") else None
-        return (env_key, self._split(), self.buffer.slab.data_ptr(), self.buffer.buffer_size)
+        pol = self.policy
+        pol_key = (id(pol), bool(getattr(pol, "deterministic_rollout", False)),
+                   tuple(p.data_ptr() for p in pol.parameters()) if isinstance(pol, nn.Module) else None)
+        return (env_key, self._split(), self.buffer.slab.data_ptr(), self.buffer.buffer_size, pol_key)
 
     def _capture(self):
         """Capture one collect step on static tensors: s_obs (the observation the policy acts on, then

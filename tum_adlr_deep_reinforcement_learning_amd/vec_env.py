@@ -65,7 +65,10 @@ class VecEnv(_SB3VecEnv if _SB3VecEnv is not None else object):
         return indices
 
 
-QUAD_AUTO_MAX = 16384  # fw_kernels.hip FW_QUAD_AUTO_MAX: the automatic choice runs quads up to this shard size
+def quad_auto_max():
+    """The library's automatic-rule threshold (fw_quad_auto_max: the build's FW_QUAD_AUTO_MAX)."""
+    from . import _native
+    return int(_native.load().fw_quad_auto_max())
 
 
 def auto_lanes(global_envs, world_size=None):
@@ -76,7 +79,7 @@ def auto_lanes(global_envs, world_size=None):
         import torch.distributed as dist
         world_size = dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
     largest = -(-int(global_envs) // int(world_size))
-    return 4 if largest <= QUAD_AUTO_MAX else 1
+    return 4 if largest <= quad_auto_max() else 1
 
 
 def termination_name(code, dynamics=("elevon_right", "elevon_left", "throttle")):
@@ -358,9 +361,36 @@ class FixedWingVecEnv(VecEnv):
         raise AttributeError("FixedWingVecEnv has no per-env attribute %r" % attr_name)
 
     def set_attr(self, attr_name, value, indices=None):
+        """SubprocVecEnv.set_attr (subproc_vec_env.py:156-161: ``setattr(env, name, value)`` on each chosen
+        worker's FixedWingAircraft).  Settable here: ``training`` (the reference's callbacks,
+        train_rl_controller.py:320), ``target`` (a {"roll", "pitch", "Va"} dict, partial allowed: the
+        chosen envs track it from their next step), ``steps_count`` (their step counter) and ``steps_max``
+        (the episode limit of every env: one device configuration, so ``indices`` must cover all envs;
+        like the reference, the turbulence sequence length fixed at construction does not change)."""
+        idx = list(self._get_indices(indices))
         if attr_name == "training":
             self.training = value
             return
+        if attr_name == "target":
+            t = self.engine.get_block(C.FW_BLK_TARGET)
+            for k, v in dict(value).items():
+                t[C.TARGET_INDEX[k], idx] = float(v)
+            self.engine.set_block(C.FW_BLK_TARGET, t)
+            return
+        if attr_name == "steps_count":
+            sw = self.engine.get_block(C.FW_BLK_STEPS)
+            keep = sw[0, idx] & ~0xFFFF
+            sw[0, idx] = keep | (int(value) & 0xFFFF)
+            self.engine.set_block(C.FW_BLK_STEPS, sw)
+            return
+        if attr_name == "steps_max":
+            if sorted(set(i % self.num_envs for i in idx)) != list(range(self.num_envs)):
+                raise NotImplementedError("steps_max is one device configuration: set it for all envs (indices=None)")
+            self.spec.steps_max = int(value)
+            self.engine.update_config(self.spec.sim, self.spec)
+            return
+        if attr_name in ("render_on_reset", "save_on_reset"):
+            raise NotImplementedError("%s is host-side plotting; out of scope for the device engine" % attr_name)
         raise AttributeError("setting %r is not supported on the device env" % attr_name)
 
     def env_method(self, method_name, *method_args, indices=None, **method_kwargs):
@@ -399,10 +429,10 @@ class FixedWingVecEnv(VecEnv):
             for i in idx:
                 for k, v in target.items():
                     tgt[C.TARGET_INDEX[k], i] = v
-        if turbulence_noise is not None:
-            if len(idx) != n:
-                raise NotImplementedError("turbulence_noise for a subset of the envs")
-            self.engine.set_noise(turbulence_noise)
+        # FixedWingAircraft.reset(**sim_reset_kw) -> PyFly.reset(turbulence_noise=...) -> Dryden.reset(noise)
+        # (fixed_wing.py:441, pyfly.py:1294, dryden.py:174-188): these envs' episodes read the given noise,
+        # and a reset without it draws fresh noise again
+        self.engine.set_env_noise(idx, turbulence_noise)
         obs = self.engine.reset(mask=mask, init=init, target=tgt)
         o = self._shaped(obs.cpu().numpy().astype(np.float32))
         return [o[i] for i in idx]

@@ -83,12 +83,8 @@ class VecNormalize:
         self._ws = torch.empty(int(self.lib.fw_moments_workspace_bytes(n, d)), dtype=torch.uint8, device=dev)
         self._rec = torch.empty(1 + 2 * (d + 1), dtype=torch.float64, device=dev)
         self._rec_ret = torch.empty(3, dtype=torch.float64, device=dev)
-        # rank-ordered records of the global batch, at fixed addresses (a captured collect step reads them)
-        W = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
-        self._parts = torch.empty(W, self._rec.numel(), dtype=torch.float64, device=dev)
-        self._parts_ret = torch.empty(W, 3, dtype=torch.float64, device=dev)
-        if W == 1:  # the record is written where update_from_moments reads it (no copy per step)
-            self._rec = self._parts[0]
+        self._parts = None
+        self._ensure_parts()
         self._zero_rew = torch.zeros(n, dtype=torch.float32, device=dev)
         self.obs_out = torch.empty(n, d, dtype=torch.float32, device=dev)
         self.rew_out = torch.empty(n, dtype=torch.float32, device=dev)
@@ -98,6 +94,24 @@ class VecNormalize:
         self.ret_rms = _RMSView(self, "ret")
 
     # --------------------------------------------------------------- internals
+    def _world(self):
+        return dist.get_world_size(self.group) if (dist.is_available() and dist.is_initialized()) else 1
+
+    def _ensure_parts(self):
+        """Rank-ordered records of the global batch, at fixed addresses (a captured collect step reads them),
+        sized for the current process group: a wrapper built before init_process_group is re-sized on first
+        use under the group (graph_key carries the world size, so a captured step is recaptured)."""
+        W = self._world()
+        grouped = dist.is_available() and dist.is_initialized()
+        if self._parts is not None and (self._parts.shape[0] == W or not grouped):
+            return  # (without a group a caller may stack records itself, as the configs[3] emulation does)
+        dev = self.device
+        n_rec = 1 + 2 * (self.obs_dim + 1)
+        self._parts = torch.empty(W, n_rec, dtype=torch.float64, device=dev)
+        self._parts_ret = torch.empty(W, 3, dtype=torch.float64, device=dev)
+        # W == 1: the record is written where update_from_moments reads it (no copy per step)
+        self._rec = self._parts[0] if W == 1 else torch.empty(n_rec, dtype=torch.float64, device=dev)
+
     def _s(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
@@ -126,6 +140,7 @@ class VecNormalize:
         d, n = self.obs_dim, self.num_envs
         L = self.lib
         s = self._s()
+        self._ensure_parts()
         if obs is not None:
             self._moments(obs, rew)
             self._gather(self._rec)
@@ -186,6 +201,7 @@ class VecNormalize:
         obs = obs.to(torch.float32).contiguous()
         rews = rews.to(torch.float32).contiguous()
         self.old_obs, self.old_reward = obs, rews
+        self._ensure_parts()
         u8 = news.view(torch.uint8) if (news.dtype == torch.bool and news.is_contiguous()) else news.to(torch.uint8)
         self._news, self._infos, self._done_u8 = news, infos, u8.contiguous()
         if self.training:
@@ -209,7 +225,7 @@ class VecNormalize:
         """Host-side choices a captured step bakes in (RolloutCollector recaptures when this changes)."""
         inner = self.venv.graph_key() if hasattr(self.venv, "graph_key") else None
         return (self.training, self.norm_obs, self.norm_reward, self.clip_obs, self.clip_reward, self.gamma,
-                self.epsilon, inner)
+                self.epsilon, self._world(), inner)
 
     def step(self, actions):
         self.step_async(actions)
