@@ -167,8 +167,9 @@ def rollout_leg(spec, n, T, dev, rank, world, precision):
     policy = MlpActorCritic(env.observation_space.shape[0], env.action_space.shape[0]).to(dev)
     buf = RolloutBuffer(T, env.observation_space, env.action_space, device=dev, gae_lambda=0.95, gamma=0.99, n_envs=n)
     col = RolloutCollector(env, policy, buf)
-    # the collect step is replayed from HIP graphs (RolloutCollector.collect(graph=True)): one graph per step
-    # on one GPU; on N > 1 two graphs around the per-step RCCL all-gather of the VecNormalize moments
+    # the collect step is replayed from ONE HIP graph per step (RolloutCollector.collect(graph=True), the fused
+    # step: fw_collect_policy, fw_env_step + its VecNormalize epilogue, the statistics update; on N > 1 the
+    # per-step RCCL all-gather of the moment records is captured inside the same graph)
     graph = True
     col.collect(min(T, 16))  # warm-up (kernels, allocator, RCCL communicator)
     col.collect(min(T, 16), graph=True)  # captures the step graph(s)
@@ -194,7 +195,9 @@ def rollout_leg(spec, n, T, dev, rank, world, precision):
     collect_s, gather_s, total_s, gae_ms = [float(x) for x in t]
     gae_bytes = (4 + 4 + 1 + 4 + 4) * T * n + (4 + 1) * n
     out = {"horizon": T, "envs_per_gpu": n, "global_envs": n * world, "collect_graphed": graph,
-           "host_launches_per_step": len(col._graphs) + (1 if len(col._graphs) > 1 else 0), "collect_s": collect_s,
+           "host_launches_per_step": col.host_launches_per_step(), "fused_step": bool(getattr(col, "_fused_graph", False)),
+           "graph_kernel_nodes": [t.count(0) for t in col.graph_nodes()] if getattr(col, "_fused_graph", False) else None,
+           "collect_s": collect_s,
            "allgather_s": gather_s if world > 1 else 0.0, "env_steps_per_s": n * world * T / total_s,
            "gathered_bytes_per_gpu": sum(s.numel() * 4 for s in gathered.slabs),
            "gae_kernel": {"ms": gae_ms, "bytes": gae_bytes, "achieved_GBs": gae_bytes / (gae_ms * 1e-3) / 1e9,

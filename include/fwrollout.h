@@ -122,6 +122,46 @@ typedef struct fw_mlp_policy {
 int fw_policy_forward(const fw_mlp_policy* p, const float* obs, int64_t n, const float* noise, const float* low,
                       const float* high, float* actions, float* clipped, float* values, float* log_probs, void* stream);
 
+/* Two-pass merge of n_records moment records (1 + 2D doubles each: n_b, mean_b[D], M2_b[D], e.g. the
+ * per-block records of fw_env_step's collect epilogue, fwsim.h fw_set_collect_epilogue) into one record
+ * `out` of the same layout: mean = sum n_b mean_b / N, M2 = sum (M2_b + n_b (mean_b - mean)^2), every sum in
+ * a fixed order.  The batch moments of RunningMeanStd.update (running_mean_std.py:20-24). */
+int fw_moments_merge(const double* records, int32_t n_records, int32_t D, double* out, void* stream);
+
+/* fw_moments_merge of the records (obs columns d, plus the return column when has_ret) followed by
+ * fw_rms_update of that single record, in ONE launch (the unsharded VecNormalize statistics update,
+ * vec_normalize.py:106-131 -> running_mean_std.py:20-40): bit-identical to the two calls.  rec_out (may be
+ * NULL) receives the merged record. */
+int fw_vecnorm_merge_update(const double* records, int32_t n_records, int32_t d, int32_t has_ret, double* rms,
+                            double* rec_out, void* stream);
+
+/* One PPO collect step's policy side, fused (OnPolicyAlgorithm.collect_rollouts,
+ * on_policy_algorithm.py:140-176 for the default MlpPolicy): reads the env's RAW step output, normalises the
+ * observation with VecNormalize's current statistics (vec_normalize.py:148-159), runs the policy (as
+ * fw_policy_forward), and stores the rollout rows (RolloutBuffer.add, buffers.py:335-361) at row t = ctrl[0]:
+ *   obs_rows[t] = normalised obs, act_rows[t], val_rows[t], logp_rows[t];  the clipped actions -> `clipped`
+ *   (the env's next action input); when t >= 1 also rew_rows[t-1] = the normalised reward of the previous
+ *   step (vec_normalize.py:161-169) and start_rows[t] = that step's done flags (the next episode start).
+ * rms NULL: observation and reward taken raw (no VecNormalize).  The row index advances elsewhere (the env
+ * step's collect epilogue), so a captured graph of {this, fw_env_step, ...} fills row t at its t-th replay.
+ * Noise (NULL = deterministic): [T][n][A], row t read.  Limits as fw_policy_forward; float32. */
+typedef struct fw_collect_io {
+  const float* obs;         /* [n][d] raw observation of the previous env step */
+  const float* reward;      /* [n] raw reward of the previous env step */
+  const uint8_t* done;      /* [n] done flags of the previous env step */
+  const double* rms;        /* fwrollout.h rms layout, or NULL */
+  double epsilon, clip_obs, clip_reward;
+  int32_t norm_obs, norm_reward;
+  const float* noise;       /* [T][n][A] or NULL */
+  const float *low, *high;  /* action space bounds [A] */
+  float* clipped;           /* [n][A] */
+  const int32_t* ctrl;      /* device {t, n_rows} */
+  float *obs_rows, *act_rows, *val_rows, *logp_rows, *rew_rows;
+  uint8_t* start_rows;
+  int64_t n;
+} fw_collect_io;
+int fw_collect_policy(const fw_mlp_policy* p, const fw_collect_io* io, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

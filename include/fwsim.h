@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FWSIM_ABI_VERSION 7
+#define FWSIM_ABI_VERSION 8
 
 /* ---- error codes ---------------------------------------------------------- */
 #define FW_OK 0
@@ -370,6 +370,30 @@ int fw_update_config(fw_handle* h, const fw_sim_config* sim, const fw_env_config
  * metrics of FixedWingAircraft.get_metric, fixed_wing.py:1644-1736, which the reference puts in
  * info on done).  NULL stops the writes.  Requires env->metrics at create time. */
 int fw_set_metrics_output(fw_handle* h, void* metrics_dev);
+
+/* The env-side half of VecNormalize.step_wait (stable_baselines3/common/vec_env/vec_normalize.py:106-131),
+ * run by fw_env_step's own epilogue while the step's observation is on chip, so a PPO collect step needs
+ * no separate statistics pass over the observations (running_mean_std.py:20-24 RunningMeanStd.update's
+ * batch moments):
+ *   ret      [N] fp64 discounted return: ret = ret * gamma + reward (VecNormalize._update_reward,
+ *            vec_normalize.py:126-129), then ret[done] = 0 (vec_normalize.py:130) -- or NULL (no return column)
+ *   records  fp64 [fw_collect_records(h)][1 + 2 * (n_obs_values + (ret != NULL))]: one exact two-pass
+ *            moment record per launch block (n_b, mean_b[D], M2_b[D]) of the float32 observation (the VecEnv
+ *            output: the reset observation of an auto-reset env) and of ret before its reset -- or NULL.
+ *            Merge with fw_moments_merge / fw_vecnorm_merge_update (fwrollout.h).
+ *   row_ctrl optional device int32: the launch does row_ctrl[0] += 1 after every block read its inputs
+ *            (the rollout row of a captured collect step, fw_collect_policy in fwrollout.h).
+ * Applies to fw_env_step only (not fw_env_rollout); NULL (or all fields NULL) turns it off. */
+typedef struct fw_collect_epilogue {
+  double* ret;
+  double gamma;
+  double* records;
+  int32_t* row_ctrl;
+} fw_collect_epilogue;
+int fw_set_collect_epilogue(fw_handle* h, const fw_collect_epilogue* epi);
+/* Records the next fw_env_step writes (its block count: depends on N and fw_get_lanes) and the most any
+ * lanes setting can write (size the buffer with that). */
+int fw_collect_records(const fw_handle* h, int64_t* n_records, int64_t* max_records);
 
 #ifdef __cplusplus
 }

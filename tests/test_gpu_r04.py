@@ -180,3 +180,198 @@ def test_graph_recaptured_when_policy_changes():
             buf.actions.shape)
     assert torch.allclose(buf.actions, mean2, rtol=1e-5, atol=1e-6)
     venv.close()
+
+
+# ---------------------------------------------------------------------------- fused collect step (round 4)
+def _P(t):
+    import ctypes
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+@pytest.mark.parametrize("n,lanes", [(1000, 4), (20037, 1)])
+def test_collect_epilogue_records_and_return_vs_numpy(n, lanes):
+    """fw_env_step's collect epilogue (fw_set_collect_epilogue): the block records merged by fw_moments_merge
+    equal numpy's mean / var of the step's float32 observation and of ret*gamma + reward (fp64, rel 1e-12);
+    ret after the step = that value, 0 where done (bit for bit, multiply and add unfused as numpy); the row
+    counter advances by one per launch; one record per launch block of the lanes setting."""
+    from tum_adlr_deep_reinforcement_learning_amd import _native
+    from tum_adlr_deep_reinforcement_learning_amd.vec_env import FixedWingVecEnv
+    lib = _native.load()
+    venv = FixedWingVecEnv(n, config_kw={"steps_max": 12}, sim_config_kw={"turbulence": False}, device=DEV, seed=9,
+                           return_tensors=True, info_target=False, lanes=lanes)
+    eng = venv.engine
+    venv.reset()
+    D = eng.n_obs_values + 1
+    nrec, nmax = eng.collect_records()
+    assert nrec == -(-n * lanes // 64) and nmax == -(-n * 4 // 64)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(n)
+    ret = torch.randn(n, generator=g, device=DEV, dtype=torch.float64)
+    rec = torch.full((nmax * (1 + 2 * D),), float("nan"), dtype=torch.float64, device=DEV)
+    ctrl = torch.zeros(2, dtype=torch.int32, device=DEV)
+    out = torch.empty(1 + 2 * D, dtype=torch.float64, device=DEV)
+    gamma = 0.99
+    for k in range(15):  # episodes end at step 12: done envs reset inside the window
+        a = torch.rand(n, 3, generator=g, device=DEV) * 2 - 1
+        ret0 = ret.clone()
+        eng.set_collect_epilogue(ret=ret, gamma=gamma, records=rec, row_ctrl=ctrl)
+        obs, rew, done, _ = eng.env_step(a)
+        eng.set_collect_epilogue()
+        _native.check(lib.fw_moments_merge(_P(rec), nrec, D, _P(out), None), "fw_moments_merge")
+        torch.cuda.synchronize()
+        r_new = ret0.cpu().numpy() * gamma + rew.cpu().numpy().astype(np.float32).astype(np.float64)
+        dn = done.cpu().numpy().astype(bool)
+        np.testing.assert_array_equal(ret.cpu().numpy(), np.where(dn, 0.0, r_new))
+        xs = np.concatenate([obs.cpu().numpy().astype(np.float32).astype(np.float64), r_new[:, None]], 1)
+        o = out.cpu().numpy()
+        assert o[0] == n
+        np.testing.assert_allclose(o[1:D + 1], xs.mean(0), rtol=1e-12, atol=1e-13)
+        np.testing.assert_allclose(o[D + 1:] / n, xs.var(0), rtol=1e-12, atol=1e-13)
+        assert int(ctrl[0]) == k + 1
+    assert dn.any() or k < 12
+    venv.close()
+
+
+def test_merge_update_equals_merge_then_update():
+    """fw_vecnorm_merge_update (one launch) == fw_moments_merge + fw_rms_update of the merged record, bit for
+    bit (the same device functions), over records of uneven block sizes."""
+    from tum_adlr_deep_reinforcement_learning_amd import _native
+    lib = _native.load()
+    d, nrec = 14, 1029
+    D = d + 1
+    g = torch.Generator(device=DEV)
+    g.manual_seed(7)
+    rec = torch.randn(nrec, 1 + 2 * D, generator=g, device=DEV, dtype=torch.float64)
+    rec[:, 0] = torch.randint(1, 65, (nrec,), generator=g, device=DEV).double()
+    rec[:, 1 + D:] = rec[:, 1 + D:].abs() * 10
+    rms0 = torch.rand(2 * d + 4, generator=g, device=DEV, dtype=torch.float64) + 0.5
+    a, b = rms0.clone(), rms0.clone()
+    out_a = torch.empty(1 + 2 * D, dtype=torch.float64, device=DEV)
+    out_b = torch.empty_like(out_a)
+    _native.check(lib.fw_vecnorm_merge_update(_P(rec), nrec, d, 1, _P(a), _P(out_a), None), "merge_update")
+    _native.check(lib.fw_moments_merge(_P(rec), nrec, D, _P(out_b), None), "merge")
+    _native.check(lib.fw_rms_update(_P(out_b), 1, d, 1, _P(b), 1, 1, None), "rms_update")
+    torch.cuda.synchronize()
+    assert torch.equal(out_a, out_b) and torch.equal(a, b) and not torch.equal(a, rms0)
+
+
+@pytest.mark.parametrize("d,A", [(14, 1), (20, 5), (9, 8)])
+def test_mfma_policy_forward_vs_torch_module(d, A):
+    """The matrix-core policy launch (v_mfma_f32_16x16x4_f32, fw_policy_forward) for action heads beyond
+    four rows (rows 4..7 come from the next lane group), one action, and observations wider than 16 (eight
+    k-steps) == the torch module within fp32 rounding (rel/abs 2e-5), ragged n."""
+    from tum_adlr_deep_reinforcement_learning_amd.rollout import MlpActorCritic
+    torch.manual_seed(d * 10 + A)
+    n = 3001
+    pol = MlpActorCritic(d, A).to(DEV)
+    with torch.no_grad():
+        for prm in pol.parameters():
+            prm.add_(0.3 * torch.randn_like(prm))
+    obs = 3 * torch.randn(n, d, device=DEV)
+    low = -0.7 * torch.ones(A, device=DEV)
+    high = 0.8 * torch.ones(A, device=DEV)
+    torch.manual_seed(11)
+    with torch.no_grad():
+        a_ref, v_ref, lp_ref = pol(obs)
+    torch.manual_seed(11)
+    a, c, v, lp = pol.collect_step(obs, low, high)
+    tol = dict(rtol=2e-5, atol=2e-5)
+    torch.testing.assert_close(a, a_ref, **tol)
+    torch.testing.assert_close(v, v_ref.reshape(-1), **tol)
+    torch.testing.assert_close(lp, lp_ref, **tol)
+    assert torch.equal(c, torch.max(torch.min(a, high), low))
+
+
+def _collect_setup(n, T, vecnorm=True, seed=21):
+    from tum_adlr_deep_reinforcement_learning_amd.rollout import MlpActorCritic, RolloutBuffer, RolloutCollector
+    from tum_adlr_deep_reinforcement_learning_amd.vec_env import FixedWingVecEnv
+    from tum_adlr_deep_reinforcement_learning_amd.vec_normalize import VecNormalize
+    torch.manual_seed(5)
+    venv = FixedWingVecEnv(n, config_kw={"steps_max": 30}, sim_config_kw={"turbulence": False}, device=DEV,
+                           seed=seed, return_tensors=True, info_target=False)
+    env = VecNormalize(venv) if vecnorm else venv
+    policy = MlpActorCritic(env.observation_space.shape[0], env.action_space.shape[0]).to(DEV)
+    buf = RolloutBuffer(T, env.observation_space, env.action_space, device=DEV, gae_lambda=0.95, gamma=0.99, n_envs=n)
+    return venv, env, buf, RolloutCollector(env, policy, buf)
+
+
+@pytest.mark.parametrize("vecnorm", [True, False])
+def test_fused_collect_step_launches_and_equals_eager(vecnorm):
+    """The fused graphed collect step is ONE graph of 3 kernels with VecNormalize (fw_collect_policy,
+    fw_env_step with its collect epilogue, fw_vecnorm_merge_update), 2 without; it stores the same rollout
+    as the eager collect bit for bit (slab, rewards, episode starts, last obs / dones, statistics, return)."""
+    from oracle import rollout_oracle as R
+    va, ea, ba, ca = _collect_setup(2048, 40, vecnorm)
+    vb, eb, bb, cb = _collect_setup(2048, 40, vecnorm)
+    for c in (ca, cb):
+        torch.manual_seed(40)
+        c.collect(8)
+    for i in range(2):
+        torch.manual_seed(41 + i)
+        ca.collect()
+        torch.manual_seed(41 + i)
+        cb.collect(graph=True)
+        assert cb._fused_graph
+        for f in ("slab", "rewards", "dones"):
+            assert torch.equal(getattr(ba, f), getattr(bb, f)), f
+        assert torch.equal(ca.last_obs, cb.last_obs) and torch.equal(ca.last_dones, cb.last_dones)
+        if vecnorm:
+            assert torch.equal(ea.rms, eb.rms) and torch.equal(ea.ret, eb.ret)
+    nodes = cb.graph_nodes()
+    assert len(nodes) == 1 and nodes[0].count(0) == (3 if vecnorm else 2), nodes
+    assert cb.host_launches_per_step() == 1
+    assert int(bb.dones.sum()) > 0 and float(bb.log_probs.abs().max()) > 0
+    with torch.no_grad():
+        lv = cb.policy.predict_values(cb.last_obs).reshape(-1).cpu().numpy()
+    a_ref, _ = R.gae(bb.rewards.cpu().numpy(), bb.values.cpu().numpy(), bb.dones.cpu().numpy(), lv,
+                     cb.last_dones.cpu().numpy(), 0.99, 0.95)
+    assert np.array_equal(bb.advantages.cpu().numpy(), a_ref)
+    va.close()
+    vb.close()
+
+
+def test_fused_collect_rccl_world1_single_graph():
+    """Under an nccl process group of size 1 the fused collect step captures the RCCL all-gather of the
+    moment records inside its one graph (1 host launch per step), and the collection equals the group-less
+    one and the eager one bit for bit."""
+    import socket
+    import torch.distributed as dist
+
+    def port():
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            return s.getsockname()[1]
+
+    runs = []
+    for grouped in (False, True):
+        if grouped:
+            dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port(), rank=0, world_size=1,
+                                    device_id=torch.device(DEV))
+        try:
+            va, ea, ba, ca = _collect_setup(4096, 32)
+            vb, eb, bb, cb = _collect_setup(4096, 32)
+            for c in (ca, cb):
+                torch.manual_seed(40)
+                c.collect(8)
+            snaps = []
+            for i in range(2):
+                torch.manual_seed(41 + i)
+                ca.collect()
+                torch.manual_seed(41 + i)
+                cb.collect(graph=True)
+                sa = [t.clone() for t in (ba.slab, ba.rewards, ba.dones, ca.last_obs, ca.last_dones, ea.rms, ea.ret)]
+                sb = [t.clone() for t in (bb.slab, bb.rewards, bb.dones, cb.last_obs, cb.last_dones, eb.rms, eb.ret)]
+                for x, y in zip(sa, sb):
+                    assert torch.equal(x, y)
+                snaps += sb
+            assert cb._fused_graph and cb.host_launches_per_step() == 1 and len(cb._graphs) == 1
+            if grouped:
+                assert dist.get_backend() == "nccl" and eb.exchanged()
+            va.close()
+            vb.close()
+        finally:
+            if grouped:
+                dist.destroy_process_group()
+        runs.append(snaps)
+    for x, y in zip(*runs):
+        assert torch.equal(x, y)

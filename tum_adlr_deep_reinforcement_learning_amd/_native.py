@@ -22,7 +22,7 @@ SOURCES = UNITS + [os.path.join(CSRC, "fw_device.hpp"), os.path.join(CSRC, "fw_q
 ARCH = os.environ.get("FWSIM_ARCH", "gfx950")
 
 _lib = None
-ABI_VERSION = 7  # include/fwsim.h FWSIM_ABI_VERSION
+ABI_VERSION = 8  # include/fwsim.h FWSIM_ABI_VERSION
 
 
 class FwError(RuntimeError):
@@ -137,6 +137,8 @@ SIGNATURES = {
     "fw_block_rows": (_c.c_int, [_vp, _i32, _c.POINTER(_i32)]),
     "fw_update_config": (_c.c_int, [_vp, _vp, _vp]),
     "fw_set_metrics_output": (_c.c_int, [_vp, _vp]),
+    "fw_set_collect_epilogue": (_c.c_int, [_vp, _vp]),
+    "fw_collect_records": (_c.c_int, [_vp, _c.POINTER(_i64), _c.POINTER(_i64)]),
     # include/fwrollout.h
     "fw_gae": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _c.c_double, _c.c_double, _vp, _vp, _vp]),
     "fw_moments_workspace_bytes": (_c.c_size_t, [_i64, _i32]),
@@ -147,6 +149,9 @@ SIGNATURES = {
     "fw_replay_add": (_c.c_int, [_vp, _i32, _vp]),
     "fw_rollout_store": (_c.c_int, [_vp, _i32, _vp, _i32, _vp]),
     "fw_policy_forward": (_c.c_int, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "fw_moments_merge": (_c.c_int, [_vp, _i32, _i32, _vp, _vp]),
+    "fw_vecnorm_merge_update": (_c.c_int, [_vp, _i32, _i32, _i32, _vp, _vp, _vp]),
+    "fw_collect_policy": (_c.c_int, [_vp, _vp, _vp]),
 }
 
 
@@ -162,6 +167,18 @@ class FwMlpPolicy(ctypes.Structure):  # include/fwrollout.h fw_mlp_policy
     _fields_ = [(k, _vp) for k in ("pi_w0", "pi_b0", "pi_w1", "pi_b1", "act_w", "act_b", "vf_w0", "vf_b0", "vf_w1",
                                    "vf_b1", "val_w", "val_b", "log_std", "noise_row")] + \
                [("d", _i32), ("hidden", _i32), ("act_dim", _i32), ("pad", _i32)]
+
+
+class FwCollectEpilogue(ctypes.Structure):  # include/fwsim.h fw_collect_epilogue
+    _fields_ = [("ret", _vp), ("gamma", _c.c_double), ("records", _vp), ("row_ctrl", _vp)]
+
+
+class FwCollectIO(ctypes.Structure):  # include/fwrollout.h fw_collect_io
+    _fields_ = [("obs", _vp), ("reward", _vp), ("done", _vp), ("rms", _vp), ("epsilon", _c.c_double),
+                ("clip_obs", _c.c_double), ("clip_reward", _c.c_double), ("norm_obs", _i32), ("norm_reward", _i32),
+                ("noise", _vp), ("low", _vp), ("high", _vp), ("clipped", _vp), ("ctrl", _vp), ("obs_rows", _vp),
+                ("act_rows", _vp), ("val_rows", _vp), ("logp_rows", _vp), ("rew_rows", _vp), ("start_rows", _vp),
+                ("n", _i64)]
 
 
 def load(path=None):

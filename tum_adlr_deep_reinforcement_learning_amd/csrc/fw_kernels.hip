@@ -110,6 +110,11 @@ struct State {
   T* obs_init;        // [n_obs][ld] raw observation row at the episode's reset (null: length-1 observations)
   T* obs_ring;        // [obs_hist][n_obs][ld] raw rows of past steps, slot = step % obs_hist
   T* prm;             // [FW_NPARAM][ld] per-aircraft parameters (null: no randomisation)
+  // collect epilogue of k_env_step (fw_set_collect_epilogue; all null: off)
+  double* col_ret;    // [n] VecNormalize discounted return, or null
+  double col_gamma;
+  double* col_rec;    // [blocks][1 + 2 D] per-block moment records, or null
+  int32_t* col_ctrl;  // rollout row counter advanced by the launch, or null
 };
 
 // streaming episode-metric state (fixed_wing.py:1644-1736 restated over running sums):
@@ -1072,6 +1077,72 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   FW_TSTAMP(4);
 }
 
+// The env-side half of VecNormalize.step_wait (vec_normalize.py:106-131) after the env step, while the
+// block's observations are still in cache (fw_set_collect_epilogue): per env ret = ret * gamma + reward
+// (vec_normalize.py:126-129, multiply and add kept separate as numpy does) then ret[done] = 0 (:130), and
+// per block one exact two-pass moment record (n_b, mean_b, M2_b) of the float32 observation columns and of
+// ret before its reset -- the batch moments of RunningMeanStd.update (running_mean_std.py:20-24), merged
+// over the blocks by fw_moments_merge / fw_vecnorm_merge_update.  Row lanes: one per aircraft (lane 0 of
+// each quad when Q = 4).  Four lanes per column, each summing 16 rows in order, then a quad butterfly:
+// every sum in a fixed order, so the records are deterministic.  Every lane of the block calls this.
+constexpr int COL_MAXD = FW_MAX_OBS + 1;
+template <typename T>
+__device__ __forceinline__ void collect_epilogue(const State<T>& s, int64_t i, bool row, int ow, const T* obs_out,
+                                                 const T* rew_out, const uint8_t* done_out, float* sx, double* sr) {
+  const int lane = (int)(threadIdx.x & 63);
+  const bool has_ret = s.col_ret != nullptr;
+  double ret = 0.0;
+  if (row && has_ret) {
+    double g = s.col_ret[i] * s.col_gamma;
+    asm volatile("" : "+v"(g));  // no FMA contraction of ret * gamma + reward
+    ret = g + (double)(float)rew_out[i];
+    s.col_ret[i] = done_out[i] ? 0.0 : ret;
+  }
+  if (s.col_rec) {
+    const int D = ow + (has_ret ? 1 : 0);
+    if (row) {
+      for (int j = 0; j < ow; j++) sx[lane * COL_MAXD + j] = (float)obs_out[i * ow + j];
+      sr[lane] = ret;
+    }
+    const unsigned long long rm = __ballot(row);
+    const double nb = (double)__popcll(rm);
+    __syncthreads();
+    double* rec = s.col_rec + (int64_t)blockIdx.x * (1 + 2 * D);
+    const int p = lane & 3;
+    for (int c0 = 0; c0 < D; c0 += 16) {
+      const int col = c0 + (lane >> 2);
+      const bool cv = col < D;
+      auto at = [&](int r) { return col < ow ? (double)sx[r * COL_MAXD + col] : sr[r]; };
+      double sum = 0.0;
+      if (cv)
+        for (int k = 0; k < 16; k++) {
+          const int r = p * 16 + k;
+          if ((rm >> r) & 1ull) sum += at(r);
+        }
+      sum += __shfl_xor(sum, 1);
+      sum += __shfl_xor(sum, 2);
+      const double mean = sum / nb;
+      double q = 0.0;
+      if (cv)
+        for (int k = 0; k < 16; k++) {
+          const int r = p * 16 + k;
+          if ((rm >> r) & 1ull) {
+            const double dv = at(r) - mean;
+            q += dv * dv;
+          }
+        }
+      q += __shfl_xor(q, 1);
+      q += __shfl_xor(q, 2);
+      if (cv && p == 0) {
+        rec[1 + col] = mean;
+        rec[1 + D + col] = q;
+      }
+    }
+    if (lane == 0) rec[0] = nb;
+  }
+  if (s.col_ctrl && blockIdx.x == 0 && lane == 0) s.col_ctrl[0] += 1;  // the stream's next launch sees it
+}
+
 template <typename T, typename C, bool RP = false, int Q = 1>
 __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_env_step(const DevCfg<T>* __restrict__ cfgp, State<T> s,
                                                     const T* __restrict__ actions, T* __restrict__ obs_out,
@@ -1081,13 +1152,20 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_env_step(const DevCfg<T>
                                                     int auto_reset) {
   const int64_t tid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const int64_t i = tid / Q;  // Q = 4: lanes 4i..4i+3 integrate aircraft i (fw_quad.hpp)
-  if (i >= s.n) return;
+  const bool collect = s.col_rec || s.col_ret || s.col_ctrl;
+  if (i >= s.n && !collect) return;
   const C& c = *reinterpret_cast<const C*>(cfgp);  // structural specialisation view (fw_device.hpp SpecCfg)
   __shared__ V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];  // y, f (+ error sum) of the block's aircraft (pairs)
   static_assert(Q != 1 || RP || FW_TAIL_QUAD == 0 || BLOCK == 64, "the tail handoff works per one-wave block");
   __shared__ qd::HoSlot<T> ho[Q == 1 && !RP ? BLOCK : 1];
-  env_step_lane<T, C, RP, Q, ((Q == 4 && (sizeof(T) == 4 || FW_PREF_Q4_F64)) || FW_PREF_Q1)>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out,
-                                                  episode_out, stats, auto_reset, (int)(tid % Q), ho);
+  static_assert(BLOCK == 64, "collect_epilogue: one-wave blocks");
+  __shared__ float col_x[64 * COL_MAXD];
+  __shared__ double col_r[64];
+  if (i < s.n)
+    env_step_lane<T, C, RP, Q, ((Q == 4 && (sizeof(T) == 4 || FW_PREF_Q4_F64)) || FW_PREF_Q1)>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out,
+                                                    episode_out, stats, auto_reset, (int)(tid % Q), ho);
+  if (collect)
+    collect_epilogue<T>(s, i, i < s.n && tid % Q == 0, c.n_obs * c.obs_len, obs_out, rew_out, done_out, col_x, col_r);
 }
 
 // One env step of k_env_rollout.  fp32: inlined, and scratch-free since the step loop re-materialises
@@ -1197,6 +1275,7 @@ struct fw_handle {
   int rand_active = 0;      // the current config randomises parameters (kernels read the rows)
   int lanes_opt = FW_LANES_AUTO;  // fw_set_lanes: 0 = automatic, 1, 4
   int quad_ok = 1;          // the config allows the quad integrator (no wrapped ODE-state variable)
+  fw_collect_epilogue col{};  // fw_set_collect_epilogue (all null: off)
 };
 
 namespace {
@@ -1550,6 +1629,10 @@ State<T> state_of(const fw_handle* h) {
   s.obs_init = h->obs_hist ? (T*)(b + h->o_obs_init) : nullptr;
   s.obs_ring = h->obs_hist ? (T*)(b + h->o_obs_ring) : nullptr;
   s.prm = h->o_prm ? (T*)(b + h->o_prm) : nullptr;
+  s.col_ret = h->col.ret;
+  s.col_gamma = h->col.gamma;
+  s.col_rec = h->col.records;
+  s.col_ctrl = h->col.row_ctrl;
   return s;
 }
 
@@ -1882,6 +1965,27 @@ int fw_set_metrics_output(fw_handle* h, void* metrics_dev) {
   if (!h) return set_err(FW_E_INVALID, "NULL handle");
   if (metrics_dev && !h->metrics) return set_err(FW_E_INVALID, "handle was created without episode metrics");
   h->met_out = metrics_dev;
+  return FW_OK;
+}
+
+int fw_set_collect_epilogue(fw_handle* h, const fw_collect_epilogue* epi) {
+  if (!h) return set_err(FW_E_INVALID, "NULL handle");
+  if (!epi) {
+    h->col = fw_collect_epilogue{};
+    return FW_OK;
+  }
+  if ((epi->ret || epi->records || epi->row_ctrl) && !h->has_env)
+    return set_err(FW_E_INVALID, "fw_set_collect_epilogue: handle has no env");
+  if (h->has_env && h->env.n_obs * std::max(h->env.obs_length, 1) + 1 > FW_MAX_OBS + 1 && epi->records)
+    return set_err(FW_E_UNSUPPORTED, "fw_set_collect_epilogue: more than FW_MAX_OBS observation values per env");
+  h->col = *epi;
+  return FW_OK;
+}
+
+int fw_collect_records(const fw_handle* h, int64_t* n_records, int64_t* max_records) {
+  if (!h) return set_err(FW_E_INVALID, "NULL handle");
+  if (n_records) *n_records = (h->n * lanes_of(h) + BLOCK - 1) / BLOCK;
+  if (max_records) *max_records = (h->n * 4 + BLOCK - 1) / BLOCK;
   return FW_OK;
 }
 

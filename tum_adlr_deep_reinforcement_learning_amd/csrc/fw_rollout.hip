@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/fwrollout.h"
@@ -217,8 +219,7 @@ __global__ __launch_bounds__(BLOCK) void k_moments_partial(const float* __restri
 // merges `parts` records (stride 1+2D) into one: one wave per column (MERGE_WAVES waves, all columns
 // at once for D <= 16), lane l holds records l, l+64, ...
 constexpr int MERGE_WAVES = 16;
-__global__ __launch_bounds__(64 * MERGE_WAVES) void k_moments_merge(const double* __restrict__ part, int parts, int D,
-                                                                    double* __restrict__ out) {
+__device__ __forceinline__ void merge_records(const double* __restrict__ part, int parts, int D, double* __restrict__ out) {
   const int S = 1 + 2 * D;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int j = w; j < D; j += MERGE_WAVES) {
@@ -244,13 +245,19 @@ __global__ __launch_bounds__(64 * MERGE_WAVES) void k_moments_merge(const double
   }
 }
 
-// RunningMeanStd.update_from_moments, one thread per column; parts merged in rank order.
-__global__ void k_rms_update(const double* __restrict__ parts, int n_parts, int d, int has_ret, double* __restrict__ rms,
-                             int update_obs, int update_ret) {
+__global__ __launch_bounds__(64 * MERGE_WAVES) void k_moments_merge(const double* __restrict__ part, int parts, int D,
+                                                                    double* __restrict__ out) {
+  merge_records(part, parts, D, out);
+}
+
+// RunningMeanStd.update_from_moments, one thread per column; parts merged in rank order.  Every thread of
+// the block calls it (old_count is read by thread 0 and shared through LDS behind a barrier).
+__device__ __forceinline__ void rms_update(const double* __restrict__ parts, int n_parts, int d, int has_ret,
+                                           double* __restrict__ rms, int update_obs, int update_ret,
+                                           double* old_count) {
   const int D = d + (has_ret ? 1 : 0);
   const int S = 1 + 2 * D;
   const int j = threadIdx.x;
-  __shared__ double old_count[2];
   if (j == 0) {
     old_count[0] = rms[2 * d];
     old_count[1] = rms[2 * d + 3];
@@ -283,6 +290,27 @@ __global__ void k_rms_update(const double* __restrict__ parts, int n_parts, int 
       }
     }
   }
+}
+
+__global__ void k_rms_update(const double* __restrict__ parts, int n_parts, int d, int has_ret, double* __restrict__ rms,
+                             int update_obs, int update_ret) {
+  __shared__ double old_count[2];
+  rms_update(parts, n_parts, d, has_ret, rms, update_obs, update_ret, old_count);
+}
+
+// k_moments_merge + k_rms_update of the single merged record in one launch (the unsharded statistics
+// update of a collect step): the same device functions, so the same bits as the two launches.
+__global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge_update(const double* __restrict__ part, int parts, int d,
+                                                                   int has_ret, double* __restrict__ rms,
+                                                                   double* __restrict__ rec_out) {
+  __shared__ double rec[1 + 2 * MAXD];
+  __shared__ double old_count[2];
+  const int D = d + (has_ret ? 1 : 0);
+  merge_records(part, parts, D, rec);
+  __syncthreads();
+  if (rec_out)
+    for (int k = threadIdx.x; k < 1 + 2 * D; k += blockDim.x) rec_out[k] = rec[k];
+  rms_update(rec, 1, d, has_ret, rms, 1, 1, old_count);  // every thread: it holds a barrier
 }
 
 __global__ __launch_bounds__(BLOCK) void k_vecnorm_apply(const float* __restrict__ obs, int64_t n, int d, int64_t ldx,
@@ -551,9 +579,270 @@ __global__ __launch_bounds__(POL_BLOCK) void k_policy_forward(fw_mlp_policy P, c
   }
 }
 
+// ---------------------------------------------------------------------------
+// The same policy forward on the matrix cores (v_mfma_f32_16x16x4_f32: f32 in, f32 accumulate, exact f32
+// products), one wave per tile of 16 envs, every weight resident in registers for the wave's lifetime.
+//
+// The layers are computed transposed, H^T = W . X^T, so the env index is the MFMA's N (column) dimension
+// and a layer's output tile is directly the next layer's B operand: the 16x16 D tile of out-tile O holds, in
+// lane l's register v, unit 16 O + 4 (l >> 4) + v of env l & 15 -- and a B operand of the 16x16x4 form takes
+// in lane l the k-row l >> 4 of column l & 15.  Reading the K dimension of the next layer in the order
+// k-step (T, v) = units {16 T + 4 g + v : g = 0..3} makes D register v of tile T exactly the B operand of
+// k-step (T, v), with no lane exchange; the A operands (weights) are loaded in that order once per wave:
+//   layer 0   A(O, s)    lane l: W0[16 O + (l & 15)][4 s + (l >> 4)]          (B = obs features 4s..4s+3)
+//   layer 1   A(O, T, v) lane l: W1[16 O + (l & 15)][16 T + 4 (l >> 4) + v]    (a float4 per (O, T))
+//   heads     rows 0..A-1 = action means (actor latent), row 15 = value (critic latent), one D tile
+// Per 16 envs: 2 x (4 S + 64 + 16) MFMAs (S = k-steps of the observation, 4 for d <= 16).  Sums run in
+// the k-step order above (not the torch GEMM's): equal to the module within fp32 rounding.
+// ---------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct PolArgs {
+  fw_mlp_policy P;
+  const float* obs;
+  const float* reward;
+  const uint8_t* done;
+  const double* rms;
+  double eps, clip_obs, clip_rew;
+  int norm_obs, norm_rew;
+  const float* noise;
+  const int32_t* noise_row;  // device row of `noise` ([T][n][A]) or null
+  const float *low, *high;
+  float* clipped;
+  const int32_t* ctrl;       // collect mode: rows at ctrl[0]; null: row 0 and no reward / start rows
+  float *obs_rows, *act, *val, *logp, *rew_rows;
+  uint8_t* start_rows;
+  int64_t n;
+};
+
+constexpr int PM_WAVES = 4;  // waves per block; one block per CU (one wave per SIMD)
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float norm_obs_val(float o, double mean, double den, double clip) {
+  double y = ((double)o - mean) / den;  // np.clip((obs - mean) / np.sqrt(var + eps), -clip, clip) (k_vecnorm_apply)
+  y = fmin(fmax(y, -clip), clip);
+  return (float)y;
+}
+
+template <int S>  // k-steps of 4 observation features (d <= 4 S)
+__global__ __launch_bounds__(64 * PM_WAVES) void k_policy_mfma(PolArgs G) {
+  const int lane = threadIdx.x & 63;
+  const int c16 = lane & 15, g = lane >> 4;
+  const int d = G.P.d, A = G.P.act_dim;
+  const int64_t n = G.n;
+  const int H = POL_MAXH;
+  // ---- weights -> registers (A operands), biases in the D layout (unit 16 O + 4 g + v)
+  float w0p[4][S], w0v[4][S], w1p[4][4][4], w1v[4][4][4], hp[4][4], hv[4][4];
+  f32x4 b0p[4], b0v[4], b1p[4], b1v[4], bh;
+#pragma unroll
+  for (int O = 0; O < 4; O++) {
+    const int u = 16 * O + c16;
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const int f = 4 * s + g;
+      w0p[O][s] = f < d ? G.P.pi_w0[u * d + f] : 0.0f;
+      w0v[O][s] = f < d ? G.P.vf_w0[u * d + f] : 0.0f;
+    }
+#pragma unroll
+    for (int T = 0; T < 4; T++) {
+      const f32x4 qp = *reinterpret_cast<const f32x4*>(G.P.pi_w1 + u * H + 16 * T + 4 * g);
+      const f32x4 qv = *reinterpret_cast<const f32x4*>(G.P.vf_w1 + u * H + 16 * T + 4 * g);
+#pragma unroll
+      for (int v = 0; v < 4; v++) {
+        w1p[O][T][v] = qp[v];
+        w1v[O][T][v] = qv[v];
+      }
+    }
+    b0p[O] = *reinterpret_cast<const f32x4*>(G.P.pi_b0 + 16 * O + 4 * g);
+    b0v[O] = *reinterpret_cast<const f32x4*>(G.P.vf_b0 + 16 * O + 4 * g);
+    b1p[O] = *reinterpret_cast<const f32x4*>(G.P.pi_b1 + 16 * O + 4 * g);
+    b1v[O] = *reinterpret_cast<const f32x4*>(G.P.vf_b1 + 16 * O + 4 * g);
+  }
+#pragma unroll
+  for (int T = 0; T < 4; T++) {
+    f32x4 qp = {0.0f, 0.0f, 0.0f, 0.0f}, qv = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (c16 < A) qp = *reinterpret_cast<const f32x4*>(G.P.act_w + c16 * H + 16 * T + 4 * g);
+    if (c16 == 15) qv = *reinterpret_cast<const f32x4*>(G.P.val_w + 16 * T + 4 * g);
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+      hp[T][v] = qp[v];
+      hv[T][v] = qv[v];
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < 4; v++) {
+    const int r = 4 * g + v;
+    bh[v] = r < A ? G.P.act_b[r] : (r == 15 ? G.P.val_b[0] : 0.0f);
+  }
+  // ---- this launch's rows and the VecNormalize statistics of this lane's features
+  const int64_t row = G.ctrl ? (int64_t)G.ctrl[0] : 0;
+  const float* noise = G.noise;
+  if (noise) noise += (G.ctrl ? row : (G.noise_row ? (int64_t)G.noise_row[0] : 0)) * n * A;
+  const bool nobs = G.rms && G.norm_obs;
+  double mean[S], den[S];
+#pragma unroll
+  for (int s = 0; s < S; s++) {
+    const int f = 4 * s + g;
+    mean[s] = (nobs && f < d) ? G.rms[f] : 0.0;
+    den[s] = (nobs && f < d) ? sqrt(G.rms[d + f] + G.eps) : 1.0;
+  }
+  const double rden = (G.rms && G.norm_rew) ? sqrt(G.rms[2 * d + 2] + G.eps) : 1.0;
+  float* obs_rows = G.obs_rows ? G.obs_rows + row * n * d : nullptr;
+  float* act = G.act + row * n * A;
+  float* val = G.val + row * n;
+  float* logp = G.logp + row * n;
+  const float half_log_2pi = 0.91893853320467274f;
+
+  const int64_t tiles = (n + 15) / 16;
+  const int64_t wid = (int64_t)blockIdx.x * PM_WAVES + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * PM_WAVES;
+  for (int64_t tile = wid; tile < tiles; tile += nw) {
+    const int64_t env = tile * 16 + c16;
+    const bool valid = env < n;
+    // ---- observation (normalised) = B operands of layer 0; the rollout's observation row
+    float x[S];
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const int f = 4 * s + g;
+      float o = (valid && f < d) ? G.obs[env * d + f] : 0.0f;
+      if (nobs && valid && f < d) o = norm_obs_val(o, mean[s], den[s], G.clip_obs);
+      x[s] = o;
+      if (obs_rows && valid && f < d) obs_rows[env * d + f] = o;
+    }
+    // ---- the previous step's reward row (normalised) and the episode starts of this row
+    if (G.ctrl && row >= 1 && g == 1 && valid) {
+      double r = (double)G.reward[env];
+      if (G.rms && G.norm_rew) r = fmin(fmax(r / rden, -G.clip_rew), G.clip_rew);
+      G.rew_rows[(row - 1) * n + env] = (float)r;
+      G.start_rows[row * n + env] = G.done[env];
+    }
+    // ---- layer 0 (8 independent accumulators)
+    f32x4 cp[4], cv[4];
+#pragma unroll
+    for (int O = 0; O < 4; O++) cp[O] = cv[O] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+#pragma unroll
+      for (int O = 0; O < 4; O++) {
+        cp[O] = mfma4(w0p[O][s], x[s], cp[O]);
+        cv[O] = mfma4(w0v[O][s], x[s], cv[O]);
+      }
+    }
+    f32x4 hpv[4], hvv[4];  // tanh(layer 0): the B operands of layer 1, k-step (T, v) = register v of tile T
+#pragma unroll
+    for (int T = 0; T < 4; T++)
+#pragma unroll
+      for (int v = 0; v < 4; v++) {
+        hpv[T][v] = ftanh(cp[T][v] + b0p[T][v]);
+        hvv[T][v] = ftanh(cv[T][v] + b0v[T][v]);
+      }
+    // ---- layer 1
+#pragma unroll
+    for (int O = 0; O < 4; O++) cp[O] = cv[O] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int T = 0; T < 4; T++)
+#pragma unroll
+      for (int v = 0; v < 4; v++)
+#pragma unroll
+        for (int O = 0; O < 4; O++) {
+          cp[O] = mfma4(w1p[O][T][v], hpv[T][v], cp[O]);
+          cv[O] = mfma4(w1v[O][T][v], hvv[T][v], cv[O]);
+        }
+#pragma unroll
+    for (int T = 0; T < 4; T++)
+#pragma unroll
+      for (int v = 0; v < 4; v++) {
+        hpv[T][v] = ftanh(cp[T][v] + b1p[T][v]);
+        hvv[T][v] = ftanh(cv[T][v] + b1v[T][v]);
+      }
+    // ---- heads: actor rows 0..A-1 and the value row 15 of one tile (two accumulators, disjoint rows)
+    f32x4 ha = {0.0f, 0.0f, 0.0f, 0.0f}, hc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int T = 0; T < 4; T++)
+#pragma unroll
+      for (int v = 0; v < 4; v++) {
+        ha = mfma4(hp[T][v], hpv[T][v], ha);
+        hc = mfma4(hv[T][v], hvv[T][v], hc);
+      }
+    f32x4 out;
+#pragma unroll
+    for (int v = 0; v < 4; v++) out[v] = (ha[v] + hc[v]) + bh[v];  // one of ha / hc is 0 in each row
+    // rows 4..7 (A > 4) from the lanes 16 up
+    f32x4 hi;
+#pragma unroll
+    for (int v = 0; v < 4; v++) hi[v] = __shfl(out[v], (lane + 16) & 63);
+    if (g == 3 && valid) val[env] = out[3];
+    if (g == 0 && valid) {
+      float lp = 0.0f;
+#pragma unroll
+      for (int a = 0; a < POL_MAXA; a++) {
+        if (a < A) {
+          const float m = a < 4 ? out[a & 3] : hi[a & 3];
+          const float ls = G.P.log_std[a];
+          const float sd = expf(ls);
+          // the module's arithmetic (rollout.py MlpActorCritic.forward): separate mul / add, as torch's kernels
+          const float ac = noise ? m + sd * noise[env * A + a] : m;
+          const float dv = ac - m;
+          lp = lp + (((-(dv * dv)) / ((2.0f * sd) * sd) - ls) - half_log_2pi);
+          act[env * A + a] = ac;
+          if (G.clipped) G.clipped[env * A + a] = fmaxf(fminf(ac, G.high[a]), G.low[a]);
+        }
+      }
+      logp[env] = lp;
+    }
+  }
+}
+
 unsigned grid_for(int64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
 
 int64_t moments_parts(int64_t n) { return std::max<int64_t>(1, (n + MROWS - 1) / MROWS); }
+
+int cu_count(int* out) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    FW_HIP(hipGetDevice(&dev));
+    FW_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  *out = cus;
+  return FW_OK;
+}
+
+// the matrix-core kernel reads the hidden / head weights and the biases as 16-byte vectors; the VALU
+// kernel (k_policy_forward) stays for unaligned parameters and as the A/B reference (FW_POL_VALU=1)
+bool use_mfma(const fw_mlp_policy* p) {
+  static const bool valu = std::getenv("FW_POL_VALU") != nullptr;
+  if (valu) return false;
+  const void* v16[] = {p->pi_w1, p->vf_w1, p->act_w, p->val_w, p->pi_b0, p->vf_b0, p->pi_b1, p->vf_b1};
+  for (const void* q : v16)
+    if ((uintptr_t)q % 16) return false;
+  return true;
+}
+
+int launch_mfma(const PolArgs& G, hipStream_t s) {
+  int cus = 0;
+  if (int rc = cu_count(&cus)) return rc;
+  const int64_t tiles = (G.n + 15) / 16;
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((tiles + PM_WAVES - 1) / PM_WAVES, cus));
+  if (G.P.d <= 16)
+    hipLaunchKernelGGL(k_policy_mfma<4>, dim3(grid), dim3(64 * PM_WAVES), 0, s, G);
+  else
+    hipLaunchKernelGGL(k_policy_mfma<8>, dim3(grid), dim3(64 * PM_WAVES), 0, s, G);
+  FW_HIP(hipGetLastError());
+  return FW_OK;
+}
+
+int check_policy(const fw_mlp_policy* p, const char* who) {
+  if (p->d < 1 || p->d > POL_MAXD || p->hidden != POL_MAXH || p->act_dim < 1 || p->act_dim > POL_MAXA)
+    return fw::set_error(FW_E_INVALID, std::string(who) + ": d 1..32, hidden 64 (SB3's default net_arch), act_dim 1..8");
+  const void* ptrs[13] = {p->pi_w0, p->pi_b0, p->pi_w1, p->pi_b1, p->act_w, p->act_b, p->vf_w0,
+                          p->vf_b0, p->vf_w1, p->vf_b1, p->val_w, p->val_b, p->log_std};
+  for (const void* q : ptrs)
+    if (!q) return fw::set_error(FW_E_INVALID, std::string(who) + ": NULL parameter");
+  return FW_OK;
+}
 
 }  // namespace
 
@@ -679,27 +968,86 @@ int fw_policy_forward(const fw_mlp_policy* p, const float* obs, int64_t n, const
                       const float* high, float* actions, float* clipped, float* values, float* log_probs, void* stream) {
   if (!p || !obs || !actions || !values || !log_probs || n < 1)
     return fw::set_error(FW_E_INVALID, "fw_policy_forward: NULL buffer or n < 1");
-  if (p->d < 1 || p->d > POL_MAXD || p->hidden != POL_MAXH || p->act_dim < 1 || p->act_dim > POL_MAXA)
-    return fw::set_error(FW_E_INVALID, "fw_policy_forward: d 1..32, hidden 64 (SB3's default net_arch), act_dim 1..8");
-  const void* ptrs[13] = {p->pi_w0, p->pi_b0, p->pi_w1, p->pi_b1, p->act_w, p->act_b, p->vf_w0,
-                          p->vf_b0, p->vf_w1, p->vf_b1, p->val_w, p->val_b, p->log_std};
-  for (const void* q : ptrs)
-    if (!q) return fw::set_error(FW_E_INVALID, "fw_policy_forward: NULL parameter");
+  if (int rc = check_policy(p, "fw_policy_forward")) return rc;
   if (clipped && (!low || !high)) return fw::set_error(FW_E_INVALID, "fw_policy_forward: clipped needs low and high");
+  if (use_mfma(p)) {
+    PolArgs G{};
+    G.P = *p;
+    G.obs = obs;
+    G.noise = noise;
+    G.noise_row = p->noise_row;
+    G.low = low;
+    G.high = high;
+    G.clipped = clipped;
+    G.act = actions;
+    G.val = values;
+    G.logp = log_probs;
+    G.n = n;
+    return launch_mfma(G, (hipStream_t)stream);
+  }
   const int d = p->d, H = p->hidden, A = p->act_dim;
   const size_t lds = (size_t)(pol_vf_offset(d, H, A) + pol_net_floats(d, H, 1)) * sizeof(float);
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    FW_HIP(hipGetDevice(&dev));
-    FW_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  }
+  int cus = 0;
+  if (int rc = cu_count(&cus)) return rc;
   const int64_t tiles = (n + POL_BLOCK / 2 - 1) / (POL_BLOCK / 2);
   const unsigned grid = (unsigned)std::min<int64_t>(tiles, (int64_t)cus * POL_BLOCKS_PER_CU);
   hipLaunchKernelGGL(k_policy_forward<POL_MAXH>, dim3(grid), dim3(POL_BLOCK), lds, (hipStream_t)stream, *p, obs, n, noise,
                      low, high, actions, clipped, values, log_probs);
   FW_HIP(hipGetLastError());
   return FW_OK;
+}
+
+int fw_moments_merge(const double* records, int32_t n_records, int32_t D, double* out, void* stream) {
+  if (!records || !out || n_records < 1 || D < 1 || D > MAXD)
+    return fw::set_error(FW_E_INVALID, "fw_moments_merge: bad arguments");
+  hipLaunchKernelGGL(k_moments_merge, dim3(1), dim3(64 * std::min<int>(D, MERGE_WAVES)), 0, (hipStream_t)stream, records,
+                     (int)n_records, (int)D, out);
+  FW_HIP(hipGetLastError());
+  return FW_OK;
+}
+
+int fw_vecnorm_merge_update(const double* records, int32_t n_records, int32_t d, int32_t has_ret, double* rms,
+                            double* rec_out, void* stream) {
+  const int D = d + (has_ret ? 1 : 0);
+  if (!records || !rms || n_records < 1 || d < 0 || D < 1 || D > MAXD)
+    return fw::set_error(FW_E_INVALID, "fw_vecnorm_merge_update: bad arguments");
+  hipLaunchKernelGGL(k_merge_update, dim3(1), dim3(64 * MERGE_WAVES), 0, (hipStream_t)stream, records, (int)n_records,
+                     (int)d, (int)(has_ret != 0), rms, rec_out);
+  FW_HIP(hipGetLastError());
+  return FW_OK;
+}
+
+int fw_collect_policy(const fw_mlp_policy* p, const fw_collect_io* io, void* stream) {
+  if (!p || !io) return fw::set_error(FW_E_INVALID, "fw_collect_policy: NULL argument");
+  if (int rc = check_policy(p, "fw_collect_policy")) return rc;
+  if (io->n < 1 || !io->obs || !io->reward || !io->done || !io->low || !io->high || !io->clipped || !io->ctrl ||
+      !io->obs_rows || !io->act_rows || !io->val_rows || !io->logp_rows || !io->rew_rows || !io->start_rows)
+    return fw::set_error(FW_E_INVALID, "fw_collect_policy: NULL buffer or n < 1");
+  if (!use_mfma(p)) return fw::set_error(FW_E_UNSUPPORTED, "fw_collect_policy: parameters must be 16-byte aligned");
+  PolArgs G{};
+  G.P = *p;
+  G.obs = io->obs;
+  G.reward = io->reward;
+  G.done = io->done;
+  G.rms = io->rms;
+  G.eps = io->epsilon;
+  G.clip_obs = io->clip_obs;
+  G.clip_rew = io->clip_reward;
+  G.norm_obs = io->norm_obs;
+  G.norm_rew = io->norm_reward;
+  G.noise = io->noise;
+  G.low = io->low;
+  G.high = io->high;
+  G.clipped = io->clipped;
+  G.ctrl = io->ctrl;
+  G.obs_rows = io->obs_rows;
+  G.act = io->act_rows;
+  G.val = io->val_rows;
+  G.logp = io->logp_rows;
+  G.rew_rows = io->rew_rows;
+  G.start_rows = io->start_rows;
+  G.n = io->n;
+  return launch_mfma(G, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -233,6 +233,42 @@ class Engine:
         _native.check(self.lib.fw_observe(self.h, _ptr(self.obs), self.stream()), "fw_observe")
         return self.obs
 
+    def set_collect_epilogue(self, ret=None, gamma=0.0, records=None, row_ctrl=None):
+        """fw_set_collect_epilogue: every following ``env_step`` also updates VecNormalize's discounted return
+        ``ret`` (fp64 [n]: ret*gamma + reward, then 0 where done) and writes one moment record per launch block
+        of (observation, ret) into ``records`` (fp64, ``collect_records()[1]`` x (1 + 2 D) rows); ``row_ctrl``
+        (int32 device tensor) gets ``[0] += 1`` per launch.  All None turns it off.  A captured step keeps the
+        setting it was captured with."""
+        if ret is None and records is None and row_ctrl is None:
+            _native.check(self.lib.fw_set_collect_epilogue(self.h, None), "fw_set_collect_epilogue")
+            self._collect = None
+            return
+        for t, dt in ((ret, torch.float64), (records, torch.float64), (row_ctrl, torch.int32)):
+            if t is not None and (t.dtype != dt or t.device != self.device or not t.is_contiguous()):
+                raise ValueError("set_collect_epilogue: ret / records fp64, row_ctrl int32, contiguous on the device")
+        if ret is not None and ret.numel() != self.n:
+            raise ValueError("set_collect_epilogue: ret must hold one value per env")
+        if records is not None:
+            D = self.n_obs_values + (1 if ret is not None else 0)
+            if records.numel() < self.collect_records()[1] * (1 + 2 * D):
+                raise ValueError("set_collect_epilogue: records buffer too small")
+        e = _native.FwCollectEpilogue(ret.data_ptr() if ret is not None else None, float(gamma),
+                                      records.data_ptr() if records is not None else None,
+                                      row_ctrl.data_ptr() if row_ctrl is not None else None)
+        _native.check(self.lib.fw_set_collect_epilogue(self.h, ctypes.byref(e)), "fw_set_collect_epilogue")
+        self._collect = (ret, records, row_ctrl)  # keep the buffers alive while the handle writes them
+
+    def collect_records(self):
+        """(records the next env_step writes, the most any lanes setting writes)."""
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        _native.check(self.lib.fw_collect_records(self.h, ctypes.byref(a), ctypes.byref(b)), "fw_collect_records")
+        return a.value, b.value
+
+    @property
+    def n_obs_values(self):
+        """Values per observation (rows x entries: observation.length x n_obs)."""
+        return int(self.obs.shape[1])
+
     # ------------------------------------------------------------------
     _U32 = (C.FW_BLK_STEPS, C.FW_BLK_GOAL)
 

@@ -264,6 +264,8 @@ class MlpActorCritic(nn.Module):
 
 
 class RolloutCollector:
+    capture_collective = True  # a sharded fused step captures its RCCL exchange inside the one graph
+
     """OnPolicyAlgorithm.collect_rollouts (on_policy_algorithm.py:126-190) with everything on the device.
 
     ``env`` is a FixedWingVecEnv (or a VecNormalize-style wrapper around one) built with
@@ -364,7 +366,8 @@ class RolloutCollector:
         pol = self.policy
         pol_key = (id(pol), bool(getattr(pol, "deterministic_rollout", False)),
                    tuple(p.data_ptr() for p in pol.parameters()) if isinstance(pol, nn.Module) else None)
-        return (env_key, self._split(), self.buffer.slab.data_ptr(), self.buffer.buffer_size, pol_key)
+        return (env_key, self._split(), self.buffer.slab.data_ptr(), self.buffer.buffer_size, pol_key,
+                self.capture_collective)
 
     def _capture(self):
         """Capture one collect step on static tensors: s_obs (the observation the policy acts on, then
@@ -374,6 +377,9 @@ class RolloutCollector:
         # capture itself records only, so no env state moves here
         if not getattr(self, "_eager_done", False):
             raise RuntimeError("collect(graph=True): run one eager collect() first (warms kernels outside the capture)")
+        if self._fused_collect_ok():
+            return self._capture_fused()
+        self._fused_graph = False
         buf, env, dev = self.buffer, self.env, self.buffer.device
         N, D, A = buf.n_envs, buf.obs_dim, buf.action_dim
         self.s_obs = torch.empty(N, D, dtype=torch.float32, device=dev)
@@ -451,6 +457,8 @@ class RolloutCollector:
         buf = self.buffer
         if getattr(self, "_graphs", None) is None or self._key != self.graph_key():
             self._capture()
+        if self._fused_graph:
+            return self._collect_fused(n)
         N, D = buf.n_envs, buf.obs_dim
         buf.reset()
         if self._fused(self.s_obs):
@@ -472,6 +480,177 @@ class RolloutCollector:
                 g1.replay()
         self.last_obs = self.s_obs.clone().reshape(self.last_obs.shape)
         self.last_dones = self._dsrc.clone()
+        buf.pos, buf.full = n, n == buf.buffer_size
+        last_values = self.policy.predict_values(self.last_obs)
+        buf.compute_returns_and_advantage(last_values, self.last_dones)
+        return buf
+
+    # ------------------------------------------------------------ the fused collect step
+    # One captured step = fw_collect_policy (VecNormalize's normalisation of the env's raw output, the
+    # policy, the rollout rows at row ctrl[0]) -> fw_env_step (+ its collect epilogue: the moment records,
+    # the return update, ctrl[0] += 1) -> the statistics update (fw_vecnorm_merge_update; sharded:
+    # fw_moments_merge -> RCCL all-gather -> fw_rms_update).  3 launches per step unsharded, and one host
+    # launch (graph replay) per step sharded too when the collective is captured.
+    def _vecnorm(self):
+        from .vec_normalize import VecNormalize
+        return self.env if isinstance(self.env, VecNormalize) else None
+
+    def _fused_collect_ok(self):
+        buf, pol = self.buffer, self.policy
+        vn = self._vecnorm()
+        venv = vn.venv if vn is not None else self.env
+        eng = getattr(venv, "engine", None)
+        if eng is None or eng.dtype != torch.float32 or getattr(venv, "_hists", None) is not None:
+            return False
+        if vn is not None and not vn.fused_stats:
+            return False
+        if not (isinstance(pol, MlpActorCritic) and self._fused(eng.obs)):
+            return False
+        lin = [m for m in pol.modules() if isinstance(m, nn.Linear)]
+        return all(t.data_ptr() % 16 == 0 for m in lin for t in (m.weight, m.bias)) and \
+            eng.n_obs_values == buf.obs_dim and buf.action_dim == pol.action_net.out_features
+
+    def _capture_fused(self):
+        buf, pol, dev = self.buffer, self.policy, self.buffer.device
+        vn = self._vecnorm()
+        venv = vn.venv if vn is not None else self.env
+        eng = venv.engine
+        lib = _native.load()
+        N, A = buf.n_envs, buf.action_dim
+        self.s_clip = torch.empty(N, A, dtype=torch.float32, device=dev)
+        self._ctrl = torch.zeros(2, dtype=torch.int32, device=dev)
+        noise = self._draw_noise(0)
+        if not hasattr(pol, "_fw_p"):
+            pol._fw_p = _native.FwMlpPolicy()
+        p = pol._fw_p
+        lin = [m for m in pol.pi if isinstance(m, nn.Linear)] + [pol.action_net] + \
+              [m for m in pol.vf if isinstance(m, nn.Linear)] + [pol.value_net]
+        for k, m in zip((("pi_w0", "pi_b0"), ("pi_w1", "pi_b1"), ("act_w", "act_b"), ("vf_w0", "vf_b0"),
+                         ("vf_w1", "vf_b1"), ("val_w", "val_b")), lin):
+            setattr(p, k[0], m.weight.data_ptr())
+            setattr(p, k[1], m.bias.data_ptr())
+        p.log_std, p.d, p.hidden, p.act_dim, p.noise_row = pol.log_std.data_ptr(), buf.obs_dim, 64, A, None
+        io = _native.FwCollectIO()
+        io.obs, io.reward, io.done = eng.obs.data_ptr(), eng.reward.data_ptr(), eng.done.data_ptr()
+        if vn is not None:
+            io.rms, io.epsilon, io.clip_obs, io.clip_reward = vn.rms.data_ptr(), vn.epsilon, vn.clip_obs, vn.clip_reward
+            io.norm_obs, io.norm_reward = int(vn.norm_obs), int(vn.norm_reward)
+        io.noise = noise.data_ptr() if noise is not None else None
+        io.low, io.high, io.clipped, io.ctrl = self.low.data_ptr(), self.high.data_ptr(), self.s_clip.data_ptr(), \
+            self._ctrl.data_ptr()
+        io.obs_rows, io.act_rows = buf.observations.data_ptr(), buf.actions.data_ptr()
+        io.val_rows, io.logp_rows = buf.values.data_ptr(), buf.log_probs.data_ptr()
+        io.rew_rows, io.start_rows, io.n = buf.rewards.data_ptr(), buf.dones.data_ptr(), N
+        self._io = io
+        grouped = vn is not None and vn.exchanged()
+        if vn is not None:
+            vn._ensure_parts()
+
+        def policy():
+            _native.check(lib.fw_collect_policy(ctypes.byref(p), ctypes.byref(io), _stream(dev)), "fw_collect_policy")
+
+        def env_step():
+            eng.env_step(self.s_clip, auto_reset=True, stats=True)
+
+        def stats_local():
+            if vn is None:
+                return
+            if grouped:
+                vn.merge_records(vn._rec)
+            else:
+                vn.merge_update()
+
+        def stats_exchange():
+            if grouped:
+                vn._gather(vn._rec)
+
+        def stats_finish():
+            if grouped:
+                vn._merge()
+
+        if vn is not None:
+            vn.set_epilogue(row_ctrl=self._ctrl)
+        else:
+            eng.set_collect_epilogue(row_ctrl=self._ctrl)
+        try:  # keep_graph: graph_nodes() can list what a step launches
+            self._graphs = [torch.cuda.CUDAGraph(keep_graph=True)]
+            if grouped and not self.capture_collective:
+                self._graphs.append(torch.cuda.CUDAGraph(keep_graph=True))
+                with torch.cuda.graph(self._graphs[0]):
+                    policy()
+                    env_step()
+                    stats_local()
+                with torch.cuda.graph(self._graphs[1]):
+                    stats_finish()
+            else:
+                with torch.cuda.graph(self._graphs[0]):
+                    policy()
+                    env_step()
+                    stats_local()
+                    stats_exchange()  # an RCCL all-gather captured into the graph (nccl backend)
+                    stats_finish()
+        finally:
+            eng.set_collect_epilogue()
+        for g in self._graphs:
+            g.instantiate()
+        self._fused_graph = True
+        self._fused_parts = (vn, eng, grouped, stats_exchange)
+        self._key = self.graph_key()
+
+    def graph_nodes(self):
+        """Node types of each captured step graph of the fused path (hipGraphGetNodes / hipGraphNodeGetType:
+        0 = kernel, 1 = memcpy, 2 = memset, 5 = empty, 6 / 7 = event wait / record)."""
+        hip = _native.load()  # dlsym through libfwsim.so reaches its HIP runtime
+        out = []
+        for g in self._graphs:
+            raw = ctypes.c_void_p(g.raw_cuda_graph())
+            cnt = ctypes.c_size_t(0)
+            if hip.hipGraphGetNodes(raw, None, ctypes.byref(cnt)) != 0:
+                raise _native.FwError("hipGraphGetNodes failed")
+            nodes = (ctypes.c_void_p * cnt.value)()
+            hip.hipGraphGetNodes(raw, nodes, ctypes.byref(cnt))
+            types = []
+            for k in range(cnt.value):
+                t = ctypes.c_int(-1)
+                hip.hipGraphNodeGetType(ctypes.c_void_p(nodes[k]), ctypes.byref(t))
+                types.append(t.value)
+            out.append(types)
+        return out
+
+    def host_launches_per_step(self):
+        """Host-side launches per replayed collect step (graph replays + an eager collective between them)."""
+        g = getattr(self, "_graphs", None) or []
+        return len(g) + (1 if len(g) > 1 else 0)
+
+    def _collect_fused(self, n):
+        buf = self.buffer
+        vn, eng, grouped, exchange = self._fused_parts
+        buf.reset()
+        self._draw_noise(n)
+        buf.dones[0].copy_(self.last_dones)  # the episode starts of row 0; row t >= 1 comes from the step
+        self._ctrl[0] = 0
+        self._ctrl[1] = n
+        if len(self._graphs) == 1:
+            g = self._graphs[0]
+            for _ in range(n):
+                g.replay()
+        else:
+            g0, g1 = self._graphs
+            for _ in range(n):
+                g0.replay()
+                exchange()
+                g1.replay()
+        # the last step's reward row and the VecNormalize outputs of the last step (its obs_out is the
+        # policy input of the next collection)
+        if vn is not None:
+            vn._apply(eng.obs, eng.reward, None)
+            vn.old_obs, vn.old_reward = eng.obs, eng.reward
+            buf.rewards[n - 1].copy_(vn.rew_out)
+            self.last_obs = vn.obs_out.clone().reshape(self.last_obs.shape)
+        else:
+            buf.rewards[n - 1].copy_(eng.reward)
+            self.last_obs = eng.obs.clone().reshape(self.last_obs.shape)
+        self.last_dones = eng.done.clone()
         buf.pos, buf.full = n, n == buf.buffer_size
         last_values = self.policy.predict_values(self.last_obs)
         buf.compute_returns_and_advantage(last_values, self.last_dones)

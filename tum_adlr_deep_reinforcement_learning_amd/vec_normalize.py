@@ -92,6 +92,14 @@ class VecNormalize:
         self.old_reward = None
         self.obs_rms = _RMSView(self, "obs")
         self.ret_rms = _RMSView(self, "ret")
+        # the env step's own epilogue computes the moment records and the return update (fwsim.h
+        # fw_set_collect_epilogue) when the wrapped env is the device engine without a host recorder
+        eng = getattr(venv, "engine", None)
+        self._epi_ok = (eng is not None and getattr(venv, "_hists", None) is None and hasattr(eng, "collect_records")
+                        and d + 1 <= 33)
+        self._records, self._n_rec, self._epi_last = None, None, False
+        if self._epi_ok:
+            self._records = torch.empty(eng.collect_records()[1] * (1 + 2 * (d + 1)), dtype=torch.float64, device=dev)
 
     # --------------------------------------------------------------- internals
     def _world(self):
@@ -197,7 +205,15 @@ class VecNormalize:
     # local (env step + this shard's moments) | exchange (RCCL all-gather of the records) | finish
     # (update_from_moments in rank order, normalisation).  Phase 1 and 3 launch only kernels.
     def step_wait_local(self):
-        obs, rews, news, infos = self.venv.step_wait()
+        epi = self._epi_ok and self.training
+        if epi:  # only around this wrapper's own env step: a direct step of the inner env leaves ret alone
+            self.set_epilogue()
+        try:
+            obs, rews, news, infos = self.venv.step_wait()
+        finally:
+            if epi:
+                self.venv.engine.set_collect_epilogue()
+        self._epi_last = epi
         obs = obs.to(torch.float32).contiguous()
         rews = rews.to(torch.float32).contiguous()
         self.old_obs, self.old_reward = obs, rews
@@ -205,7 +221,10 @@ class VecNormalize:
         u8 = news.view(torch.uint8) if (news.dtype == torch.bool and news.is_contiguous()) else news.to(torch.uint8)
         self._news, self._infos, self._done_u8 = news, infos, u8.contiguous()
         if self.training:
-            self._moments(obs, rews)
+            if not epi:
+                self._moments(obs, rews)
+            elif self.exchanged():  # this shard's record, for the exchange
+                self.merge_records(self._rec)
 
     def step_exchange(self):
         if self.training:
@@ -213,8 +232,41 @@ class VecNormalize:
 
     def step_wait_finish(self):
         if self.training:
-            self._merge()
+            if self._epi_last and not self.exchanged():
+                self.merge_update()
+            else:
+                self._merge()
         self._apply(self.old_obs, self.old_reward, self._done_u8)
+
+    # ---- the fused path: records from the env step's epilogue (fwsim.h fw_set_collect_epilogue)
+    def exchanged(self):
+        """The statistics combine several records (a process group, or a caller stacking shard records)."""
+        return self._parts.shape[0] > 1 or (dist.is_available() and dist.is_initialized())
+
+    @property
+    def fused_stats(self):
+        """The env step writes this wrapper's moment records and return update (training on the engine)."""
+        return self._epi_ok and self.training
+
+    def set_epilogue(self, row_ctrl=None):
+        """Point the engine's collect epilogue at this wrapper's return and record buffers (and, for a
+        captured collect step, the rollout row counter)."""
+        eng = self.venv.engine
+        eng.set_collect_epilogue(ret=self.ret, gamma=self.gamma, records=self._records, row_ctrl=row_ctrl)
+        self._n_rec = eng.collect_records()[0]
+
+    def merge_records(self, out):
+        """fw_moments_merge of the env step's block records into one (obs + return) record."""
+        d = self.obs_dim
+        _native.check(self.lib.fw_moments_merge(_p(self._records), self._n_rec, d + 1, _p(out), self._s()),
+                      "fw_moments_merge")
+
+    def merge_update(self):
+        """fw_vecnorm_merge_update: the records merged and applied to the running statistics, one launch
+        (the merged record also lands in _rec)."""
+        d = self.obs_dim
+        _native.check(self.lib.fw_vecnorm_merge_update(_p(self._records), self._n_rec, d, 1, _p(self.rms),
+                                                       _p(self._rec), self._s()), "fw_vecnorm_merge_update")
         news, infos = self._news, self._infos
         if self.return_tensors:
             return self.obs_out, self.rew_out, news, infos
@@ -225,7 +277,7 @@ class VecNormalize:
         """Host-side choices a captured step bakes in (RolloutCollector recaptures when this changes)."""
         inner = self.venv.graph_key() if hasattr(self.venv, "graph_key") else None
         return (self.training, self.norm_obs, self.norm_reward, self.clip_obs, self.clip_reward, self.gamma,
-                self.epsilon, self._world(), inner)
+                self.epsilon, self._world(), self._epi_ok, inner)
 
     def step(self, actions):
         self.step_async(actions)
