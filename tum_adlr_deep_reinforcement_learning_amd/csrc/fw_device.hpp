@@ -355,7 +355,7 @@ FW_HD void fatan2_2(float y0, float x0, float y1, float x1, float& r0, float& r1
 // ---------------------------------------------------------------------------
 FW_HD bool any_lane(bool p) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return __any(p);
+  return __builtin_amdgcn_ballot_w64(p) != 0;  // an SGPR mask test (the __any form round-trips through a VGPR)
 #else
   return p;
 #endif
@@ -773,26 +773,30 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
   // accepted or rejected; see rk45_quad_core): one trial step is written out with its six RHS sites,
   // so the accumulators have static lifetimes instead of merging at a stage switch.
   bool begin_step = false;
-  // K = f(ys); false once no lane of the wave integrates any more
-  auto eval = [&](bool first) {
+  // K = f(ys) at evaluation site k of a sequence that started with `nfev` evaluations done (f0 / probe:
+  // k = 1 / 2 from 0; a trial step: k = 1..6 from its start, nfev += 6 at its step control).  `room` =
+  // evaluations left before the max_nfev budget, set at the sequence start, so the common path is one
+  // compare against the site's constant plus the violated-condition test (counting per evaluation cost ~9
+  // VALU per RHS on the lone-wave tail).  A lane stops on a violated condition (result = its code) or when
+  // this evaluation reaches the budget (hard bound on the work of one step so that no input can keep a wave
+  // spinning; scipy has none; ends the step like its TOO_SMALL_STEP failure, reported in the stats).
+  // Returns false once no lane of the wave integrates any more.
+  int room = c.max_nfev;
+  auto eval = [&](bool first, int k) {
     const int term = rhs(c, a, X, first, (const T*)ys, (T*)K);
     K[NP - 1].y = T(0);  // pad element
-    if (active) {
-      nfev++;
-      if (term) {
-        result = term;
+    const bool stop = active && (term != 0 || k >= room);
+    if (any_lane(stop)) {
+      if (stop) {
+        result = term ? term : -2;
+        nfev += k;
         active = false;
       }
-      // hard bound on work per step so that no input can keep a wave spinning (scipy has
-      // none; ends the step like its TOO_SMALL_STEP failure, reported in the stats)
-      else if (nfev >= c.max_nfev) {
-        result = -2;
-        active = false;
-      }
+      return any_lane(active);
     }
-    return any_lane(active);
+    return true;  // every lane that was integrating still is (the caller only evaluates while one is)
   };
-  if (!eval(true)) goto rk_done;
+  if (!eval(true, 1)) goto rk_done;
   {  // ---- f0; select_initial_step (common.py:68-110)
     T d0s = T(0), d1s = T(0);
 #pragma unroll
@@ -810,7 +814,8 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
 #pragma unroll
     for (int p = 0; p < NP; p++) ys[p] = Y(p) + h0t * F(p);
   }
-  if (!eval(false)) goto rk_done;
+  if (!eval(false, 2)) goto rk_done;
+  if (active) nfev = 2;
   {  // ---- probe; select_initial_step (common.py:111-134)
     T d2s = T(0);
 #pragma unroll
@@ -828,6 +833,7 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
       if (h_abs < min_step) h_abs = min_step;
       rejected = false;
     }
+    room = c.max_nfev - nfev;
     {  // one trial step (rk.py:126-137); stage 1 input, accumulators seeded
       double h = h_abs;
       t_new = t + h;
@@ -857,7 +863,7 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
       }
     }
 #endif
-    if (!eval(false)) break;  // K1
+    if (!eval(false, 1)) break;  // K1
 #pragma unroll
     for (int p = 0; p < NP; p++) {
       ys[p] = Y(p) + (P2v[p] + K[p] * T(A21)) * ht;
@@ -865,7 +871,7 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
       PA(P4, p) += K[p] * T(A41);
       PA(P5, p) += K[p] * T(A51);
     }
-    if (!eval(false)) break;  // K2
+    if (!eval(false, 2)) break;  // K2
 #pragma unroll
     for (int p = 0; p < NP; p++) {
       PA(P3, p) += K[p] * T(A32);
@@ -875,7 +881,7 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
       ERV(p) += K[p] * T(E2);
       ys[p] = Y(p) + PA(P3, p) * ht;
     }
-    if (!eval(false)) break;  // K3
+    if (!eval(false, 3)) break;  // K3
 #pragma unroll
     for (int p = 0; p < NP; p++) {
       PA(P4, p) += K[p] * T(A43);
@@ -884,7 +890,7 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
       ERV(p) += K[p] * T(E3);
       ys[p] = Y(p) + PA(P4, p) * ht;
     }
-    if (!eval(false)) break;  // K4
+    if (!eval(false, 4)) break;  // K4
 #pragma unroll
     for (int p = 0; p < NP; p++) {
       PA(P5, p) += K[p] * T(A54);
@@ -892,14 +898,15 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
       ERV(p) += K[p] * T(E4);
       ys[p] = Y(p) + PA(P5, p) * ht;
     }
-    if (!eval(false)) break;  // K5; ys <- y_new
+    if (!eval(false, 5)) break;  // K5; ys <- y_new
 #pragma unroll
     for (int p = 0; p < NP; p++) {
       PA(YB, p) += K[p] * T(B5);
       ERV(p) += K[p] * T(E5);
       ys[p] = Y(p) + ht * PA(YB, p);
     }
-    if (!eval(false)) break;  // K = f(t_new, y_new): error norm + step control (rk.py:138-173)
+    if (!eval(false, 6)) break;  // K = f(t_new, y_new): error norm + step control (rk.py:138-173)
+    if (active) nfev += 6;
     {
       T es = T(0);
 #pragma unroll

@@ -408,20 +408,22 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
     return s;
   };
   auto sq2 = [](V v) { return v.x * v.x + v.y * v.y; };
-  // K = f(ys); false once no lane of the wave integrates any more
-  auto eval = [&](bool first) {
+  // K = f(ys) at evaluation site k of a sequence begun with `nfev` evaluations done; `room` = evaluations
+  // left before the budget (the bookkeeping of rk45()'s eval: one compare per evaluation, the count
+  // updated per sequence).  False once no lane of the wave integrates any more.
+  int room = c.max_nfev;
+  auto eval = [&](bool first, int k) {
     const int term = rhs_quad(c, a, Q, first, (const T*)ys, (T*)K);
-    if (active) {
-      nfev++;
-      if (term) {
-        result = term;
-        active = false;
-      } else if (nfev >= c.max_nfev) {
-        result = -2;
+    const bool stop = active && (term != 0 || k >= room);
+    if (any_lane(stop)) {
+      if (stop) {
+        result = term ? term : -2;
+        nfev += k;
         active = false;
       }
+      return any_lane(active);
     }
-    return any_lane(active);
+    return true;
   };
   auto seed = [&]() {  // stage-1 input and accumulators of a trial step
 #pragma unroll
@@ -450,7 +452,7 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
   } else {
 #pragma unroll
     for (int p = 0; p < NQ; p++) ys[p] = Y[p];
-    if (!eval(true)) goto done;
+    if (!eval(true, 1)) goto done;
     T d1;
     double h0;
     {  // f0; select_initial_step (common.py:68-110)
@@ -470,7 +472,8 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
 #pragma unroll
       for (int p = 0; p < NQ; p++) ys[p] = Y[p] + h0t * F[p];
     }
-    if (!eval(false)) goto done;
+    if (!eval(false, 2)) goto done;
+    if (active) nfev = 2;
     {  // probe; select_initial_step (common.py:111-134)
       T d2s = T(0);
 #pragma unroll
@@ -500,7 +503,8 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
       seed();
     }
     seeded = false;
-    if (!eval(false)) break;  // K1
+    room = c.max_nfev - nfev;
+    if (!eval(false, 1)) break;  // K1
 #pragma unroll
     for (int p = 0; p < NQ; p++) {
       ys[p] = Y[p] + (P2v[p] + K[p] * T(A21)) * ht;
@@ -508,7 +512,7 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
       P4[p] += K[p] * T(A41);
       P5[p] += K[p] * T(A51);
     }
-    if (!eval(false)) break;  // K2
+    if (!eval(false, 2)) break;  // K2
 #pragma unroll
     for (int p = 0; p < NQ; p++) {
       P3[p] += K[p] * T(A32);
@@ -518,7 +522,7 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
       ER[p] += K[p] * T(E2);
       ys[p] = Y[p] + P3[p] * ht;
     }
-    if (!eval(false)) break;  // K3
+    if (!eval(false, 3)) break;  // K3
 #pragma unroll
     for (int p = 0; p < NQ; p++) {
       P4[p] += K[p] * T(A43);
@@ -527,7 +531,7 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
       ER[p] += K[p] * T(E3);
       ys[p] = Y[p] + P4[p] * ht;
     }
-    if (!eval(false)) break;  // K4
+    if (!eval(false, 4)) break;  // K4
 #pragma unroll
     for (int p = 0; p < NQ; p++) {
       P5[p] += K[p] * T(A54);
@@ -535,14 +539,15 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
       ER[p] += K[p] * T(E4);
       ys[p] = Y[p] + P5[p] * ht;
     }
-    if (!eval(false)) break;  // K5; ys <- y_new
+    if (!eval(false, 5)) break;  // K5; ys <- y_new
 #pragma unroll
     for (int p = 0; p < NQ; p++) {
       YB[p] += K[p] * T(B5);
       ER[p] += K[p] * T(E5);
       ys[p] = Y[p] + ht * YB[p];
     }
-    if (!eval(false)) break;  // K = f(t_new, y_new): error norm + step control (rk.py:138-173)
+    if (!eval(false, 6)) break;  // K = f(t_new, y_new): error norm + step control (rk.py:138-173)
+    if (active) nfev += 6;
     T es = T(0);
 #pragma unroll
     for (int p = 0; p < NQ; p++) {
