@@ -1159,13 +1159,21 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_env_step(const DevCfg<T>
   static_assert(Q != 1 || RP || FW_TAIL_QUAD == 0 || BLOCK == 64, "the tail handoff works per one-wave block");
   __shared__ qd::HoSlot<T> ho[Q == 1 && !RP ? BLOCK : 1];
   static_assert(BLOCK == 64, "collect_epilogue: one-wave blocks");
-  __shared__ float col_x[64 * COL_MAXD];
-  __shared__ double col_r[64];
+  // the epilogue's staging (64 rows x COL_MAXD floats + 64 doubles) reuses the integrator's LDS slots once
+  // the step is done (one-lane instances; LDS bounds how many fp64 blocks fit a CU); quads get their own
+  constexpr size_t COL_BYTES = 64 * COL_MAXD * sizeof(float) + 64 * sizeof(double);
+  constexpr bool COL_ALIAS = sizeof(lds) >= COL_BYTES;
+  __shared__ double col_sep[COL_ALIAS ? 1 : COL_BYTES / sizeof(double)];
+  char* const col_base = COL_ALIAS ? (char*)lds : (char*)col_sep;
+  float* const col_x = (float*)col_base;
+  double* const col_r = (double*)(col_base + 64 * COL_MAXD * sizeof(float));
   if (i < s.n)
     env_step_lane<T, C, RP, Q, ((Q == 4 && (sizeof(T) == 4 || FW_PREF_Q4_F64)) || FW_PREF_Q1)>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out,
                                                     episode_out, stats, auto_reset, (int)(tid % Q), ho);
-  if (collect)
+  if (collect) {
+    if (COL_ALIAS) __syncthreads();  // (one wave: orders the slot reuse after the integrator's last accesses)
     collect_epilogue<T>(s, i, i < s.n && tid % Q == 0, c.n_obs * c.obs_len, obs_out, rew_out, done_out, col_x, col_r);
+  }
 }
 
 // One env step of k_env_rollout.  fp32: inlined, and scratch-free since the step loop re-materialises

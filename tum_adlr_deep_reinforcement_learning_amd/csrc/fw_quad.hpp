@@ -847,11 +847,15 @@ __device__ __forceinline__ int rk45_quad(const C& c, const A& a, const StepCtx<T
 // slots (the quads read and write them in place); the step-control state and the step context go
 // through a per-wave LDS slot array.  Quad k (lanes 4k..4k+3) takes the k-th integrating lane.
 // ---------------------------------------------------------------------------
+// 160 B in fp64 (QRun's fields unpadded, `rejected` in src's bit 8): 64 slots + the one-lane LDS state
+// = 40 KB, four one-wave blocks per CU (at 168 B the fp64 one-lane instances fit three)
 template <typename T>
 struct HoSlot {
-  QRun R;
+  double t, t_new, h_abs, min_step;
   StepCtx<T> X;
-  int src, result;
+  int nfev, nacc;
+  int src;  // source lane | rejected << 8
+  int result;
 };
 
 // true on the handed-off lanes, whose R (nfev, nacc) and result are then the integration's
@@ -864,15 +868,20 @@ __device__ __forceinline__ bool handoff(const C& c, const A& a, const StepCtx<T>
   const int na = __popcll(am);
   const int kk = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(am >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)am, 0u));
   if (active) {
-    st[kk].R = R;
+    st[kk].t = R.t;
+    st[kk].t_new = R.t_new;
+    st[kk].h_abs = R.h_abs;
+    st[kk].min_step = R.min_step;
+    st[kk].nfev = R.nfev;
+    st[kk].nacc = R.nacc;
     st[kk].X = X;
-    st[kk].src = lane;
+    st[kk].src = lane | (R.rejected ? 256 : 0);
   }
   __syncthreads();
   const int k = lane >> 2, r = lane & 3;
   if (k < na) {
-    const int src = st[k].src;
-    QRun Rq = st[k].R;
+    const int src = st[k].src & 255;
+    QRun Rq{st[k].t, st[k].t_new, st[k].h_abs, st[k].min_step, st[k].src >> 8, st[k].nfev, st[k].nacc};
     const StepCtx<T> Xs = st[k].X;
     const QCtx<T> Q = qctx<T>(c, Xs, r);
     V2<T>* const ysrc = sy - lane + src;
@@ -897,15 +906,15 @@ __device__ __forceinline__ bool handoff(const C& c, const A& a, const StepCtx<T>
     }
     if (r == 0) {
       st[k].result = res;
-      st[k].R.nfev = Rq.nfev;
-      st[k].R.nacc = Rq.nacc;
+      st[k].nfev = Rq.nfev;
+      st[k].nacc = Rq.nacc;
     }
   }
   __syncthreads();
   if (active) {
     result = st[kk].result;
-    R.nfev = st[kk].R.nfev;
-    R.nacc = st[kk].R.nacc;
+    R.nfev = st[kk].nfev;
+    R.nacc = st[kk].nacc;
   }
   return active;
 }
