@@ -237,6 +237,11 @@ class VecNormalize:
             else:
                 self._merge()
         self._apply(self.old_obs, self.old_reward, self._done_u8)
+        news, infos = self._news, self._infos
+        if self.return_tensors:
+            return self.obs_out, self.rew_out, news, infos
+        return self.obs_out.cpu().numpy(), self.rew_out.cpu().numpy().astype(np.float64), \
+            news.cpu().numpy().astype(bool), infos
 
     # ---- the fused path: records from the env step's epilogue (fwsim.h fw_set_collect_epilogue)
     def exchanged(self):
@@ -267,11 +272,6 @@ class VecNormalize:
         d = self.obs_dim
         _native.check(self.lib.fw_vecnorm_merge_update(_p(self._records), self._n_rec, d, 1, _p(self.rms),
                                                        _p(self._rec), self._s()), "fw_vecnorm_merge_update")
-        news, infos = self._news, self._infos
-        if self.return_tensors:
-            return self.obs_out, self.rew_out, news, infos
-        return self.obs_out.cpu().numpy(), self.rew_out.cpu().numpy().astype(np.float64), \
-            news.cpu().numpy().astype(bool), infos
 
     def graph_key(self):
         """Host-side choices a captured step bakes in (RolloutCollector recaptures when this changes)."""
