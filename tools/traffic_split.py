@@ -23,7 +23,8 @@ from tum_adlr_deep_reinforcement_learning_amd.engine import Engine  # noqa: E402
 
 def main():
     n, K, prep = 65536, 20, int(os.environ.get("SPLIT_PREP", "1000"))
-    spec = C.EnvSpec(sim_config_kw={"turbulence": False})
+    kw = {"steps_max": int(os.environ["SPLIT_STEPS_MAX"])} if os.environ.get("SPLIT_STEPS_MAX") else None
+    spec = C.EnvSpec(config_kw=kw, sim_config_kw={"turbulence": False})
     eng = Engine(spec.sim, spec, n, device="cuda:0", precision="float32")
     eng.seed(1234)
     eng.reset()
@@ -35,14 +36,18 @@ def main():
     for _ in range(K):
         eng.env_step(zero)
         quiet.append(int(eng.done.sum()))
+    prep_dones = []
     for s in range(prep):
         eng.env_step(pool[s % 16])
+        prep_dones.append(eng.done.sum())
+    prep_dones = [int(x) for x in torch.stack(prep_dones).cpu()] if prep else []
     steady = []
     for s in range(K):
         eng.env_step(pool[s % 16])
         steady.append(int(eng.done.sum()))
     torch.cuda.synchronize()
     print(json.dumps({"n": n, "window": K, "prep": prep, "noreset_dones": quiet, "steady_dones": steady,
+                      "prep_dones": prep_dones, "steps_max": spec.steps_max,
                       "dispatches": {"noreset": [0, K], "steady": [K + prep, 2 * K + prep]}}))
     eng.close()
 

@@ -216,36 +216,77 @@ __global__ __launch_bounds__(BLOCK) void k_moments_partial(const float* __restri
   if (threadIdx.x == 0) out[0] = dn;
 }
 
-// merges `parts` records (stride 1+2D) into one: one wave per column (MERGE_WAVES waves, all columns
-// at once for D <= 16), lane l holds records l, l+64, ...
-constexpr int MERGE_WAVES = 16;
+// merges `parts` records (stride 1+2D) into one, two-pass: mean = sum n_b mean_b / N, then
+// M2 = sum (M2_b + n_b (mean_b - mean)^2).  The whole block (MERGE_THREADS) works on it: thread t folds
+// records t, t + MERGE_THREADS, ... (every column at once, so each record is read once per pass), then a
+// wave butterfly, then the waves in order -- a fixed order, so the result is deterministic.  (Round 3's one
+// wave per column walked the records serially: 20 us for the 1024 block records of a 65536-env step.)
+constexpr int MERGE_THREADS = 256;  // 4 waves: the 33 fp64 column accumulators fit without spilling
+constexpr int MERGE_WAVES = MERGE_THREADS / 64;
 __device__ __forceinline__ void merge_records(const double* __restrict__ part, int parts, int D, double* __restrict__ out) {
+  __shared__ double wsum[MERGE_WAVES][MAXD + 1];  // per-wave partial sums; [MAXD]: the count
+  __shared__ double smean[MAXD + 1];              // column means; [MAXD]: N
   const int S = 1 + 2 * D;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int j = w; j < D; j += MERGE_WAVES) {
-    double cn = 0.0, cs = 0.0;
-    for (int k = lane; k < parts; k += 64) {
-      const double nk = part[(int64_t)k * S];
-      cn += nk;
-      cs += nk * part[(int64_t)k * S + 1 + j];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  double acc[MAXD], cn = 0.0;
+#pragma unroll
+  for (int j = 0; j < MAXD; j++) acc[j] = 0.0;
+  for (int k = tid; k < parts; k += MERGE_THREADS) {  // pass 1
+    const double* r = part + (int64_t)k * S;
+    const double nk = r[0];
+    cn += nk;
+#pragma unroll
+    for (int j = 0; j < MAXD; j++)
+      if (j < D) acc[j] += nk * r[1 + j];
+  }
+  cn = wave_sum(cn);
+  if (lane == 0) wsum[w][MAXD] = cn;
+#pragma unroll
+  for (int j = 0; j < MAXD; j++)
+    if (j < D) {
+      const double v = wave_sum(acc[j]);
+      if (lane == 0) wsum[w][j] = v;
     }
-    const double N = wave_sum(cn);
-    const double mean = wave_sum(cs) / N;
-    double cq = 0.0;
-    for (int k = lane; k < parts; k += 64) {
-      const double dm = part[(int64_t)k * S + 1 + j] - mean;
-      cq += part[(int64_t)k * S + 1 + D + j] + part[(int64_t)k * S] * (dm * dm);
+  __syncthreads();
+  if (tid <= D) {  // thread j: column j's sum over the waves in order; thread D: N
+    const int j = tid == D ? MAXD : tid;
+    double a = 0.0;
+    for (int q = 0; q < MERGE_WAVES; q++) a += wsum[q][j];
+    smean[j] = a;
+  }
+  __syncthreads();
+  const double N = smean[MAXD];
+  if (tid < D) smean[tid] = smean[tid] / N;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < MAXD; j++) acc[j] = 0.0;
+  for (int k = tid; k < parts; k += MERGE_THREADS) {  // pass 2
+    const double* r = part + (int64_t)k * S;
+    const double nk = r[0];
+#pragma unroll
+    for (int j = 0; j < MAXD; j++)
+      if (j < D) {
+        const double dm = r[1 + j] - smean[j];
+        acc[j] += r[1 + D + j] + nk * (dm * dm);
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < MAXD; j++)
+    if (j < D) {
+      const double v = wave_sum(acc[j]);
+      if (lane == 0) wsum[w][j] = v;
     }
-    const double M2 = wave_sum(cq);
-    if (lane == 0) {
-      if (j == 0) out[0] = N;
-      out[1 + j] = mean;
-      out[1 + D + j] = M2;
-    }
+  __syncthreads();
+  if (tid < D) {
+    double a = 0.0;
+    for (int q = 0; q < MERGE_WAVES; q++) a += wsum[q][tid];
+    out[1 + tid] = smean[tid];
+    out[1 + D + tid] = a;
+    if (tid == 0) out[0] = N;
   }
 }
 
-__global__ __launch_bounds__(64 * MERGE_WAVES) void k_moments_merge(const double* __restrict__ part, int parts, int D,
+__global__ __launch_bounds__(MERGE_THREADS) void k_moments_merge(const double* __restrict__ part, int parts, int D,
                                                                     double* __restrict__ out) {
   merge_records(part, parts, D, out);
 }
@@ -300,7 +341,7 @@ __global__ void k_rms_update(const double* __restrict__ parts, int n_parts, int 
 
 // k_moments_merge + k_rms_update of the single merged record in one launch (the unsharded statistics
 // update of a collect step): the same device functions, so the same bits as the two launches.
-__global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge_update(const double* __restrict__ part, int parts, int d,
+__global__ __launch_bounds__(MERGE_THREADS) void k_merge_update(const double* __restrict__ part, int parts, int d,
                                                                    int has_ret, double* __restrict__ rms,
                                                                    double* __restrict__ rec_out) {
   __shared__ double rec[1 + 2 * MAXD];
@@ -695,28 +736,76 @@ __global__ __launch_bounds__(64 * PM_WAVES) void k_policy_mfma(PolArgs G) {
   float* val = G.val + row * n;
   float* logp = G.logp + row * n;
   const float half_log_2pi = 0.91893853320467274f;
+  // per-action constants, loaded once (uniform: scalar registers), not per tile inside the lane-divergent
+  // action stage (where each load waited for every outstanding load, the next tile's prefetch included)
+  float lsA[POL_MAXA], sdA[POL_MAXA], hiA[POL_MAXA], loA[POL_MAXA];
+#pragma unroll
+  for (int a = 0; a < POL_MAXA; a++) {
+    lsA[a] = a < A ? G.P.log_std[a] : 0.0f;
+    sdA[a] = expf(lsA[a]);
+    hiA[a] = (a < A && G.clipped) ? G.high[a] : 0.0f;
+    loA[a] = (a < A && G.clipped) ? G.low[a] : 0.0f;
+  }
 
   const int64_t tiles = (n + 15) / 16;
   const int64_t wid = (int64_t)blockIdx.x * PM_WAVES + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * PM_WAVES;
+  // A tile's inputs are loaded one tile ahead (their HBM latency hides under the previous tile's MFMAs):
+  // the raw observation features of this lane, and -- for the row stores -- the previous step's reward and
+  // done flag (lanes g == 1) and this step's noise draws (lanes g == 0).  Restrict-qualified locals: the
+  // output stores cannot alias the inputs, so the loads are not serialised behind them.
+  const float* __restrict__ obs_in = G.obs;
+  const float* __restrict__ rew_in = G.reward;
+  const uint8_t* __restrict__ done_in = G.done;
+  const float* __restrict__ noise_in = noise;
+  const bool rows_prev = G.ctrl && row >= 1;
+  struct In {
+    float o[S];
+    float r;
+    uint32_t dn;
+    float z[POL_MAXA];
+  };
+  // branch-free, and not selected on load: every lane loads from a clamped, valid address straight into the
+  // register it is consumed from one tile later; the validity masks apply at the use (a select right after
+  // the load, or a load inside an exec-masked block, makes the compiler wait for it there)
+  auto fetch = [&](int64_t t, In& in) {
+    const int64_t e = t * 16 + c16;
+    const int64_t ec = (t < tiles && e < n) ? e : 0;
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const int f = 4 * s + g;
+      in.o[s] = obs_in[ec * d + (f < d ? f : d - 1)];
+    }
+    if (rows_prev) {
+      in.r = rew_in[ec];
+      in.dn = done_in[ec];
+    }
+#pragma unroll
+    for (int a = 0; a < POL_MAXA; a++)
+      if (noise_in && a < A) in.z[a] = noise_in[ec * A + a];
+  };
+  In nxt{};
+  fetch(wid, nxt);
   for (int64_t tile = wid; tile < tiles; tile += nw) {
     const int64_t env = tile * 16 + c16;
     const bool valid = env < n;
+    const In cur = nxt;
+    fetch(tile + nw, nxt);
     // ---- observation (normalised) = B operands of layer 0; the rollout's observation row
     float x[S];
 #pragma unroll
     for (int s = 0; s < S; s++) {
       const int f = 4 * s + g;
-      float o = (valid && f < d) ? G.obs[env * d + f] : 0.0f;
+      float o = (valid && f < d) ? cur.o[s] : 0.0f;
       if (nobs && valid && f < d) o = norm_obs_val(o, mean[s], den[s], G.clip_obs);
       x[s] = o;
       if (obs_rows && valid && f < d) obs_rows[env * d + f] = o;
     }
     // ---- the previous step's reward row (normalised) and the episode starts of this row
-    if (G.ctrl && row >= 1 && g == 1 && valid) {
-      double r = (double)G.reward[env];
+    if (rows_prev && g == 1 && valid) {
+      double r = (double)cur.r;
       if (G.rms && G.norm_rew) r = fmin(fmax(r / rden, -G.clip_rew), G.clip_rew);
       G.rew_rows[(row - 1) * n + env] = (float)r;
-      G.start_rows[row * n + env] = G.done[env];
+      G.start_rows[row * n + env] = (uint8_t)cur.dn;
     }
     // ---- layer 0 (8 independent accumulators)
     f32x4 cp[4], cv[4];
@@ -780,14 +869,14 @@ __global__ __launch_bounds__(64 * PM_WAVES) void k_policy_mfma(PolArgs G) {
       for (int a = 0; a < POL_MAXA; a++) {
         if (a < A) {
           const float m = a < 4 ? out[a & 3] : hi[a & 3];
-          const float ls = G.P.log_std[a];
-          const float sd = expf(ls);
+          const float ls = lsA[a];
+          const float sd = sdA[a];
           // the module's arithmetic (rollout.py MlpActorCritic.forward): separate mul / add, as torch's kernels
-          const float ac = noise ? m + sd * noise[env * A + a] : m;
+          const float ac = noise ? m + sd * cur.z[a] : m;
           const float dv = ac - m;
           lp = lp + (((-(dv * dv)) / ((2.0f * sd) * sd) - ls) - half_log_2pi);
           act[env * A + a] = ac;
-          if (G.clipped) G.clipped[env * A + a] = fmaxf(fminf(ac, G.high[a]), G.low[a]);
+          if (G.clipped) G.clipped[env * A + a] = fmaxf(fminf(ac, hiA[a]), loA[a]);
         }
       }
       logp[env] = lp;
@@ -880,7 +969,7 @@ int fw_moments(const float* x, int64_t n, int32_t d, int64_t ldx, const float* r
   double* part = (double*)workspace;
   hipLaunchKernelGGL(k_moments_partial, dim3((unsigned)parts), dim3(BLOCK), 0, s, x, n, d, ldx, rew, ret, gamma, part);
   FW_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_moments_merge, dim3(1), dim3(64 * std::min(D, MERGE_WAVES)), 0, s, part, (int)parts, D, out);
+  hipLaunchKernelGGL(k_moments_merge, dim3(1), dim3(MERGE_THREADS), 0, s, part, (int)parts, D, out);
   FW_HIP(hipGetLastError());
   return FW_OK;
 }
@@ -1000,7 +1089,7 @@ int fw_policy_forward(const fw_mlp_policy* p, const float* obs, int64_t n, const
 int fw_moments_merge(const double* records, int32_t n_records, int32_t D, double* out, void* stream) {
   if (!records || !out || n_records < 1 || D < 1 || D > MAXD)
     return fw::set_error(FW_E_INVALID, "fw_moments_merge: bad arguments");
-  hipLaunchKernelGGL(k_moments_merge, dim3(1), dim3(64 * std::min<int>(D, MERGE_WAVES)), 0, (hipStream_t)stream, records,
+  hipLaunchKernelGGL(k_moments_merge, dim3(1), dim3(MERGE_THREADS), 0, (hipStream_t)stream, records,
                      (int)n_records, (int)D, out);
   FW_HIP(hipGetLastError());
   return FW_OK;
@@ -1011,7 +1100,7 @@ int fw_vecnorm_merge_update(const double* records, int32_t n_records, int32_t d,
   const int D = d + (has_ret ? 1 : 0);
   if (!records || !rms || n_records < 1 || d < 0 || D < 1 || D > MAXD)
     return fw::set_error(FW_E_INVALID, "fw_vecnorm_merge_update: bad arguments");
-  hipLaunchKernelGGL(k_merge_update, dim3(1), dim3(64 * MERGE_WAVES), 0, (hipStream_t)stream, records, (int)n_records,
+  hipLaunchKernelGGL(k_merge_update, dim3(1), dim3(MERGE_THREADS), 0, (hipStream_t)stream, records, (int)n_records,
                      (int)d, (int)(has_ret != 0), rms, rec_out);
   FW_HIP(hipGetLastError());
   return FW_OK;
