@@ -94,11 +94,13 @@ struct State {
   T* target;       // [3][ld]
   T* cmd;          // [3][ld] last constrained commands
   T* ep_ret;       // [ld]
-  T* act_ring;     // [act_window][3][ld]
-  T* cmd_ring;     // [cmd_window][3][ld] or null
+  T* act_ring;     // [act_window][3][ld], action k of an episode in slot (L_ep + k - 1) % act_window
+  T* cmd_ring;     // [cmd_window][3][ld] or null, the same slots
   uint32_t* steps;    // [ld]: steps_count | steps_for_current_target << 16
   uint32_t* goal;     // [4][ld] 128-bit goal history shift register (bit 0 newest)
   uint32_t* episode;  // [ld]
+  uint32_t* life;     // [ld] env steps since the handle was created (never reset): every launch steps every
+                      // aircraft, so the value is the same on all lanes -- ring slots are indexed by it (below)
   const T* noise;     // injected N(0,1) turbulence noise [4][noise_len][ld] or null
   int64_t noise_len;
   int32_t* noise_env_len;  // [ld] per-env injected length (0: Philox; zeroed by the auto-reset) or null: all
@@ -108,7 +110,7 @@ struct State {
   uint32_t* metu;     // [MU_ROWS][ld] their counters / indices
   T* met_out;         // [FW_NMETRIC][N] (SoA) record of done envs (null: not requested)
   T* obs_init;        // [n_obs][ld] raw observation row at the episode's reset (null: length-1 observations)
-  T* obs_ring;        // [obs_hist][n_obs][ld] raw rows of past steps, slot = step % obs_hist
+  T* obs_ring;        // [obs_hist][n_obs][ld] raw rows of past steps, slot = (L_ep + step) % obs_hist
   T* prm;             // [FW_NPARAM][ld] per-aircraft parameters (null: no randomisation)
   // collect epilogue of k_env_step (fw_set_collect_epilogue; all null: off)
   double* col_ret;    // [n] VecNormalize discounted return, or null
@@ -277,7 +279,7 @@ constexpr int OBS_STEP = 0, OBS_FAIL = 1, OBS_RESET = 2, OBS_PEEK = 3;
 template <typename T>
 __device__ __forceinline__ void observe_full(const DevCfg<T>& c, const State<T>& s, int64_t i, uint32_t episode,
                                           int mode, const T* y, const T* der, const T* tgt, int steps,
-                                          const T (*seqA)[3], const T (*seqC)[3], T* out) {
+                                          const T (*seqA)[3], const T (*seqC)[3], T* out, uint32_t lep) {
   const int64_t ld = s.ld;
   const int nr = c.n_obs;
   const bool hist = c.obs_hist > 0;
@@ -301,7 +303,8 @@ __device__ __forceinline__ void observe_full(const DevCfg<T>& c, const State<T>&
         v = obs_raw(c, E, y, der, tgt, steps, seqA, seqC);
       } else if (!clamp) {
         const int at = (mode == OBS_FAIL && !act) ? steps - lag : steps - lag + 1;  // step whose row holds it
-        v = at <= 0 ? s.obs_init[(int64_t)o * ld + i] : s.obs_ring[((int64_t)(at % c.obs_hist) * nr + o) * ld + i];
+        v = at <= 0 ? s.obs_init[(int64_t)o * ld + i]
+                    : s.obs_ring[((int64_t)((lep + (uint32_t)at) % (uint32_t)c.obs_hist) * nr + o) * ld + i];
       } else if (act || steps == 0) {
         v = obs_raw(c, E, y, der, tgt, 0, seqA, seqC);  // current values (steps_count - i < 0 branch)
       } else {
@@ -319,7 +322,8 @@ __device__ __forceinline__ void observe_full(const DevCfg<T>& c, const State<T>&
     }
   }
   if (hist && (mode == OBS_RESET || mode == OBS_STEP)) {  // this step's raw row for later lags
-    T* dst = mode == OBS_RESET ? s.obs_init : s.obs_ring + (int64_t)(steps % c.obs_hist) * nr * ld;
+    T* dst = mode == OBS_RESET ? s.obs_init
+                               : s.obs_ring + (int64_t)((lep + (uint32_t)steps) % (uint32_t)c.obs_hist) * nr * ld;
     for (int o = 0; o < nr; o++) dst[(int64_t)o * ld + i] = obs_raw(c, c.obs[o], y, der, tgt, steps, seqA, seqC);
   }
 }
@@ -329,8 +333,8 @@ __device__ __forceinline__ void observe_full(const DevCfg<T>& c, const State<T>&
 template <typename T, typename C>
 __device__ __forceinline__ void observe_env(const C& c, const State<T>& s, int64_t i, uint32_t episode, int mode,
                                             const T* y, const T* der, const T* tgt, int steps, const T (*seqA)[3],
-                                            const T (*seqC)[3], T* out) {
-  if (c.obs_general) observe_full<T>(c, s, i, episode, mode, y, der, tgt, steps, seqA, seqC, out);
+                                            const T (*seqC)[3], T* out, uint32_t lep) {
+  if (c.obs_general) observe_full<T>(c, s, i, episode, mode, y, der, tgt, steps, seqA, seqC, out, lep);
   else observe<T>(c, y, der, tgt, steps, seqA, seqC, out, 1);
 }
 
@@ -416,7 +420,8 @@ __device__ __forceinline__ bool settled(const DevCfg<T>& c, const uint32_t g[4],
 
 template <typename T>
 __device__ __forceinline__ void metrics_init(const DevCfg<T>& c, const State<T>& s, int64_t i, const T* tgt,
-                                             const T* vals) {
+                                             const T* vals, uint32_t lep) {
+  const int slot0 = (int)(lep % (uint32_t)FW_M_END_WINDOW);  // entry 0 of the episode
   const int64_t ld = s.ld;
   const uint32_t gb = goal_status_bits(c, tgt, vals);
 #pragma unroll
@@ -429,7 +434,7 @@ __device__ __forceinline__ void metrics_init(const DevCfg<T>& c, const State<T>&
     st_(s.met, MR_EMAX + k, ld, i, err);
     st_(s.met, MR_PREV + k, ld, i, err);
     st_(s.met, MR_WSUM + k, ld, i, err);
-    st_(s.met, MR_RING + k, ld, i, err);
+    st_(s.met, MR_RING + 3 * slot0 + k, ld, i, err);
   }
   st_(s.met, MR_CV, ld, i, T(0));
   st_(s.metu, MU_N, ld, i, 1u);
@@ -456,13 +461,14 @@ struct Met {
   T old[3];                // ring entries the next error overwrites (slot `slot`)
   int slot;
   // `slot` is known before the count is loaded: within an episode every step but a terminal
-  // failure appends an error, so the new entry's index is steps0 + 1
-  __device__ __forceinline__ void load(const State<T>& s, int64_t i, int steps0) {
+  // failure appends an error, so the new entry's index is steps0 + 1; entry b lives in ring slot
+  // (lep + b) % FW_M_END_WINDOW (lep = the episode's first `life`: the same on every lane, so coalesced)
+  __device__ __forceinline__ void load(const State<T>& s, int64_t i, uint32_t lep, int steps0) {
 #pragma unroll
     for (int r = 0; r < MR_RING; r++) row[r] = ld_(s.met, r, s.ld, i);
 #pragma unroll
     for (int r = 0; r < MU_ROWS; r++) u[r] = ld_(s.metu, r, s.ld, i);
-    slot = (steps0 + 1) % FW_M_END_WINDOW;
+    slot = (int)((lep + (uint32_t)steps0 + 1u) % (uint32_t)FW_M_END_WINDOW);
 #pragma unroll
     for (int k = 0; k < 3; k++) old[k] = ld_(s.met, MR_RING + 3 * slot + k, s.ld, i);
   }
@@ -479,9 +485,10 @@ struct Met {
 // error into the end-error ring.
 template <typename T>
 __device__ __forceinline__ void metrics_step(const DevCfg<T>& c, const State<T>& s, int64_t i, Met<T>& M,
-                                             const T* tgt, const T* vals, uint32_t gb, const uint32_t gall[4]) {
+                                             const T* tgt, const T* vals, uint32_t gb, const uint32_t gall[4],
+                                             uint32_t lep) {
   const uint32_t n0 = M.u[MU_N], b = n0;  // index of the new history entry
-  const int slot = (int)(n0 % FW_M_END_WINDOW);
+  const int slot = (int)((lep + n0) % (uint32_t)FW_M_END_WINDOW);
   if (slot != M.slot) {  // stepping on after a failed (done) step without reset: re-read
     M.slot = slot;
 #pragma unroll
@@ -723,7 +730,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(const DevCfg<T>* __restrict__ c
   store_env_fresh(c, s, i, y, der, wind, tgt);
   if (c.has_env && c.metrics) {
     const T vr[3] = {der[0], der[1], der[3]};
-    metrics_init(c, s, i, tgt, vr);
+    metrics_init(c, s, i, tgt, vr, s.life[i]);
   }
   if (c.has_env && (obs || c.obs_hist)) {  // the history needs the reset row even without an output
     T seq[RING + 1][3];
@@ -732,7 +739,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(const DevCfg<T>* __restrict__ c
 #pragma unroll
       for (int a = 0; a < 3; a++) seq[j][a] = T(0);
     observe_env(c, s, i, s.episode[i], OBS_RESET, y, der, tgt, 0, seq, seq,
-                obs ? obs + i * (int64_t)c.n_obs * c.obs_len : nullptr);
+                obs ? obs + i * (int64_t)c.n_obs * c.obs_len : nullptr, s.life[i]);
   }
 }
 
@@ -747,6 +754,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const DevCfg<T>* __restrict__
   load_row(s.der, 8, ld, i, der);
   load_row(s.target, 3, ld, i, tgt);
   const int steps = (int)(s.steps[i] & 0xFFFFu);
+  const uint32_t life = s.life[i];
   T seqA[RING + 1][3], seqC[RING + 1][3];
 #pragma unroll
   for (int j = 0; j <= RING; j++)
@@ -756,17 +764,18 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const DevCfg<T>* __restrict__
 #pragma unroll
   for (int j = 0; j <= RING; j++) {
     if (j < c.act_window && steps - 1 - j >= 0) {
-      const int slot = (steps - 1 - j) % c.act_window;
+      const int slot = (int)((life - 1u - (uint32_t)j) % (uint32_t)c.act_window);
 #pragma unroll
       for (int a = 0; a < 3; a++) seqA[j][a] = s.act_ring[((int64_t)slot * 3 + a) * ld + i];
     }
     if (j < c.cmd_window && steps - 1 - j >= 0) {
-      const int slot = (steps - 1 - j) % c.cmd_window;
+      const int slot = (int)((life - 1u - (uint32_t)j) % (uint32_t)c.cmd_window);
 #pragma unroll
       for (int a = 0; a < 3; a++) seqC[j][a] = s.cmd_ring[((int64_t)slot * 3 + a) * ld + i];
     }
   }
-  observe_env(c, s, i, s.episode[i], OBS_PEEK, y, der, tgt, steps, seqA, seqC, obs + i * (int64_t)c.n_obs * c.obs_len);
+  observe_env(c, s, i, s.episode[i], OBS_PEEK, y, der, tgt, steps, seqA, seqC, obs + i * (int64_t)c.n_obs * c.obs_len,
+              life - (uint32_t)steps);
 }
 
 // Re-reads the pre-step ODE state after the RK loop (sim_step_masked's reload hook): the
@@ -833,6 +842,7 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_sim_step(const DevCfg<T>
 #pragma unroll
   for (int a = 0; a < 3; a++) st_(s.cmd, a, ld, i, cmd[a]);
   s.steps[i] = (sw & 0xFFFF0000u) | (uint32_t)((k + 1) & 0xFFFF);  // cur_sim_step += 1 (pyfly.py:1418)
+  s.life[i] += 1u;
   if (cmd_out)
 #pragma unroll
     for (int a = 0; a < 3; a++) cmd_out[i * 3 + a] = cmd[a];
@@ -870,8 +880,10 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   const int steps0 = (int)(sw & 0xFFFFu);
   const int steps_tgt0 = (int)(sw >> 16);
   const uint32_t episode = s.episode[i];
-
-  // ---- FixedWingAircraft.step prologue (fixed_wing.py:491-506) ----
+  // ring slots by `life` (the same on every lane: coalesced rows however the episodes are staggered; slots by
+  // the episode step scattered a wave's ring accesses over up to 64 rows once resets desynchronised the
+  // episodes, +30 % HBM traffic per launch at the bench's steady state, profiles/r04_traffic_split.json)
+  uint32_t life0 = 0u, lep = 0u;  // loaded with the epilogue's inputs: lep = the episode's first `life` (fixed_wing.py:491-506) ----
   T cmd[3];
 #pragma unroll
   for (int q = 0; q < 3; q++) cmd[q] = c.scale_actions ? scale_fwd(c, q, clipv(a[q], c.scale_low, c.scale_high)) : a[q];
@@ -885,25 +897,27 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   T prev_cmd[3];
   T ep_ret0;
   auto load_epilogue = [&]() {
+    life0 = s.life[i];
+    lep = life0 - (uint32_t)steps0;
 #pragma unroll
     for (int j = 1; j <= RING; j++) {
 #pragma unroll
       for (int q = 0; q < 3; q++) seqA[j][q] = seqC[j][q] = T(0);
-      // previous action j = action number steps-j (1-based) -> slot (steps-j-1) % window
+      // previous action j = action number steps-j (1-based) -> slot (life0 - j) % window
       if (j <= c.act_window && steps - j >= 1) {
-        const int slot = (steps - j - 1) % c.act_window;
+        const int slot = (int)((life0 - (uint32_t)j) % (uint32_t)c.act_window);
 #pragma unroll
         for (int q = 0; q < 3; q++) seqA[j][q] = s.act_ring[((int64_t)slot * 3 + q) * ld + i];
       }
       if (j <= c.cmd_window && steps - j >= 1) {
-        const int slot = (steps - j - 1) % c.cmd_window;
+        const int slot = (int)((life0 - (uint32_t)j) % (uint32_t)c.cmd_window);
 #pragma unroll
         for (int q = 0; q < 3; q++) seqC[j][q] = s.cmd_ring[((int64_t)slot * 3 + q) * ld + i];
       }
     }
     load_row(s.goal, 4, ld, i, g);
     if (c.metrics) {
-      M.load(s, i, steps0);
+      M.load(s, i, lep, steps0);
       load_row(s.cmd, 3, ld, i, prev_cmd);
     }
     ep_ret0 = ld_(s.ep_ret, 0, ld, i);
@@ -948,11 +962,11 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
     seqC[0][q] = cmd[q];
   }
   {
-    const int slot = (steps - 1) % c.act_window;
+    const int slot = (int)(life0 % (uint32_t)c.act_window);
 #pragma unroll
     for (int q = 0; q < 3; q++) s.act_ring[((int64_t)slot * 3 + q) * ld + i] = a[q];
     if (c.cmd_window) {
-      const int cs = (steps - 1) % c.cmd_window;
+      const int cs = (int)(life0 % (uint32_t)c.cmd_window);
 #pragma unroll
       for (int q = 0; q < 3; q++) s.cmd_ring[((int64_t)cs * 3 + q) * ld + i] = cmd[q];
     }
@@ -1002,7 +1016,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
     reward = reward_of(c, y, der, tgt, steps, seqA);
     next_target(c, steps_tgt, tgt);
 #ifndef FW_MET_SKIP_STEP
-    if (c.metrics) metrics_step(c, s, i, M, tgt, vals, gb, g);
+    if (c.metrics) metrics_step(c, s, i, M, tgt, vals, gb, g, lep);
 #endif
   } else {
     done = true;
@@ -1015,7 +1029,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   const int64_t ow = (int64_t)c.n_obs * c.obs_len;  // values per observation (rows x entries)
   const int omode = sterm ? OBS_FAIL : OBS_STEP;
   T* orow = obs_out + i * ow;
-  if (done && tobs_out) observe_env(c, s, i, episode, omode, y, der, tgt, steps, seqA, seqC, tobs_out + i * ow);
+  if (done && tobs_out) observe_env(c, s, i, episode, omode, y, der, tgt, steps, seqA, seqC, tobs_out + i * ow, lep);
 
   rew_out[i] = reward;
   done_out[i] = done ? 1 : 0;
@@ -1052,17 +1066,18 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
 #ifndef FW_MET_SKIP_INIT
       if (c.metrics) {
         const T vr[3] = {dr[0], dr[1], dr[3]};
-        metrics_init(c, s, i, tr, vr);
+        metrics_init(c, s, i, tr, vr, life0 + 1u);
       }
 #endif
       T seq0[RING + 1][3];
-      observe_env(c, s, i, episode + 1u, OBS_RESET, yr, dr, tr, 0, seq0, seq0, orow);
+      observe_env(c, s, i, episode + 1u, OBS_RESET, yr, dr, tr, 0, seq0, seq0, orow, life0 + 1u);
+      s.life[i] = life0 + 1u;
       FW_TSTAMP(5);
       return;
     }
   }
 #ifndef FW_SKIP_OBS
-  observe_env(c, s, i, episode, omode, y, der, tgt, steps, seqA, seqC, orow);
+  observe_env(c, s, i, episode, omode, y, der, tgt, steps, seqA, seqC, orow, lep);
 #endif
 #pragma unroll
   for (int r = 0; r < NY; r++) st_(s.y, r, ld, i, y[r]);
@@ -1074,6 +1089,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   for (int w = 0; w < 4; w++) st_(s.goal, w, ld, i, g[w]);
   st_(s.ep_ret, 0, ld, i, ep_ret);
   s.steps[i] = (uint32_t)(steps & 0xFFFF) | ((uint32_t)(steps_tgt & 0xFFFF) << 16);
+  s.life[i] = life0 + 1u;
   FW_TSTAMP(4);
 }
 
@@ -1275,7 +1291,7 @@ struct fw_handle {
   int metrics = 0;          // streaming episode-metric state allocated (env->metrics at create)
   void* met_out = nullptr;  // [FW_NMETRIC][N] done-episode records (fw_set_metrics_output)
   // offsets (bytes) of the SoA blocks inside base
-  size_t o_y, o_der, o_wind, o_target, o_cmd, o_epret, o_act, o_cmdring, o_steps, o_goal, o_episode;
+  size_t o_y, o_der, o_wind, o_target, o_cmd, o_epret, o_act, o_cmdring, o_steps, o_goal, o_episode, o_life;
   size_t o_met = 0, o_metu = 0;
   int obs_hist = 0;         // past raw observation rows kept per env ((length - 1) * step + 2, 0 = none)
   size_t o_obs_init = 0, o_obs_ring = 0;
@@ -1625,6 +1641,7 @@ State<T> state_of(const fw_handle* h) {
   s.steps = (uint32_t*)(b + h->o_steps);
   s.goal = (uint32_t*)(b + h->o_goal);
   s.episode = (uint32_t*)(b + h->o_episode);
+  s.life = (uint32_t*)(b + h->o_life);
   s.noise = (const T*)h->noise;
   s.noise_len = h->noise_len;
   s.noise_env_len = h->noise_env_len;
@@ -1766,6 +1783,7 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
   h->o_steps = off; off += row32;
   h->o_goal = off; off += 4 * row32;
   h->o_episode = off; off += row32;
+  h->o_life = off; off += row32;
   if (h->metrics) {
     h->o_met = off; off += (size_t)MT_ROWS * row;
     h->o_metu = off; off += (size_t)MU_ROWS * row32;
@@ -1997,6 +2015,39 @@ int fw_collect_records(const fw_handle* h, int64_t* n_records, int64_t* max_reco
   return FW_OK;
 }
 
+// FW_BLK_ACT_RING / FW_BLK_CMD_RING as the ABI presents them (action k of the current episode in slot
+// (k - 1) % W, fwsim.h) <-> the device layout (slot (L_ep + k - 1) % W with L_ep = life - steps_count, the
+// lifetime-indexed rings of State): a per-aircraft rotation of the W slots.
+__global__ void k_ring_xlate(const char* __restrict__ src, char* __restrict__ dst, int W, int64_t n, int esz,
+                             int64_t row_dev, int64_t row_abi, const uint32_t* __restrict__ life,
+                             const uint32_t* __restrict__ steps, int to_abi) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t lep = life[i] - (steps[i] & 0xFFFFu);
+  for (int q = 0; q < W; q++) {
+    const int p = (int)((lep + (uint32_t)q) % (uint32_t)W);
+    for (int a = 0; a < 3; a++) {
+      const int64_t rl = (int64_t)q * 3 + a, rp = (int64_t)p * 3 + a;
+      const char* from = to_abi ? src + rp * row_dev + i * esz : src + rl * row_abi + i * esz;
+      char* to = to_abi ? dst + rl * row_abi + i * esz : dst + rp * row_dev + i * esz;
+      if (esz == 8) *(uint64_t*)to = *(const uint64_t*)from;
+      else *(uint32_t*)to = *(const uint32_t*)from;
+    }
+  }
+}
+
+static int ring_copy(fw_handle* h, int32_t block, size_t off, size_t esz, const void* src, void* dst, int to_abi,
+                     hipStream_t st) {
+  const int W = block == FW_BLK_ACT_RING ? h->act_window : h->cmd_window;
+  const int64_t row_dev = (int64_t)align_up((size_t)h->ld * esz, 256), row_abi = h->n * (int64_t)esz;
+  char* b = (char*)h->base;
+  hipLaunchKernelGGL(k_ring_xlate, dim3((unsigned)((h->n + 255) / 256)), dim3(256), 0, st,
+                     to_abi ? (const char*)(b + off) : (const char*)src, to_abi ? (char*)dst : (char*)(b + off), W,
+                     h->n, (int)esz, row_dev, row_abi, (const uint32_t*)(b + h->o_life),
+                     (const uint32_t*)(b + h->o_steps), to_abi);
+  return check_launch();
+}
+
 static int block_info(const fw_handle* h, int32_t block, size_t* off, int* rows, size_t* esz) {
   const size_t T_ = h->precision == FW_F64 ? 8 : 4;
   switch (block) {
@@ -2039,6 +2090,7 @@ int fw_get_state(fw_handle* h, int32_t block, void* dst_dev, void* stream) {
   if (v) return v;
   FW_HIP(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
+  if (block == FW_BLK_ACT_RING || block == FW_BLK_CMD_RING) return ring_copy(h, block, off, esz, nullptr, dst_dev, 1, st);
   const size_t row = align_up((size_t)h->ld * esz, 256);
   FW_HIP(hipMemcpy2DAsync(dst_dev, h->n * esz, (char*)h->base + off, row, h->n * esz, rows, hipMemcpyDeviceToDevice,
                           st));
@@ -2053,6 +2105,7 @@ int fw_set_state(fw_handle* h, int32_t block, const void* src_dev, void* stream)
   if (v) return v;
   FW_HIP(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
+  if (block == FW_BLK_ACT_RING || block == FW_BLK_CMD_RING) return ring_copy(h, block, off, esz, src_dev, nullptr, 0, st);
   const size_t row = align_up((size_t)h->ld * esz, 256);
   FW_HIP(hipMemcpy2DAsync((char*)h->base + off, row, src_dev, h->n * esz, h->n * esz, rows, hipMemcpyDeviceToDevice,
                           st));

@@ -231,13 +231,17 @@ __device__ __forceinline__ void merge_records(const double* __restrict__ part, i
   double acc[MAXD], cn = 0.0;
 #pragma unroll
   for (int j = 0; j < MAXD; j++) acc[j] = 0.0;
+  // loads from clamped indices, unconditionally (a load in a D-guarded block is waited for right there: the
+  // first version of this loop issued its loads one at a time, 34 us per merge); the guard selects after
   for (int k = tid; k < parts; k += MERGE_THREADS) {  // pass 1
     const double* r = part + (int64_t)k * S;
     const double nk = r[0];
+    double m[MAXD];
+#pragma unroll
+    for (int j = 0; j < MAXD; j++) m[j] = r[1 + (j < D ? j : D - 1)];
     cn += nk;
 #pragma unroll
-    for (int j = 0; j < MAXD; j++)
-      if (j < D) acc[j] += nk * r[1 + j];
+    for (int j = 0; j < MAXD; j++) acc[j] += j < D ? nk * m[j] : 0.0;
   }
   cn = wave_sum(cn);
   if (lane == 0) wsum[w][MAXD] = cn;
@@ -263,12 +267,18 @@ __device__ __forceinline__ void merge_records(const double* __restrict__ part, i
   for (int k = tid; k < parts; k += MERGE_THREADS) {  // pass 2
     const double* r = part + (int64_t)k * S;
     const double nk = r[0];
+    double m[MAXD], q[MAXD];
 #pragma unroll
-    for (int j = 0; j < MAXD; j++)
-      if (j < D) {
-        const double dm = r[1 + j] - smean[j];
-        acc[j] += r[1 + D + j] + nk * (dm * dm);
-      }
+    for (int j = 0; j < MAXD; j++) {
+      const int jc = j < D ? j : D - 1;
+      m[j] = r[1 + jc];
+      q[j] = r[1 + D + jc];
+    }
+#pragma unroll
+    for (int j = 0; j < MAXD; j++) {
+      const double dm = m[j] - smean[j < D ? j : D - 1];
+      acc[j] += j < D ? q[j] + nk * (dm * dm) : 0.0;
+    }
   }
 #pragma unroll
   for (int j = 0; j < MAXD; j++)
@@ -914,7 +924,9 @@ int launch_mfma(const PolArgs& G, hipStream_t s) {
   int cus = 0;
   if (int rc = cu_count(&cus)) return rc;
   const int64_t tiles = (G.n + 15) / 16;
-  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((tiles + PM_WAVES - 1) / PM_WAVES, cus));
+  static const int per_cu = std::getenv("FW_POL_BLOCKS_PER_CU") ? std::atoi(std::getenv("FW_POL_BLOCKS_PER_CU")) : 1;
+  const unsigned grid = (unsigned)std::max<int64_t>(
+      1, std::min<int64_t>((tiles + PM_WAVES - 1) / PM_WAVES, (int64_t)cus * std::max(per_cu, 1)));
   if (G.P.d <= 16)
     hipLaunchKernelGGL(k_policy_mfma<4>, dim3(grid), dim3(64 * PM_WAVES), 0, s, G);
   else
