@@ -243,9 +243,9 @@ def test_merge_update_equals_merge_then_update():
     D = d + 1
     g = torch.Generator(device=DEV)
     g.manual_seed(7)
-    rec = torch.randn(nrec, 1 + 2 * D, generator=g, device=DEV, dtype=torch.float64)
-    rec[:, 0] = torch.randint(1, 65, (nrec,), generator=g, device=DEV).double()
-    rec[:, 1 + D:] = rec[:, 1 + D:].abs() * 10
+    rec = torch.randn(1 + 2 * D, nrec, generator=g, device=DEV, dtype=torch.float64)  # column-major records
+    rec[0] = torch.randint(1, 65, (nrec,), generator=g, device=DEV).double()
+    rec[1 + D:] = rec[1 + D:].abs() * 10
     rms0 = torch.rand(2 * d + 4, generator=g, device=DEV, dtype=torch.float64) + 0.5
     a, b = rms0.clone(), rms0.clone()
     out_a = torch.empty(1 + 2 * D, dtype=torch.float64, device=DEV)

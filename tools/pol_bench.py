@@ -2,7 +2,6 @@
 """Per-launch time of the fused policy forward (fw_policy_forward, 65536 envs, SB3 default MlpPolicy) and of
 the collect-mode launch (fw_collect_policy, rows + VecNormalize normalisation).  FW_POL_VALU=1 selects the
 VALU kernel; FW_POL_BLOCKS_PER_CU the persistent grid."""
-import ctypes
 import json
 import os
 import sys
@@ -36,7 +35,6 @@ def main():
     print(json.dumps({"kernel": "valu" if os.environ.get("FW_POL_VALU") else "mfma", "n": n,
                       "blocks_per_cu": os.environ.get("FW_POL_BLOCKS_PER_CU", "1"),
                       "us_per_launch": a.elapsed_time(b) / reps * 1e3}), flush=True)
-    del ctypes
 
 
 if __name__ == "__main__":

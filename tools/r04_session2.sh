@@ -3,8 +3,10 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 OUT=gpurun_out/${1:-s2}
 mkdir -p "$OUT"
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -rf > "$OUT/pytest.log" 2>&1
-rc=$?; tail -1 "$OUT/pytest.log"; [ $rc -eq 0 ] || exit $rc
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -rf > "$OUT/pytest.log" 2>&1
+  rc=$?; tail -1 "$OUT/pytest.log"; [ $rc -eq 0 ] || exit $rc
+fi
 bash tools/r04_pol.sh "$(basename $OUT)_pol" || exit $?
 SKIP_SPLIT=1 bash tools/r04_prof.sh "$(basename $OUT)_prof" || exit $?
 bash tools/r04_traffic.sh "$(basename $OUT)_split" || exit $?

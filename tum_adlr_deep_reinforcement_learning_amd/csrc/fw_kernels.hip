@@ -1123,7 +1123,8 @@ __device__ __forceinline__ void collect_epilogue(const State<T>& s, int64_t i, b
     const unsigned long long rm = __ballot(row);
     const double nb = (double)__popcll(rm);
     __syncthreads();
-    double* rec = s.col_rec + (int64_t)blockIdx.x * (1 + 2 * D);
+    double* rec = s.col_rec + blockIdx.x;  // column-major: field q at rec[q * blocks] (coalesced merge reads)
+    const int64_t qs = gridDim.x;
     const int p = lane & 3;
     for (int c0 = 0; c0 < D; c0 += 16) {
       const int col = c0 + (lane >> 2);
@@ -1150,8 +1151,8 @@ __device__ __forceinline__ void collect_epilogue(const State<T>& s, int64_t i, b
       q += __shfl_xor(q, 1);
       q += __shfl_xor(q, 2);
       if (cv && p == 0) {
-        rec[1 + col] = mean;
-        rec[1 + D + col] = q;
+        rec[(1 + col) * qs] = mean;
+        rec[(1 + D + col) * qs] = q;
       }
     }
     if (lane == 0) rec[0] = nb;

@@ -199,7 +199,9 @@ __global__ __launch_bounds__(BLOCK) void k_moments_partial(const float* __restri
     if (sub == 0) smean[j] = s / dn;
   }
   __syncthreads();
-  double* out = part + (int64_t)blockIdx.x * (1 + 2 * D);
+  // column-major records (field q of block b at part[q * blocks + b]): merge_records reads them coalesced
+  double* out = part + blockIdx.x;
+  const int64_t qs = gridDim.x;
   for (int j = cg; j < D; j += NCG) {  // pass 2: sum of squared deviations
     const double m = smean[j];
     double q = 0.0;
@@ -209,14 +211,15 @@ __global__ __launch_bounds__(BLOCK) void k_moments_partial(const float* __restri
     }
     q = grp_sum8(q);
     if (sub == 0) {
-      out[1 + j] = m;
-      out[1 + D + j] = q;
+      out[(1 + j) * qs] = m;
+      out[(1 + D + j) * qs] = q;
     }
   }
-  if (threadIdx.x == 0) out[0] = dn;
+  if (threadIdx.x == 0) out[0] = dn;  // field 0
 }
 
-// merges `parts` records (stride 1+2D) into one, two-pass: mean = sum n_b mean_b / N, then
+// merges `parts` records (column-major: field q of record k at part[q * parts + k]; q = 0 count, 1..D means,
+// D+1..2D M2) into one record `out` (contiguous 1 + 2D), two-pass: mean = sum n_b mean_b / N, then
 // M2 = sum (M2_b + n_b (mean_b - mean)^2).  The whole block (MERGE_THREADS) works on it: thread t folds
 // records t, t + MERGE_THREADS, ... (every column at once, so each record is read once per pass), then a
 // wave butterfly, then the waves in order -- a fixed order, so the result is deterministic.  (Round 3's one
@@ -226,7 +229,6 @@ constexpr int MERGE_WAVES = MERGE_THREADS / 64;
 __device__ __forceinline__ void merge_records(const double* __restrict__ part, int parts, int D, double* __restrict__ out) {
   __shared__ double wsum[MERGE_WAVES][MAXD + 1];  // per-wave partial sums; [MAXD]: the count
   __shared__ double smean[MAXD + 1];              // column means; [MAXD]: N
-  const int S = 1 + 2 * D;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   double acc[MAXD], cn = 0.0;
 #pragma unroll
@@ -234,11 +236,11 @@ __device__ __forceinline__ void merge_records(const double* __restrict__ part, i
   // loads from clamped indices, unconditionally (a load in a D-guarded block is waited for right there: the
   // first version of this loop issued its loads one at a time, 34 us per merge); the guard selects after
   for (int k = tid; k < parts; k += MERGE_THREADS) {  // pass 1
-    const double* r = part + (int64_t)k * S;
+    const double* r = part + k;  // consecutive threads read consecutive records of every field
     const double nk = r[0];
     double m[MAXD];
 #pragma unroll
-    for (int j = 0; j < MAXD; j++) m[j] = r[1 + (j < D ? j : D - 1)];
+    for (int j = 0; j < MAXD; j++) m[j] = r[(int64_t)(1 + (j < D ? j : D - 1)) * parts];
     cn += nk;
 #pragma unroll
     for (int j = 0; j < MAXD; j++) acc[j] += j < D ? nk * m[j] : 0.0;
@@ -265,14 +267,14 @@ __device__ __forceinline__ void merge_records(const double* __restrict__ part, i
 #pragma unroll
   for (int j = 0; j < MAXD; j++) acc[j] = 0.0;
   for (int k = tid; k < parts; k += MERGE_THREADS) {  // pass 2
-    const double* r = part + (int64_t)k * S;
+    const double* r = part + k;
     const double nk = r[0];
     double m[MAXD], q[MAXD];
 #pragma unroll
     for (int j = 0; j < MAXD; j++) {
       const int jc = j < D ? j : D - 1;
-      m[j] = r[1 + jc];
-      q[j] = r[1 + D + jc];
+      m[j] = r[(int64_t)(1 + jc) * parts];
+      q[j] = r[(int64_t)(1 + D + jc) * parts];
     }
 #pragma unroll
     for (int j = 0; j < MAXD; j++) {
@@ -481,6 +483,10 @@ __device__ __forceinline__ float ftanh(float x) {
   const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);  // exp(2x)
   return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
 }
+// the same of x2 = 2 log2(e) x (the scale folded into the producing layer)
+__device__ __forceinline__ float ftanh2(float x2) {
+  return fmaf(-2.0f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(x2) + 1.0f), 1.0f);
+}
 
 template <int H>
 __global__ __launch_bounds__(POL_BLOCK) void k_policy_forward(fw_mlp_policy P, const float* __restrict__ obs, int64_t n,
@@ -666,7 +672,7 @@ struct PolArgs {
   int64_t n;
 };
 
-constexpr int PM_WAVES = 4;  // waves per block; one block per CU (one wave per SIMD)
+constexpr int PM_WAVES = 4;  // waves per block; two blocks per CU (two waves per SIMD)
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -678,56 +684,69 @@ __device__ __forceinline__ float norm_obs_val(float o, double mean, double den, 
   return (float)y;
 }
 
+// LDS image of the A operands (per block, read by every wave of it): lane l's fragment of a k-step group is
+// 16 contiguous bytes, consecutive lanes consecutive (ds_read_b128, conflict-free).  Floats:
+//   L1 [net][O][T][lane][v]   K2 W1[16 O + (l & 15)][16 T + 4 (l >> 4) + v]
+//   L0 [net][O][lane][s]      K2 W0[16 O + (l & 15)][4 s + (l >> 4)]
+//   HD [net][T][lane][v]      actor rows l & 15 < A / critic row 15 of the heads (unscaled)
+//   B  [layer][net][O][16]    K2 bias of unit 16 O + 4 g + v (read as lane group g's float4)
+//   BH [16]                   head bias of rows 0..15
+template <int S>
+struct PolLds {
+  static constexpr int L1 = 0, L0 = L1 + 2 * 4 * 4 * 64 * 4, HD = L0 + 2 * 4 * 64 * S, B = HD + 2 * 4 * 64 * 4,
+                       BH = B + 2 * 2 * 4 * 16, FLOATS = BH + 16;
+};
+
+template <int S>
+__device__ __forceinline__ void pol_fill_lds(const fw_mlp_policy& P, float* W) {
+  using L = PolLds<S>;
+  const int d = P.d, A = P.act_dim, H = POL_MAXH;
+  const float K2 = 2.8853900817779268f;  // 2 log2(e): tanh(x) = 1 - 2 / (exp2(K2 x) + 1)
+  for (int i = threadIdx.x; i < L::FLOATS; i += blockDim.x) {
+    float v = 0.0f;
+    if (i < L::L0) {
+      const int q = i - L::L1, vv = q & 3, l = (q >> 2) & 63, T = (q >> 8) & 3, O = (q >> 10) & 3, net = q >> 12;
+      const float* w = net ? P.vf_w1 : P.pi_w1;
+      v = K2 * w[(16 * O + (l & 15)) * H + 16 * T + 4 * (l >> 4) + vv];
+    } else if (i < L::HD) {
+      const int q = i - L::L0, sidx = q % S, l = (q / S) & 63, O = (q / (S * 64)) & 3, net = q / (S * 256);
+      const int f = 4 * sidx + (l >> 4);
+      const float* w = net ? P.vf_w0 : P.pi_w0;
+      v = f < d ? K2 * w[(16 * O + (l & 15)) * d + f] : 0.0f;
+    } else if (i < L::B) {
+      const int q = i - L::HD, vv = q & 3, l = (q >> 2) & 63, T = (q >> 8) & 3, net = q >> 10;
+      const int r = l & 15, k = 16 * T + 4 * (l >> 4) + vv;
+      v = net ? (r == 15 ? P.val_w[k] : 0.0f) : (r < A ? P.act_w[r * H + k] : 0.0f);
+    } else if (i < L::BH) {
+      const int q = i - L::B, u = q & 15, O = (q >> 4) & 3, net = (q >> 6) & 1, layer = q >> 7;
+      const float* b = layer ? (net ? P.vf_b1 : P.pi_b1) : (net ? P.vf_b0 : P.pi_b0);
+      v = K2 * b[16 * O + u];
+    } else {
+      const int r = i - L::BH;
+      v = r < A ? P.act_b[r] : (r == 15 ? P.val_b[0] : 0.0f);
+    }
+    W[i] = v;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ f32x4 lds4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
 template <int S>  // k-steps of 4 observation features (d <= 4 S)
-__global__ __launch_bounds__(64 * PM_WAVES) void k_policy_mfma(PolArgs G) {
+__global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
+  using L = PolLds<S>;
+  extern __shared__ float Wl[];
   const int lane = threadIdx.x & 63;
   const int c16 = lane & 15, g = lane >> 4;
   const int d = G.P.d, A = G.P.act_dim;
   const int64_t n = G.n;
-  const int H = POL_MAXH;
-  // ---- weights -> registers (A operands), biases in the D layout (unit 16 O + 4 g + v)
-  float w0p[4][S], w0v[4][S], w1p[4][4][4], w1v[4][4][4], hp[4][4], hv[4][4];
-  f32x4 b0p[4], b0v[4], b1p[4], b1v[4], bh;
-#pragma unroll
-  for (int O = 0; O < 4; O++) {
-    const int u = 16 * O + c16;
-#pragma unroll
-    for (int s = 0; s < S; s++) {
-      const int f = 4 * s + g;
-      w0p[O][s] = f < d ? G.P.pi_w0[u * d + f] : 0.0f;
-      w0v[O][s] = f < d ? G.P.vf_w0[u * d + f] : 0.0f;
-    }
-#pragma unroll
-    for (int T = 0; T < 4; T++) {
-      const f32x4 qp = *reinterpret_cast<const f32x4*>(G.P.pi_w1 + u * H + 16 * T + 4 * g);
-      const f32x4 qv = *reinterpret_cast<const f32x4*>(G.P.vf_w1 + u * H + 16 * T + 4 * g);
-#pragma unroll
-      for (int v = 0; v < 4; v++) {
-        w1p[O][T][v] = qp[v];
-        w1v[O][T][v] = qv[v];
-      }
-    }
-    b0p[O] = *reinterpret_cast<const f32x4*>(G.P.pi_b0 + 16 * O + 4 * g);
-    b0v[O] = *reinterpret_cast<const f32x4*>(G.P.vf_b0 + 16 * O + 4 * g);
-    b1p[O] = *reinterpret_cast<const f32x4*>(G.P.pi_b1 + 16 * O + 4 * g);
-    b1v[O] = *reinterpret_cast<const f32x4*>(G.P.vf_b1 + 16 * O + 4 * g);
-  }
-#pragma unroll
-  for (int T = 0; T < 4; T++) {
-    f32x4 qp = {0.0f, 0.0f, 0.0f, 0.0f}, qv = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (c16 < A) qp = *reinterpret_cast<const f32x4*>(G.P.act_w + c16 * H + 16 * T + 4 * g);
-    if (c16 == 15) qv = *reinterpret_cast<const f32x4*>(G.P.val_w + 16 * T + 4 * g);
-#pragma unroll
-    for (int v = 0; v < 4; v++) {
-      hp[T][v] = qp[v];
-      hv[T][v] = qv[v];
-    }
-  }
-#pragma unroll
-  for (int v = 0; v < 4; v++) {
-    const int r = 4 * g + v;
-    bh[v] = r < A ? G.P.act_b[r] : (r == 15 ? G.P.val_b[0] : 0.0f);
-  }
+  // ---- the block's A-operand image in LDS (two blocks per CU, two waves per SIMD: one wave's MFMAs overlap
+  // the other's tanh / loads; with the weights in registers a wave took 430 VGPRs and ran alone on its SIMD)
+  pol_fill_lds<S>(G.P, Wl);
+  const float* W0 = Wl + L::L0 + lane * S;
+  const float* W1 = Wl + L::L1 + lane * 4;
+  const float* WH = Wl + L::HD + lane * 4;
+  const float* WB = Wl + L::B + 4 * g;
   // ---- this launch's rows and the VecNormalize statistics of this lane's features
   const int64_t row = G.ctrl ? (int64_t)G.ctrl[0] : 0;
   const float* noise = G.noise;
@@ -817,16 +836,24 @@ __global__ __launch_bounds__(64 * PM_WAVES) void k_policy_mfma(PolArgs G) {
       G.rew_rows[(row - 1) * n + env] = (float)r;
       G.start_rows[row * n + env] = (uint8_t)cur.dn;
     }
-    // ---- layer 0 (8 independent accumulators)
+    asm volatile("" ::: "memory");  // the A operands are re-read from LDS every tile (not hoisted into VGPRs)
+    // ---- layer 0 (8 independent accumulators, starting at the scaled bias)
     f32x4 cp[4], cv[4];
 #pragma unroll
-    for (int O = 0; O < 4; O++) cp[O] = cv[O] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int O = 0; O < 4; O++) {
+      cp[O] = lds4(WB + (0 * 4 + O) * 16);
+      cv[O] = lds4(WB + (1 * 4 + O) * 16);
+    }
 #pragma unroll
-    for (int s = 0; s < S; s++) {
+    for (int O = 0; O < 4; O++) {
 #pragma unroll
-      for (int O = 0; O < 4; O++) {
-        cp[O] = mfma4(w0p[O][s], x[s], cp[O]);
-        cv[O] = mfma4(w0v[O][s], x[s], cv[O]);
+      for (int s4 = 0; s4 < S; s4 += 4) {
+        const f32x4 ap = lds4(W0 + (0 * 4 + O) * 64 * S + s4), av = lds4(W0 + (1 * 4 + O) * 64 * S + s4);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          cp[O] = mfma4(ap[k], x[s4 + k], cp[O]);
+          cv[O] = mfma4(av[k], x[s4 + k], cv[O]);
+        }
       }
     }
     f32x4 hpv[4], hvv[4];  // tanh(layer 0): the B operands of layer 1, k-step (T, v) = register v of tile T
@@ -834,37 +861,45 @@ __global__ __launch_bounds__(64 * PM_WAVES) void k_policy_mfma(PolArgs G) {
     for (int T = 0; T < 4; T++)
 #pragma unroll
       for (int v = 0; v < 4; v++) {
-        hpv[T][v] = ftanh(cp[T][v] + b0p[T][v]);
-        hvv[T][v] = ftanh(cv[T][v] + b0v[T][v]);
+        hpv[T][v] = ftanh2(cp[T][v]);
+        hvv[T][v] = ftanh2(cv[T][v]);
       }
     // ---- layer 1
 #pragma unroll
-    for (int O = 0; O < 4; O++) cp[O] = cv[O] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int O = 0; O < 4; O++) {
+      cp[O] = lds4(WB + (2 * 4 + O) * 16);
+      cv[O] = lds4(WB + (3 * 4 + O) * 16);
+    }
 #pragma unroll
     for (int T = 0; T < 4; T++)
 #pragma unroll
-      for (int v = 0; v < 4; v++)
+      for (int O = 0; O < 4; O++) {
+        const f32x4 ap = lds4(W1 + ((0 * 4 + O) * 4 + T) * 256), av = lds4(W1 + ((1 * 4 + O) * 4 + T) * 256);
 #pragma unroll
-        for (int O = 0; O < 4; O++) {
-          cp[O] = mfma4(w1p[O][T][v], hpv[T][v], cp[O]);
-          cv[O] = mfma4(w1v[O][T][v], hvv[T][v], cv[O]);
+        for (int v = 0; v < 4; v++) {
+          cp[O] = mfma4(ap[v], hpv[T][v], cp[O]);
+          cv[O] = mfma4(av[v], hvv[T][v], cv[O]);
         }
+      }
 #pragma unroll
     for (int T = 0; T < 4; T++)
 #pragma unroll
       for (int v = 0; v < 4; v++) {
-        hpv[T][v] = ftanh(cp[T][v] + b1p[T][v]);
-        hvv[T][v] = ftanh(cv[T][v] + b1v[T][v]);
+        hpv[T][v] = ftanh2(cp[T][v]);
+        hvv[T][v] = ftanh2(cv[T][v]);
       }
     // ---- heads: actor rows 0..A-1 and the value row 15 of one tile (two accumulators, disjoint rows)
     f32x4 ha = {0.0f, 0.0f, 0.0f, 0.0f}, hc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int T = 0; T < 4; T++)
+    for (int T = 0; T < 4; T++) {
+      const f32x4 ap = lds4(WH + (0 * 4 + T) * 256), av = lds4(WH + (1 * 4 + T) * 256);
 #pragma unroll
       for (int v = 0; v < 4; v++) {
-        ha = mfma4(hp[T][v], hpv[T][v], ha);
-        hc = mfma4(hv[T][v], hvv[T][v], hc);
+        ha = mfma4(ap[v], hpv[T][v], ha);
+        hc = mfma4(av[v], hvv[T][v], hc);
       }
+    }
+    const f32x4 bh = lds4(Wl + L::BH + 4 * g);
     f32x4 out;
 #pragma unroll
     for (int v = 0; v < 4; v++) out[v] = (ha[v] + hc[v]) + bh[v];  // one of ha / hc is 0 in each row
@@ -924,13 +959,13 @@ int launch_mfma(const PolArgs& G, hipStream_t s) {
   int cus = 0;
   if (int rc = cu_count(&cus)) return rc;
   const int64_t tiles = (G.n + 15) / 16;
-  static const int per_cu = std::getenv("FW_POL_BLOCKS_PER_CU") ? std::atoi(std::getenv("FW_POL_BLOCKS_PER_CU")) : 1;
+  static const int per_cu = std::getenv("FW_POL_BLOCKS_PER_CU") ? std::atoi(std::getenv("FW_POL_BLOCKS_PER_CU")) : 2;
   const unsigned grid = (unsigned)std::max<int64_t>(
       1, std::min<int64_t>((tiles + PM_WAVES - 1) / PM_WAVES, (int64_t)cus * std::max(per_cu, 1)));
   if (G.P.d <= 16)
-    hipLaunchKernelGGL(k_policy_mfma<4>, dim3(grid), dim3(64 * PM_WAVES), 0, s, G);
+    hipLaunchKernelGGL(k_policy_mfma<4>, dim3(grid), dim3(64 * PM_WAVES), PolLds<4>::FLOATS * sizeof(float), s, G);
   else
-    hipLaunchKernelGGL(k_policy_mfma<8>, dim3(grid), dim3(64 * PM_WAVES), 0, s, G);
+    hipLaunchKernelGGL(k_policy_mfma<8>, dim3(grid), dim3(64 * PM_WAVES), PolLds<8>::FLOATS * sizeof(float), s, G);
   FW_HIP(hipGetLastError());
   return FW_OK;
 }
