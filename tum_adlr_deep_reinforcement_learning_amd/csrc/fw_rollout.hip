@@ -220,23 +220,30 @@ __global__ __launch_bounds__(BLOCK) void k_moments_partial(const float* __restri
 
 // merges `parts` records (column-major: field q of record k at part[q * parts + k]; q = 0 count, 1..D means,
 // D+1..2D M2) into one record `out` (contiguous 1 + 2D), two-pass: mean = sum n_b mean_b / N, then
-// M2 = sum (M2_b + n_b (mean_b - mean)^2).  The whole block (MERGE_THREADS) works on it: thread t folds
-// records t, t + MERGE_THREADS, ... (every column at once, so each record is read once per pass), then a
-// wave butterfly, then the waves in order -- a fixed order, so the result is deterministic.  (Round 3's one
-// wave per column walked the records serially: 20 us for the 1024 block records of a 65536-env step.)
-constexpr int MERGE_THREADS = 256;  // 4 waves: the 33 fp64 column accumulators fit without spilling
-constexpr int MERGE_WAVES = MERGE_THREADS / 64;
+// M2 = sum (M2_b + n_b (mean_b - mean)^2).  Thread t folds records t, t + MERGE_THREADS, ... (coalesced per
+// field, every field of a record in one batch of loads), the per-thread partials go through LDS, and thread
+// j sums column j over the threads in 8 interleaved chains combined in a fixed order: deterministic, and no
+// fp64 cross-lane shuffles (a butterfly per column and pass serialised ~180 LDS round trips: 30 us).
+constexpr int MERGE_THREADS = 256;
+__device__ __forceinline__ double col_sum(const double* c) {  // c[0..MERGE_THREADS), fixed order
+  double p[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) p[k] = c[k];
+  for (int t = 8; t < MERGE_THREADS; t += 8)
+#pragma unroll
+    for (int k = 0; k < 8; k++) p[k] += c[t + k];
+  return ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+}
 __device__ __forceinline__ void merge_records(const double* __restrict__ part, int parts, int D, double* __restrict__ out) {
-  __shared__ double wsum[MERGE_WAVES][MAXD + 1];  // per-wave partial sums; [MAXD]: the count
+  __shared__ double tp[MAXD + 1][MERGE_THREADS];  // per-thread partials, column-major; row MAXD: the counts
   __shared__ double smean[MAXD + 1];              // column means; [MAXD]: N
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x;
   double acc[MAXD], cn = 0.0;
 #pragma unroll
   for (int j = 0; j < MAXD; j++) acc[j] = 0.0;
-  // loads from clamped indices, unconditionally (a load in a D-guarded block is waited for right there: the
-  // first version of this loop issued its loads one at a time, 34 us per merge); the guard selects after
+  // loads from clamped indices, unconditionally (a load in a D-guarded block is waited for right there)
   for (int k = tid; k < parts; k += MERGE_THREADS) {  // pass 1
-    const double* r = part + k;  // consecutive threads read consecutive records of every field
+    const double* r = part + k;
     const double nk = r[0];
     double m[MAXD];
 #pragma unroll
@@ -245,20 +252,14 @@ __device__ __forceinline__ void merge_records(const double* __restrict__ part, i
 #pragma unroll
     for (int j = 0; j < MAXD; j++) acc[j] += j < D ? nk * m[j] : 0.0;
   }
-  cn = wave_sum(cn);
-  if (lane == 0) wsum[w][MAXD] = cn;
 #pragma unroll
   for (int j = 0; j < MAXD; j++)
-    if (j < D) {
-      const double v = wave_sum(acc[j]);
-      if (lane == 0) wsum[w][j] = v;
-    }
+    if (j < D) tp[j][tid] = acc[j];
+  tp[MAXD][tid] = cn;
   __syncthreads();
-  if (tid <= D) {  // thread j: column j's sum over the waves in order; thread D: N
+  if (tid <= D) {
     const int j = tid == D ? MAXD : tid;
-    double a = 0.0;
-    for (int q = 0; q < MERGE_WAVES; q++) a += wsum[q][j];
-    smean[j] = a;
+    smean[j] = col_sum(tp[j]);
   }
   __syncthreads();
   const double N = smean[MAXD];
@@ -282,18 +283,14 @@ __device__ __forceinline__ void merge_records(const double* __restrict__ part, i
       acc[j] += j < D ? q[j] + nk * (dm * dm) : 0.0;
     }
   }
+  __syncthreads();  // (every thread has read smean; tp is rewritten below)
 #pragma unroll
   for (int j = 0; j < MAXD; j++)
-    if (j < D) {
-      const double v = wave_sum(acc[j]);
-      if (lane == 0) wsum[w][j] = v;
-    }
+    if (j < D) tp[j][tid] = acc[j];
   __syncthreads();
   if (tid < D) {
-    double a = 0.0;
-    for (int q = 0; q < MERGE_WAVES; q++) a += wsum[q][tid];
     out[1 + tid] = smean[tid];
-    out[1 + D + tid] = a;
+    out[1 + D + tid] = col_sum(tp[tid]);
     if (tid == 0) out[0] = N;
   }
 }
@@ -697,36 +694,57 @@ struct PolLds {
                        BH = B + 2 * 2 * 4 * 16, FLOATS = BH + 16;
 };
 
+// The image is filled region by region with unrolled, independent loads (a load-then-store loop with a region
+// switch in its body issued one global load per iteration and waited for each: ~15 us of a 34-us launch).
 template <int S>
 __device__ __forceinline__ void pol_fill_lds(const fw_mlp_policy& P, float* W) {
   using L = PolLds<S>;
-  const int d = P.d, A = P.act_dim, H = POL_MAXH;
+  static_assert(64 * PM_WAVES == 256, "fill strides assume 256 threads");
+  const int d = P.d, A = P.act_dim, H = POL_MAXH, t = threadIdx.x;
   const float K2 = 2.8853900817779268f;  // 2 log2(e): tanh(x) = 1 - 2 / (exp2(K2 x) + 1)
-  for (int i = threadIdx.x; i < L::FLOATS; i += blockDim.x) {
-    float v = 0.0f;
-    if (i < L::L0) {
-      const int q = i - L::L1, vv = q & 3, l = (q >> 2) & 63, T = (q >> 8) & 3, O = (q >> 10) & 3, net = q >> 12;
+  {  // L1: 2048 float4 fragments, 8 per thread; fragment q = ((net * 4 + O) * 4 + T) * 64 + l
+    f32x4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int q = t + 256 * k, l = q & 63, T = (q >> 6) & 3, O = (q >> 8) & 3, net = q >> 10;
       const float* w = net ? P.vf_w1 : P.pi_w1;
-      v = K2 * w[(16 * O + (l & 15)) * H + 16 * T + 4 * (l >> 4) + vv];
-    } else if (i < L::HD) {
-      const int q = i - L::L0, sidx = q % S, l = (q / S) & 63, O = (q / (S * 64)) & 3, net = q / (S * 256);
+      v[k] = *reinterpret_cast<const f32x4*>(w + (16 * O + (l & 15)) * H + 16 * T + 4 * (l >> 4));
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) *reinterpret_cast<f32x4*>(W + L::L1 + 4 * (t + 256 * k)) = K2 * v[k];
+  }
+  {  // L0: 512 S floats, 2 S per thread; element q = ((net * 4 + O) * 64 + l) * S + s
+    float v[2 * S];
+#pragma unroll
+    for (int k = 0; k < 2 * S; k++) {
+      const int q = t + 256 * k, sidx = q % S, l = (q / S) & 63, O = (q / (S * 64)) & 3, net = q / (S * 256);
       const int f = 4 * sidx + (l >> 4);
       const float* w = net ? P.vf_w0 : P.pi_w0;
-      v = f < d ? K2 * w[(16 * O + (l & 15)) * d + f] : 0.0f;
-    } else if (i < L::B) {
-      const int q = i - L::HD, vv = q & 3, l = (q >> 2) & 63, T = (q >> 8) & 3, net = q >> 10;
-      const int r = l & 15, k = 16 * T + 4 * (l >> 4) + vv;
-      v = net ? (r == 15 ? P.val_w[k] : 0.0f) : (r < A ? P.act_w[r * H + k] : 0.0f);
-    } else if (i < L::BH) {
-      const int q = i - L::B, u = q & 15, O = (q >> 4) & 3, net = (q >> 6) & 1, layer = q >> 7;
-      const float* b = layer ? (net ? P.vf_b1 : P.pi_b1) : (net ? P.vf_b0 : P.pi_b0);
-      v = K2 * b[16 * O + u];
-    } else {
-      const int r = i - L::BH;
-      v = r < A ? P.act_b[r] : (r == 15 ? P.val_b[0] : 0.0f);
+      v[k] = w[(16 * O + (l & 15)) * d + (f < d ? f : d - 1)];
+      v[k] = f < d ? K2 * v[k] : 0.0f;
     }
-    W[i] = v;
+#pragma unroll
+    for (int k = 0; k < 2 * S; k++) W[L::L0 + t + 256 * k] = v[k];
   }
+  {  // HD: 512 float4 fragments, 2 per thread; fragment q = (net * 4 + T) * 64 + l (row r = l & 15)
+    f32x4 v[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int q = t + 256 * k, l = q & 63, T = (q >> 6) & 3, net = q >> 8, r = l & 15;
+      const int kk = 16 * T + 4 * (l >> 4);
+      const float* src = net ? P.val_w + kk : P.act_w + (r < A ? r : 0) * H + kk;
+      v[k] = *reinterpret_cast<const f32x4*>(src);
+      if (net ? r != 15 : r >= A) v[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) *reinterpret_cast<f32x4*>(W + L::HD + 4 * (t + 256 * k)) = v[k];
+  }
+  {  // B: 256 floats, one per thread; q = ((layer * 2 + net) * 4 + O) * 16 + u
+    const int u = t & 15, O = (t >> 4) & 3, net = (t >> 6) & 1, layer = t >> 7;
+    const float* b = layer ? (net ? P.vf_b1 : P.pi_b1) : (net ? P.vf_b0 : P.pi_b0);
+    W[L::B + t] = K2 * b[16 * O + u];
+  }
+  if (t < 16) W[L::BH + t] = t < A ? P.act_b[t] : (t == 15 ? P.val_b[0] : 0.0f);
   __syncthreads();
 }
 
