@@ -295,6 +295,112 @@ __device__ __forceinline__ void merge_records(const double* __restrict__ part, i
   }
 }
 
+// The common case, D <= 15 columns (the default task: 14 observation values + the return; the count takes
+// column D of the 16-column staging), 256 threads: a
+// thread's records (four at 65536 envs) are loaded in ONE batch per pass (the general kernel waits a memory
+// round trip per record), only the D live columns are read, and the column sums are two-level through LDS
+// (16 threads per column, 16 values each, in order; then the 16 partials in order) -- fp64 cross-lane
+// butterflies serialised ~100 dependent LDS round trips per pass (tools/merge_bench.py: 19 us at 64 records).
+constexpr int MERGE16_THREADS = 256, MERGE16_BATCH = 4;
+__device__ __forceinline__ double sum16_cols(double (*tp)[MERGE16_THREADS + 1], double (*pp)[17], int ncols) {
+  // column j (< ncols) of tp summed over the 256 threads: thread 16 j + h sums threads 16 h .. 16 h + 15
+  const int tid = threadIdx.x, j = tid >> 4, h = tid & 15;
+  if (j < ncols) {
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) a += tp[j][16 * h + k];
+    pp[j][h] = a;
+  }
+  __syncthreads();
+  double r = 0.0;
+  if (tid < ncols)
+#pragma unroll
+    for (int k = 0; k < 16; k++) r += pp[tid][k];
+  return r;  // on thread j
+}
+__device__ __forceinline__ void merge_records16(const double* __restrict__ part, int parts, int D,
+                                                double* __restrict__ out) {
+  constexpr int MD = 16, BT = MERGE16_BATCH;
+  __shared__ double tp[MD + 1][MERGE16_THREADS + 1];  // per-thread partials ([MD]: counts)
+  __shared__ double pp[MD + 1][17];
+  __shared__ double smean[MD + 1];
+  const int tid = threadIdx.x;
+  double acc[MD], cn = 0.0;
+#pragma unroll
+  for (int j = 0; j < MD; j++) acc[j] = 0.0;
+  for (int k0 = tid; k0 < parts; k0 += MERGE16_THREADS * BT) {  // pass 1
+    double nk[BT], m[BT][MD];
+#pragma unroll
+    for (int b = 0; b < BT; b++) {
+      const int k = k0 + b * MERGE16_THREADS, kc = k < parts ? k : parts - 1;
+      nk[b] = part[kc];
+#pragma unroll
+      for (int j = 0; j < MD; j++) m[b][j] = part[(int64_t)(1 + (j < D ? j : D - 1)) * parts + kc];
+      if (k >= parts) nk[b] = 0.0;
+    }
+#pragma unroll
+    for (int b = 0; b < BT; b++) {
+      cn += nk[b];
+#pragma unroll
+      for (int j = 0; j < MD; j++) acc[j] += j < D ? nk[b] * m[b][j] : 0.0;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < MD; j++) tp[j][tid] = acc[j];
+  tp[MD][tid] = cn;
+  __syncthreads();
+  {
+    // columns 0..D-1 and the count column (row D: D <= 15, so it is a zero column of acc)
+    tp[D][tid] = cn;
+    __syncthreads();
+    const double v = sum16_cols(tp, pp, D + 1);
+    if (tid <= D) smean[tid == D ? MD : tid] = v;
+  }
+  __syncthreads();
+  const double N = smean[MD];
+  if (tid < D) smean[tid] = smean[tid] / N;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < MD; j++) acc[j] = 0.0;
+  for (int k0 = tid; k0 < parts; k0 += MERGE16_THREADS * BT) {  // pass 2
+    double nk[BT], m[BT][MD], q[BT][MD];
+#pragma unroll
+    for (int b = 0; b < BT; b++) {
+      const int k = k0 + b * MERGE16_THREADS, kc = k < parts ? k : parts - 1;
+      nk[b] = part[kc];
+#pragma unroll
+      for (int j = 0; j < MD; j++) {
+        const int jc = j < D ? j : D - 1;
+        m[b][j] = part[(int64_t)(1 + jc) * parts + kc];
+        q[b][j] = part[(int64_t)(1 + D + jc) * parts + kc];
+      }
+      if (k >= parts) nk[b] = -1.0;  // marks a padding slot
+    }
+#pragma unroll
+    for (int b = 0; b < BT; b++)
+#pragma unroll
+      for (int j = 0; j < MD; j++) {
+        const double dm = m[b][j] - smean[j < D ? j : D - 1];
+        acc[j] += (j < D && nk[b] >= 0.0) ? q[b][j] + nk[b] * (dm * dm) : 0.0;
+      }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < MD; j++) tp[j][tid] = acc[j];
+  __syncthreads();
+  const double m2 = sum16_cols(tp, pp, D);
+  if (tid < D) {
+    out[1 + tid] = smean[tid];
+    out[1 + D + tid] = m2;
+    if (tid == 0) out[0] = N;
+  }
+}
+
+__global__ __launch_bounds__(MERGE16_THREADS) void k_moments_merge16(const double* __restrict__ part, int parts, int D,
+                                                                     double* __restrict__ out) {
+  merge_records16(part, parts, D, out);
+}
+
 __global__ __launch_bounds__(MERGE_THREADS) void k_moments_merge(const double* __restrict__ part, int parts, int D,
                                                                     double* __restrict__ out) {
   merge_records(part, parts, D, out);
@@ -346,6 +452,19 @@ __global__ void k_rms_update(const double* __restrict__ parts, int n_parts, int 
                              int update_obs, int update_ret) {
   __shared__ double old_count[2];
   rms_update(parts, n_parts, d, has_ret, rms, update_obs, update_ret, old_count);
+}
+
+__global__ __launch_bounds__(MERGE16_THREADS) void k_merge_update16(const double* __restrict__ part, int parts, int d,
+                                                                    int has_ret, double* __restrict__ rms,
+                                                                    double* __restrict__ rec_out) {
+  __shared__ double rec[1 + 2 * MAXD];
+  __shared__ double old_count[2];
+  const int D = d + (has_ret ? 1 : 0);
+  merge_records16(part, parts, D, rec);
+  __syncthreads();
+  if (rec_out)
+    for (int k = threadIdx.x; k < 1 + 2 * D; k += blockDim.x) rec_out[k] = rec[k];
+  rms_update(rec, 1, d, has_ret, rms, 1, 1, old_count);
 }
 
 // k_moments_merge + k_rms_update of the single merged record in one launch (the unsharded statistics
@@ -988,6 +1107,12 @@ int launch_mfma(const PolArgs& G, hipStream_t s) {
   return FW_OK;
 }
 
+// A/B switch (tools/merge_bench.py): FW_MERGE256=1 runs the 256-thread general merge for every D
+bool merge256() {
+  static const bool v = std::getenv("FW_MERGE256") != nullptr;
+  return v;
+}
+
 int check_policy(const fw_mlp_policy* p, const char* who) {
   if (p->d < 1 || p->d > POL_MAXD || p->hidden != POL_MAXH || p->act_dim < 1 || p->act_dim > POL_MAXA)
     return fw::set_error(FW_E_INVALID, std::string(who) + ": d 1..32, hidden 64 (SB3's default net_arch), act_dim 1..8");
@@ -1154,8 +1279,12 @@ int fw_policy_forward(const fw_mlp_policy* p, const float* obs, int64_t n, const
 int fw_moments_merge(const double* records, int32_t n_records, int32_t D, double* out, void* stream) {
   if (!records || !out || n_records < 1 || D < 1 || D > MAXD)
     return fw::set_error(FW_E_INVALID, "fw_moments_merge: bad arguments");
-  hipLaunchKernelGGL(k_moments_merge, dim3(1), dim3(MERGE_THREADS), 0, (hipStream_t)stream, records,
-                     (int)n_records, (int)D, out);
+  if (D <= 15 && !merge256())
+    hipLaunchKernelGGL(k_moments_merge16, dim3(1), dim3(MERGE16_THREADS), 0, (hipStream_t)stream, records,
+                       (int)n_records, (int)D, out);
+  else
+    hipLaunchKernelGGL(k_moments_merge, dim3(1), dim3(MERGE_THREADS), 0, (hipStream_t)stream, records,
+                       (int)n_records, (int)D, out);
   FW_HIP(hipGetLastError());
   return FW_OK;
 }
@@ -1165,8 +1294,12 @@ int fw_vecnorm_merge_update(const double* records, int32_t n_records, int32_t d,
   const int D = d + (has_ret ? 1 : 0);
   if (!records || !rms || n_records < 1 || d < 0 || D < 1 || D > MAXD)
     return fw::set_error(FW_E_INVALID, "fw_vecnorm_merge_update: bad arguments");
-  hipLaunchKernelGGL(k_merge_update, dim3(1), dim3(MERGE_THREADS), 0, (hipStream_t)stream, records, (int)n_records,
-                     (int)d, (int)(has_ret != 0), rms, rec_out);
+  if (D <= 15 && !merge256())
+    hipLaunchKernelGGL(k_merge_update16, dim3(1), dim3(MERGE16_THREADS), 0, (hipStream_t)stream, records,
+                       (int)n_records, (int)d, (int)(has_ret != 0), rms, rec_out);
+  else
+    hipLaunchKernelGGL(k_merge_update, dim3(1), dim3(MERGE_THREADS), 0, (hipStream_t)stream, records, (int)n_records,
+                       (int)d, (int)(has_ret != 0), rms, rec_out);
   FW_HIP(hipGetLastError());
   return FW_OK;
 }
