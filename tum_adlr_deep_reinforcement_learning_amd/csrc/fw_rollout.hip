@@ -320,39 +320,42 @@ __device__ __forceinline__ double sum16_cols(double (*tp)[MERGE16_THREADS + 1], 
 }
 __device__ __forceinline__ void merge_records16(const double* __restrict__ part, int parts, int D,
                                                 double* __restrict__ out) {
+  // parts <= MERGE16_THREADS * MERGE16_BATCH: a thread's records are loaded ONCE (one memory round trip) and
+  // both passes run from registers
   constexpr int MD = 16, BT = MERGE16_BATCH;
-  __shared__ double tp[MD + 1][MERGE16_THREADS + 1];  // per-thread partials ([MD]: counts)
+  __shared__ double tp[MD + 1][MERGE16_THREADS + 1];  // per-thread partials
   __shared__ double pp[MD + 1][17];
   __shared__ double smean[MD + 1];
   const int tid = threadIdx.x;
+  double nk[BT], m[BT][MD], q[BT][MD];
+#pragma unroll
+  for (int b = 0; b < BT; b++) {
+    const int k = tid + b * MERGE16_THREADS, kc = k < parts ? k : parts - 1;
+    nk[b] = part[kc];
+#pragma unroll
+    for (int j = 0; j < MD; j++) {
+      const int jc = j < D ? j : D - 1;
+      m[b][j] = part[(int64_t)(1 + jc) * parts + kc];
+      q[b][j] = part[(int64_t)(1 + D + jc) * parts + kc];
+    }
+    if (k >= parts) nk[b] = -1.0;  // padding slot
+  }
   double acc[MD], cn = 0.0;
 #pragma unroll
   for (int j = 0; j < MD; j++) acc[j] = 0.0;
-  for (int k0 = tid; k0 < parts; k0 += MERGE16_THREADS * BT) {  // pass 1
-    double nk[BT], m[BT][MD];
 #pragma unroll
-    for (int b = 0; b < BT; b++) {
-      const int k = k0 + b * MERGE16_THREADS, kc = k < parts ? k : parts - 1;
-      nk[b] = part[kc];
+  for (int b = 0; b < BT; b++) {  // pass 1
+    const double w = nk[b] >= 0.0 ? nk[b] : 0.0;
+    cn += w;
 #pragma unroll
-      for (int j = 0; j < MD; j++) m[b][j] = part[(int64_t)(1 + (j < D ? j : D - 1)) * parts + kc];
-      if (k >= parts) nk[b] = 0.0;
-    }
-#pragma unroll
-    for (int b = 0; b < BT; b++) {
-      cn += nk[b];
-#pragma unroll
-      for (int j = 0; j < MD; j++) acc[j] += j < D ? nk[b] * m[b][j] : 0.0;
-    }
+    for (int j = 0; j < MD; j++) acc[j] += j < D ? w * m[b][j] : 0.0;
   }
 #pragma unroll
   for (int j = 0; j < MD; j++) tp[j][tid] = acc[j];
-  tp[MD][tid] = cn;
+  __syncthreads();
+  tp[D][tid] = cn;  // the count in column D (D <= 15: a zero column of acc)
   __syncthreads();
   {
-    // columns 0..D-1 and the count column (row D: D <= 15, so it is a zero column of acc)
-    tp[D][tid] = cn;
-    __syncthreads();
     const double v = sum16_cols(tp, pp, D + 1);
     if (tid <= D) smean[tid == D ? MD : tid] = v;
   }
@@ -362,29 +365,13 @@ __device__ __forceinline__ void merge_records16(const double* __restrict__ part,
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < MD; j++) acc[j] = 0.0;
-  for (int k0 = tid; k0 < parts; k0 += MERGE16_THREADS * BT) {  // pass 2
-    double nk[BT], m[BT][MD], q[BT][MD];
 #pragma unroll
-    for (int b = 0; b < BT; b++) {
-      const int k = k0 + b * MERGE16_THREADS, kc = k < parts ? k : parts - 1;
-      nk[b] = part[kc];
+  for (int b = 0; b < BT; b++)  // pass 2
 #pragma unroll
-      for (int j = 0; j < MD; j++) {
-        const int jc = j < D ? j : D - 1;
-        m[b][j] = part[(int64_t)(1 + jc) * parts + kc];
-        q[b][j] = part[(int64_t)(1 + D + jc) * parts + kc];
-      }
-      if (k >= parts) nk[b] = -1.0;  // marks a padding slot
+    for (int j = 0; j < MD; j++) {
+      const double dm = m[b][j] - smean[j < D ? j : D - 1];
+      acc[j] += (j < D && nk[b] >= 0.0) ? q[b][j] + nk[b] * (dm * dm) : 0.0;
     }
-#pragma unroll
-    for (int b = 0; b < BT; b++)
-#pragma unroll
-      for (int j = 0; j < MD; j++) {
-        const double dm = m[b][j] - smean[j < D ? j : D - 1];
-        acc[j] += (j < D && nk[b] >= 0.0) ? q[b][j] + nk[b] * (dm * dm) : 0.0;
-      }
-  }
-  __syncthreads();
 #pragma unroll
   for (int j = 0; j < MD; j++) tp[j][tid] = acc[j];
   __syncthreads();
@@ -1279,7 +1266,7 @@ int fw_policy_forward(const fw_mlp_policy* p, const float* obs, int64_t n, const
 int fw_moments_merge(const double* records, int32_t n_records, int32_t D, double* out, void* stream) {
   if (!records || !out || n_records < 1 || D < 1 || D > MAXD)
     return fw::set_error(FW_E_INVALID, "fw_moments_merge: bad arguments");
-  if (D <= 15 && !merge256())
+  if (D <= 15 && n_records <= MERGE16_THREADS * MERGE16_BATCH && !merge256())
     hipLaunchKernelGGL(k_moments_merge16, dim3(1), dim3(MERGE16_THREADS), 0, (hipStream_t)stream, records,
                        (int)n_records, (int)D, out);
   else
@@ -1294,7 +1281,7 @@ int fw_vecnorm_merge_update(const double* records, int32_t n_records, int32_t d,
   const int D = d + (has_ret ? 1 : 0);
   if (!records || !rms || n_records < 1 || d < 0 || D < 1 || D > MAXD)
     return fw::set_error(FW_E_INVALID, "fw_vecnorm_merge_update: bad arguments");
-  if (D <= 15 && !merge256())
+  if (D <= 15 && n_records <= MERGE16_THREADS * MERGE16_BATCH && !merge256())
     hipLaunchKernelGGL(k_merge_update16, dim3(1), dim3(MERGE16_THREADS), 0, (hipStream_t)stream, records,
                        (int)n_records, (int)d, (int)(has_ret != 0), rms, rec_out);
   else
