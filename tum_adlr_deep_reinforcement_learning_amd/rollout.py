@@ -85,11 +85,14 @@ class RolloutBuffer:
         self.values, self.log_probs, self.advantages, self.returns = (
             slab[o + k * T * N:o + (k + 1) * T * N].view(T, N) for k in range(4))
 
-    def reset(self):
+    def reset(self, zero=True):
+        """buffers.py RolloutBuffer.reset.  zero=False skips clearing the arrays (11.3 GB at configs[2]'s shape):
+        for a collection that rewrites every row it later reads (the fused graphed collect)."""
         self.pos, self.full, self.generator_ready = 0, False, False
-        self.slab.zero_()
-        self.rewards.zero_()
-        self.dones.zero_()
+        if zero:
+            self.slab.zero_()
+            self.rewards.zero_()
+            self.dones.zero_()
         self._flat = None
 
     def size(self):
@@ -265,6 +268,7 @@ class MlpActorCritic(nn.Module):
 
 class RolloutCollector:
     capture_collective = True  # a sharded fused step captures its RCCL exchange inside the one graph
+    steps_per_graph = 16       # the fused step is also captured K times in one graph (one replay per K steps)
 
     """OnPolicyAlgorithm.collect_rollouts (on_policy_algorithm.py:126-190) with everything on the device.
 
@@ -367,7 +371,7 @@ class RolloutCollector:
         pol_key = (id(pol), bool(getattr(pol, "deterministic_rollout", False)),
                    tuple(p.data_ptr() for p in pol.parameters()) if isinstance(pol, nn.Module) else None)
         return (env_key, self._split(), self.buffer.slab.data_ptr(), self.buffer.buffer_size, pol_key,
-                self.capture_collective)
+                self.capture_collective, self.steps_per_graph)
 
     def _capture(self):
         """Capture one collect step on static tensors: s_obs (the observation the policy acts on, then
@@ -583,16 +587,29 @@ class RolloutCollector:
                 with torch.cuda.graph(self._graphs[1]):
                     stats_finish()
             else:
-                with torch.cuda.graph(self._graphs[0]):
+                def step():
                     policy()
                     env_step()
                     stats_local()
                     stats_exchange()  # an RCCL all-gather captured into the graph (nccl backend)
                     stats_finish()
+                with torch.cuda.graph(self._graphs[0]):
+                    step()
+                # and K steps in one graph: one host replay (and one inter-graph gap) per K steps; the rows,
+                # noise row and counter advance on the device, so the K copies are the same launches
+                K = max(1, int(self.steps_per_graph))
+                self._graphK = None
+                if K > 1:
+                    self._graphK = torch.cuda.CUDAGraph(keep_graph=True)
+                    with torch.cuda.graph(self._graphK):
+                        for _ in range(K):
+                            step()
         finally:
             eng.set_collect_epilogue()
         for g in self._graphs:
             g.instantiate()
+        if getattr(self, "_graphK", None) is not None:
+            self._graphK.instantiate()
         self._fused_graph = True
         self._fused_parts = (vn, eng, grouped, stats_exchange)
         self._key = self.graph_key()
@@ -618,21 +635,30 @@ class RolloutCollector:
         return out
 
     def host_launches_per_step(self):
-        """Host-side launches per replayed collect step (graph replays + an eager collective between them)."""
+        """Host-side launches per replayed collect step: graph replays + an eager collective between them (split
+        path), or 1 / steps_per_graph when the fused step is replayed K steps per graph."""
         g = getattr(self, "_graphs", None) or []
+        if len(g) == 1 and getattr(self, "_graphK", None) is not None:
+            return 1.0 / int(self.steps_per_graph)
         return len(g) + (1 if len(g) > 1 else 0)
 
     def _collect_fused(self, n):
         buf = self.buffer
         vn, eng, grouped, exchange = self._fused_parts
-        buf.reset()
+        buf.reset(zero=n < buf.buffer_size)  # a full collection writes every row of every field
         self._draw_noise(n)
         buf.dones[0].copy_(self.last_dones)  # the episode starts of row 0; row t >= 1 comes from the step
         self._ctrl[0] = 0
         self._ctrl[1] = n
         if len(self._graphs) == 1:
-            g = self._graphs[0]
-            for _ in range(n):
+            g, gK = self._graphs[0], getattr(self, "_graphK", None)
+            done = 0
+            if gK is not None:
+                K = int(self.steps_per_graph)
+                for _ in range(n // K):
+                    gK.replay()
+                done = (n // K) * K
+            for _ in range(n - done):
                 g.replay()
         else:
             g0, g1 = self._graphs
