@@ -130,6 +130,8 @@ constexpr int MT_ROWS = MR_RING + 3 * FW_M_END_WINDOW;
 constexpr int MU_N = 0, MU_GB = 1, MU_GC = 13, MU_SET = 17, MU_RISE = 21;
 constexpr int MU_ROWS = MU_RISE + 6;
 constexpr uint32_t M_NONE = 0xFFFFFFFFu;
+constexpr int MD_MINMAX = 0, MD_U = 6;  // Met::dirty bits: 6 min/max rows, then the MU_ROWS - MU_GC rare u32 rows
+static_assert(MD_U + (MU_ROWS - MU_GC) <= 32, "Met::dirty holds one bit per rarely-changing row");
 
 // Debug build only (-DFW_TIMING, tools/phase_timing.py): lane 0 of every wave stamps the
 // 100 MHz real-time clock at phase boundaries into the episode_out buffer (8 x u64 per wave),
@@ -452,6 +454,11 @@ __device__ __forceinline__ void metrics_init(const DevCfg<T>& c, const State<T>&
   for (int r = 0; r < 6; r++) st_(s.metu, MU_RISE + r, ld, i, M_NONE);
 }
 
+__device__ __forceinline__ bool bits_differ(float a, float b) { return __float_as_uint(a) != __float_as_uint(b); }
+__device__ __forceinline__ bool bits_differ(double a, double b) {
+  return __double_as_longlong(a) != __double_as_longlong(b);
+}
+
 // The per-step metric state of one aircraft, loaded with ONE batch of independent loads
 // (no load depends on another, none follows a store) and written back in one batch.
 template <typename T>
@@ -460,6 +467,10 @@ struct Met {
   uint32_t u[MU_ROWS];     // count, goal registers, goal counts, settling, rise
   T old[3];                // ring entries the next error overwrites (slot `slot`)
   int slot;
+  // rows that change only now and then (the minima / maxima, goal counts, settling and rise indices): a set
+  // bit k marks row MD_* k as changed in this lane; store() writes such a row when some lane of the wave
+  // changed it (whole-row coalesced stores), so a steady step writes the rows the traffic accounting counts
+  uint32_t dirty;
   // `slot` is known before the count is loaded: within an episode every step but a terminal
   // failure appends an error, so the new entry's index is steps0 + 1; entry b lives in ring slot
   // (lep + b) % FW_M_END_WINDOW (lep = the episode's first `life`: the same on every lane, so coalesced)
@@ -469,14 +480,22 @@ struct Met {
 #pragma unroll
     for (int r = 0; r < MU_ROWS; r++) u[r] = ld_(s.metu, r, s.ld, i);
     slot = (int)((lep + (uint32_t)steps0 + 1u) % (uint32_t)FW_M_END_WINDOW);
+    dirty = 0u;
 #pragma unroll
     for (int k = 0; k < 3; k++) old[k] = ld_(s.met, MR_RING + 3 * slot + k, s.ld, i);
   }
   __device__ __forceinline__ void store(const State<T>& s, int64_t i) const {
+    // MR_E0 (the episode's initial errors) never changes after metrics_init: not written back
 #pragma unroll
-    for (int r = 0; r < MR_RING; r++) st_(s.met, r, s.ld, i, row[r]);
+    for (int r = MR_ESUM; r < MR_RING; r++) {
+      const bool rare = r >= MR_EMIN && r < MR_EMIN + 6;  // the minima and maxima
+      if (!rare || __ballot((dirty >> (MD_MINMAX + r - MR_EMIN)) & 1u)) st_(s.met, r, s.ld, i, row[r]);
+    }
 #pragma unroll
-    for (int r = 0; r < MU_ROWS; r++) st_(s.metu, r, s.ld, i, u[r]);
+    for (int r = 0; r < MU_ROWS; r++) {
+      const bool rare = r >= MU_GC;  // goal counts, settling, rise indices
+      if (!rare || __ballot((dirty >> (MD_U + r - MU_GC)) & 1u)) st_(s.metu, r, s.ld, i, u[r]);
+    }
   }
 };
 
@@ -500,8 +519,13 @@ __device__ __forceinline__ void metrics_step(const DevCfg<T>& c, const State<T>&
     const T prev = M.row[MR_PREV + k], e0 = M.row[MR_E0 + k];
     M.row[MR_ESUM + k] += err;
     M.row[MR_EABS + k] += T(fabs(err));
-    M.row[MR_EMIN + k] = fmin(M.row[MR_EMIN + k], err);
-    M.row[MR_EMAX + k] = fmax(M.row[MR_EMAX + k], err);
+    {
+      const T mn = fmin(M.row[MR_EMIN + k], err), mx = fmax(M.row[MR_EMAX + k], err);
+      if (bits_differ(mn, M.row[MR_EMIN + k])) M.dirty |= 1u << (MD_MINMAX + k);
+      if (bits_differ(mx, M.row[MR_EMAX + k])) M.dirty |= 1u << (MD_MINMAX + 3 + k);
+      M.row[MR_EMIN + k] = mn;
+      M.row[MR_EMAX + k] = mx;
+    }
     M.row[MR_PREV + k] = err;
     M.row[MR_WSUM + k] += n0 >= (uint32_t)FW_M_END_WINDOW ? err - M.old[k] : err;
     st_(s.met, MR_RING + 3 * slot + k, s.ld, i, err);
@@ -510,7 +534,10 @@ __device__ __forceinline__ void metrics_step(const DevCfg<T>& c, const State<T>&
 #pragma unroll
     for (int w = 0; w < 2; w++) {
       uint32_t& r = M.u[MU_RISE + 2 * k + w];
-      if (r == M_NONE && fabs(prev) >= lims[w] && fabs(err) < lims[w]) r = b;
+      if (r == M_NONE && fabs(prev) >= lims[w] && fabs(err) < lims[w]) {
+        r = b;
+        M.dirty |= 1u << (MD_U + MU_RISE - MU_GC + 2 * k + w);
+      }
     }
   }
   if (c.streak_req > 0) {
@@ -531,7 +558,11 @@ __device__ __forceinline__ void metrics_step(const DevCfg<T>& c, const State<T>&
         for (int w = 0; w < 4; w++) g[w] = gall[w];
       }
       M.u[MU_GC + k] += bit;
-      if (M.u[MU_SET + k] == M_NONE && settled(c, g, n0 + 1u)) M.u[MU_SET + k] = b;
+      M.dirty |= bit << (MD_U + k);
+      if (M.u[MU_SET + k] == M_NONE && settled(c, g, n0 + 1u)) {
+        M.u[MU_SET + k] = b;
+        M.dirty |= 1u << (MD_U + MU_SET - MU_GC + k);
+      }
     }
   }
   M.u[MU_N] = n0 + 1u;
