@@ -54,11 +54,14 @@ def algorithmic_bytes_per_env_step(spec, esz=4):
 
     reads : ODE state 19, elevator/aileron 2, steady wind 3, targets 3, action 3,
             previous actions ring (act_window*3), ep_return 1            -> T
-            steps word, episode word, goal history 4 words               -> u32
+            steps word, episode word, goal history 4 words, life word    -> u32
     writes: ODE state 19, derived 8, targets 3, ring slot 3, ep_return 1,
             observation n_obs, reward 1                                  -> T
-            steps word, goal history 4 words, term code                  -> u32
+            steps word, goal history 4 words, term code, life word       -> u32
             done flag                                                    -> u8
+    (life: the lifetime step counter the ring slots are indexed by, round 4.)  Not counted: the kernel's
+    deliberate re-reads after the RK loop (pre-step state 19, targets 3, actions 3 -- held across the
+    integration they would cost VGPRs), which PMC shows partly served from HBM (profiles/r04_traffic_split.json).
     """
     act_window = 1
     for o in spec.cfg["observation"]["states"]:
@@ -67,8 +70,8 @@ def algorithmic_bytes_per_env_step(spec, esz=4):
     for f in spec.cfg["reward"]["factors"]:
         if f["class"] == "action" and f["type"] == "delta":
             act_window = max(act_window, int(f["window_size"]) - 1)
-    rd = (19 + 2 + 3 + 3 + 3 + act_window * 3 + 1) * esz + (1 + 1 + 4) * 4
-    wr = (19 + 8 + 3 + 3 + 3 + 1 + spec.n_obs + 1) * esz + (1 + 4 + 1) * 4 + 1  # incl. last command
+    rd = (19 + 2 + 3 + 3 + 3 + act_window * 3 + 1) * esz + (1 + 1 + 4 + 1) * 4
+    wr = (19 + 8 + 3 + 3 + 3 + 1 + spec.n_obs + 1) * esz + (1 + 4 + 1 + 1) * 4 + 1  # incl. last command
     if spec.cfg.get("metrics") and spec.metrics_enabled:
         # streaming episode metrics (csrc/fw_kernels.hip metrics_step): previous command, control
         # variation, e0/sum/|sum|/min/max x3, previous ring error x3 (T); count, 3 goal registers x4,

@@ -549,6 +549,9 @@ class RolloutCollector:
         grouped = vn is not None and vn.exchanged()
         if vn is not None:
             vn._ensure_parts()
+        # the exchange is captured only on RCCL (nccl backend); gloo runs collectives on host threads, which a
+        # stream capture cannot record (the one-device rehearsals of the N > 1 bench path use it)
+        split = grouped and not (self.capture_collective and self._capturable_group())
 
         def policy():
             _native.check(lib.fw_collect_policy(ctypes.byref(p), ctypes.byref(io), _stream(dev)), "fw_collect_policy")
@@ -578,7 +581,7 @@ class RolloutCollector:
             eng.set_collect_epilogue(row_ctrl=self._ctrl)
         try:  # keep_graph: graph_nodes() can list what a step launches
             self._graphs = [torch.cuda.CUDAGraph(keep_graph=True)]
-            if grouped and not self.capture_collective:
+            if split:
                 self._graphs.append(torch.cuda.CUDAGraph(keep_graph=True))
                 with torch.cuda.graph(self._graphs[0]):
                     policy()
@@ -613,6 +616,13 @@ class RolloutCollector:
         self._fused_graph = True
         self._fused_parts = (vn, eng, grouped, stats_exchange)
         self._key = self.graph_key()
+
+    def _capturable_group(self):
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()):
+            return True
+        vn = self._vecnorm()
+        return dist.get_backend(getattr(vn, "group", None)) == "nccl"
 
     def graph_nodes(self):
         """Node types of each captured step graph of the fused path (hipGraphGetNodes / hipGraphNodeGetType:
