@@ -780,11 +780,14 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
   // VALU per RHS on the lone-wave tail).  A lane stops on a violated condition (result = its code) or when
   // this evaluation reaches the budget (hard bound on the work of one step so that no input can keep a wave
   // spinning; scipy has none; ends the step like its TOO_SMALL_STEP failure, reported in the stats).
-  // Returns false once no lane of the wave integrates any more.
+  // Returns false once no lane of the wave integrates any more.  `tight` (wave-uniform): some lane may
+  // reach its budget within the sequence; otherwise the common path is one ballot of the condition codes.
   int room = c.max_nfev;
+  bool tight = true;
   auto eval = [&](bool first, int k) {
     const int term = rhs(c, a, X, first, (const T*)ys, (T*)K);
     K[NP - 1].y = T(0);  // pad element
+    if (!tight && !any_lane(term != 0)) return true;
     const bool stop = active && (term != 0 || k >= room);
     if (any_lane(stop)) {
       if (stop) {
@@ -834,6 +837,7 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
       rejected = false;
     }
     room = c.max_nfev - nfev;
+    tight = any_lane(active && room <= 6);
     {  // one trial step (rk.py:126-137); stage 1 input, accumulators seeded
       double h = h_abs;
       t_new = t + h;

@@ -111,12 +111,17 @@ struct QCtx {
   T dmax;
   bool om_clip, vel_clip, act_clip, dclip;
   T ac0, ac1, ac2, ac3, ac4, ac5;  // actuator coefficients of row r (0 on lane 3)
-  // _f_omega_dot row r = kpq PQ + kqr QR + kpr PR + kpp (P^2 - R^2) + kt0 t0 + kt1 t1 + kt2 t2 (0 on lane 3)
-  T kpq, kqr, kpr, kpp, kt0, kt1, kt2;
+  // gyroscopic part of _f_omega_dot row r in the lane's cyclic frame (om, om1, om2 = omega_r, _r+1, _r+2):
+  // kx om om1 + ky om1 om2 + kz om om2 + kw (om2^2 - om1^2)  (0 on lane 3)
+  T kx, ky, kz, kw;
+  // rhs_quad's per-lane coefficients of the lift / pitch-moment / drag factor (fK) and of the side-force /
+  // torque-row formula (tK, t0 .. tda, the propeller torque tpr); computed once here: with the products in
+  // the arms of a per-lane select, the compiler branched on the lane in every RHS evaluation
+  T fK, tK, t0, tb, tp, tr, tda, tpr;
 };
 
-template <typename T, typename C>
-__device__ __forceinline__ QCtx<T> qctx(const C& c, const StepCtx<T>& X, int r) {
+template <typename T, typename C, typename A>
+__device__ __forceinline__ QCtx<T> qctx(const C& c, const A& a, const StepCtx<T>& X, int r) {
   QCtx<T> Q;
   auto s3 = [r](T a0, T a1, T a2) { return r == 0 ? a0 : (r == 1 ? a1 : a2); };
   const T inf = T(__builtin_inf());
@@ -169,13 +174,28 @@ __device__ __forceinline__ QCtx<T> qctx(const C& c, const StepCtx<T>& X, int r) 
   Q.ac5 = s3r(c.ac[0][5], c.ac[1][5], c.ac[2][5]);
   // pyfly.py:1659-1683: p' = g1 PQ - g2 QR + g3 l + g4 n;  q' = g5 PR - g6 (P^2 - R^2) + m / Jy;
   //                     r' = g7 PQ - g1 QR + g4 l + g8 n
-  Q.kpq = s3r(c.gam[1], z, c.gam[7]);
-  Q.kqr = s3r(-c.gam[2], z, -c.gam[1]);
-  Q.kpr = s3r(z, c.gam[5], z);
-  Q.kpp = s3r(z, -c.gam[6], z);
-  Q.kt0 = s3r(c.gam[3], z, c.gam[4]);
-  Q.kt1 = s3r(z, c.inv_Jy, z);
-  Q.kt2 = s3r(c.gam[4], z, c.gam[8]);
+  //   row 0 (om, om1, om2 = P, Q, R): g1 PQ - g2 QR;  row 1 (Q, R, P): g5 PR - g6 (P^2 - R^2);
+  //   row 2 (R, P, Q): g7 PQ - g1 QR
+  Q.kx = s3r(c.gam[1], z, z);
+  Q.ky = s3r(-c.gam[2], c.gam[5], c.gam[7]);
+  Q.kz = s3r(z, z, -c.gam[1]);
+  Q.kw = s3r(z, -c.gam[6], z);
+  const T jm = a.qSc * c.inv_Jy;
+  Q.fK = r == 1 ? jm : a.qS;
+  // side force Y on lane 1, roll / yaw torque rows on lanes 0 / 2: row 0 = g3 l + g4 n, row 2 = g4 l + g8 n
+  const T g3 = c.gam[3], g4 = c.gam[4], g8 = c.gam[8];
+  auto tq = [&](T cl, T cn, T cy) {
+    const T r0v = g3 * cl + g4 * cn, r2v = g4 * cl + g8 * cn;
+    return s3r(r0v, cy, r2v);
+  };
+  Q.tK = s3r(a.qSb, a.qS, a.qSb);
+  Q.t0 = tq(a.Cl0, a.Cn0, a.CY0);
+  Q.tb = tq(a.Clb, a.Cnb, a.CYb);
+  Q.tp = tq(a.Clp, a.Cnp, a.CYp);
+  Q.tr = tq(a.Clr, a.Cnr, a.CYr);
+  Q.tda = tq(a.Clda, a.Cnda, a.CYda);
+  const T k3 = -a.kTP2 * g3, k4 = -a.kTP2 * g4;
+  Q.tpr = s3r(k3, z, k4);
   return Q;
 }
 
@@ -197,12 +217,14 @@ __device__ __forceinline__ T ucond(const C& c, int v, T x, int& key, int k) {
 }
 
 // PyFly._dynamics (pyfly.py:1450-1482) of lane Q.r's rows: s = this lane's 6 stage values,
-// ds = their derivatives.  Returns the first violated condition of the aircraft (0 = none).
+// ds = their derivatives.  term = the first violated condition of the aircraft (0 = none); returns
+// whether any aircraft of the wave violated one (wave-uniform; term is only written then).
 // Written for the lone-wave tail, where every VALU instruction costs its issue slot: the checks a
 // configuration does not have are compiled out (mask tests fold for the SpecCfg views), lane 3's zero
 // rows need no selects (QCtx), and the per-row force rotation shares its beta rotation.
 template <typename T, typename C, typename A>
-__device__ __forceinline__ int rhs_quad(const C& c, const A& a, const QCtx<T>& Q, bool first, const T* s, T* ds) {
+__device__ __forceinline__ bool rhs_quad(const C& c, const A& a, const QCtx<T>& Q, bool first, const T* s, T* ds,
+                                         int& term) {
   int key = KEY_NONE;
   T om = s[1], vel = s[3], av = s[4], ad = s[5];
   T elev = Q.elev0, ail = Q.ail0;
@@ -236,7 +258,7 @@ __device__ __forceinline__ int rhs_quad(const C& c, const A& a, const QCtx<T>& Q
   }
   const T thr = bc<2>(av);
   const T er = s[0];  // raw attitude (pyfly.py:1464): eps_r, lane 3: e0
-  const T e0 = bc<3>(er), e1 = bc<0>(er), e2 = bc<1>(er), e3 = bc<2>(er);
+  const T e0 = bc<3>(er);
   const T er1 = nx1(er), er2 = nx2(er);
 
   // ---- _forces (pyfly.py:1484-1643) ----
@@ -297,29 +319,29 @@ __device__ __forceinline__ int rhs_quad(const C& c, const A& a, const QCtx<T>& Q
   //   K V2a (c0 + osig (pa + pb alpha)(pg + ph alpha) + sigma ssa (mu ca + mv sa + mw)
   //          + kq q/Va + kde elev + kde2 elev^2 + kb1 beta + kb2 beta^2)
   //   lift:   CL0 + CLa a, stall 2 ca,  C_L_q c/2,  C_L_de elev                       (K = rho/2 S)
+  //   moment: Cm0 + Cma a, stall C_m_fp, C_m_q b/2, C_m_de elev                (K = rho/2 S c / Jy)
   //   drag:   CDp + (CL0 + CLa a)^2 / (pi e AR), stall 2 sa, C_D_q c/2, C_D_de elev^2,
   //           C_D_beta1 b + C_D_beta2 b^2                                            (K = rho/2 S)
-  //   moment: Cm0 + Cma a, stall C_m_fp, C_m_q b/2, C_m_de elev                        (K = rho/2 S c)
+  // on lanes 0 / 1 / 2: lane 1's pitch moment over Jy is row 1 of _f_omega_dot's torque term as it stands
   const int rr = Q.r == 3 ? 0 : Q.r;
   auto s3r = [rr](T x0, T x1, T x2) { return rr == 0 ? x0 : (rr == 1 ? x1 : x2); };
   const T z = T(0), one = T(1), two = T(2);
-  const T pa = s3r(a.CL0, a.CL0, a.Cm0), pb = s3r(a.CLa, a.CLa, a.Cma);
-  const T pg = s3r(one, a.CL0 * a.inv_pi_e_ar, one), ph = s3r(z, a.CLa * a.inv_pi_e_ar, z);
-  const T c0 = s3r(z, a.CDp, z), mu = s3r(two, z, z), mv = s3r(z, two, z), mw = s3r(z, z, a.Cmfp);
-  const T kq = s3r(a.kCLq, a.kCDq, a.kCmq), kde = s3r(a.CLde, z, a.Cmde), kde2 = s3r(z, a.CDde, z);
-  const T kb1 = s3r(z, a.CDb1, z), kb2 = s3r(z, a.CDb2, z), K = s3r(a.qS, a.qS, a.qSc);
+  const T pa = s3r(a.CL0, a.Cm0, a.CL0), pb = s3r(a.CLa, a.Cma, a.CLa);
+  const T pg = s3r(one, one, a.CL0 * a.inv_pi_e_ar), ph = s3r(z, z, a.CLa * a.inv_pi_e_ar);
+  const T c0 = s3r(z, z, a.CDp), mu = s3r(two, z, z), mv = s3r(z, z, two), mw = s3r(z, a.Cmfp, z);
+  const T kq = s3r(a.kCLq, a.kCmq, a.kCDq), kde = s3r(a.CLde, a.Cmde, z), kde2 = s3r(z, z, a.CDde);
+  const T kb1 = s3r(z, z, a.CDb1), kb2 = s3r(z, z, a.CDb2), K = Q.fK;
   const T P = (pa + pb * alpha) * (pg + ph * alpha);
   const T Cr = c0 + osig * P + (sigma * ssa) * (mu * ca + mv * sa + mw);
   const T Fr = K * V2a * (Cr + kq * qn + kde * elev + kde2 * (elev * elev) + kb1 * beta + kb2 * (beta * beta));
-  const T flift = bc<0>(Fr), fdrag = bc<1>(Fr), mm = bc<2>(Fr);
+  const T flift = bc<0>(Fr), fdrag = bc<2>(Fr);
   const T bp = a.hb * p * iVa, br = a.hb * r * iVa;
-  // side force / roll / yaw moment: the same formula with row constants, one item per lane (lane 3
-  // repeats lane 0's), broadcast
-  auto s3c = [&Q](T x0, T x1, T x2) { return Q.r == 1 ? x1 : (Q.r == 2 ? x2 : x0); };
-  const T g2 = s3c(a.qS, a.qSb, a.qSb) * V2a *
-               (s3c(a.CY0, a.Cl0, a.Cn0) + s3c(a.CYb, a.Clb, a.Cnb) * beta + s3c(a.CYp, a.Clp, a.Cnp) * bp +
-                s3c(a.CYr, a.Clr, a.Cnr) * br + s3c(a.CYda, a.Clda, a.Cnda) * ail);
-  const T fy = bc<0>(g2), ll = bc<1>(g2), nn = bc<2>(g2);
+  // side force Y (lane 1) and the roll / yaw torque rows of _f_omega_dot (pyfly.py:1659-1683) on lanes 0 / 2:
+  // row 0 = g3 (l + tprop) + g4 n, row 2 = g4 (l + tprop) + g8 n, with l, n, Y linear in the same items
+  // (pyfly.py:1581-1643) -- one formula with the torque-combined coefficients per lane; lane 3: zero
+  // (coefficients: QCtx; the propeller torque -kTP2 thr^2 adds to l, pyfly.py:1615-1643)
+  const T g2 = Q.tK * V2a * (Q.t0 + Q.tb * beta + Q.tp * bp + Q.tr * br + Q.tda * ail) + Q.tpr * (thr * thr);
+  const T fy = bc<1>(g2);
   // Row selections below pick among values computed on every lane: selects, not divergent branches
   // (a conditional expression with work in its arms compiles to exec-masked branches here).
   const bool r0 = Q.r == 0, r1 = Q.r == 1;
@@ -333,18 +355,16 @@ __device__ __forceinline__ int rhs_quad(const C& c, const A& a, const QCtx<T>& Q
   const T fg = a.mg * (r0 ? Rr2 : (r1 ? Rr1 : Dr));
   const T Vd = Va + thr * (a.kmotor - Va);
   const T fprop = a.prop_k * Vd * (Vd - Va);
-  const T tprop = -a.kTP2 * (thr * thr);
   const T fr = (r0 ? fprop : T(0)) + fg + fa;
-  const T t0 = ll + tprop, t1 = mm, t2 = nn;
 
-  const T P0 = bc<0>(om), Q0 = bc<1>(om), R0 = bc<2>(om);
   const T om1 = nx1(om), om2 = nx2(om), vel1 = nx1(vel), vel2 = nx2(vel);
-  // _f_attitude_dot (pyfly.py:1645-1657): row r = d eps_r, lane 3 = d e0
+  // _f_attitude_dot (pyfly.py:1645-1657): row r = d eps_r, lane 3 = d e0 = -(P e1 + Q e2 + R e3) / 2, the
+  // quad sum of omega_r eps_r (lane 3's omega slot is 0)
   const T deps = T(0.5) * (om * e0 + om2 * er1 - om1 * er2);
-  const T de0 = T(0.5) * (-P0 * e1 - Q0 * e2 - R0 * e3);
-  // _f_omega_dot (pyfly.py:1659-1683), row r
-  const T dw = Q.kpq * (P0 * Q0) + Q.kqr * (Q0 * R0) + Q.kpr * (P0 * R0) + Q.kpp * (P0 * P0 - R0 * R0) + Q.kt0 * t0 +
-               Q.kt1 * t1 + Q.kt2 * t2;
+  const T de0 = T(-0.5) * sum4(om * er);
+  // _f_omega_dot (pyfly.py:1659-1683), row r: gyroscopic terms + the torque row (lane 1: Fr, else g2)
+  const T dw = Q.kx * (om * om1) + Q.ky * (om1 * om2) + Q.kz * (om * om2) + Q.kw * (om2 * om2 - om1 * om1) +
+               rowsel<1>(Fr, g2);
   // _f_p_dot (pyfly.py:1706-1737), row r
   const T dp = Dr * vel + T(2) * (er * er1 - er2 * e0) * vel1 +
                T(2) * (er * er2 + er1 * e0) * vel2;
@@ -360,9 +380,10 @@ __device__ __forceinline__ int rhs_quad(const C& c, const A& a, const QCtx<T>& Q
   ds[3] = dv;
   ds[4] = da;
   ds[5] = dd;
-  if (!any_lane(key != KEY_NONE)) return 0;  // (wave-uniform) no condition violated: the common case
+  if (!any_lane(key != KEY_NONE)) return false;  // (wave-uniform) no condition violated: the common case
   key = min4(key);
-  return key == KEY_NONE ? 0 : FW_TERM_VAR(key_var(key));
+  term = key == KEY_NONE ? 0 : FW_TERM_VAR(key_var(key));
+  return true;
 }
 
 // Where one aircraft's integration stands at the start of a trial step (the resumable part of the
@@ -410,10 +431,15 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
   auto sq2 = [](V v) { return v.x * v.x + v.y * v.y; };
   // K = f(ys) at evaluation site k of a sequence begun with `nfev` evaluations done; `room` = evaluations
   // left before the budget (the bookkeeping of rk45()'s eval: one compare per evaluation, the count
-  // updated per sequence).  False once no lane of the wave integrates any more.
+  // updated per sequence).  False once no lane of the wave integrates any more.  `tight`: some lane of the
+  // wave may reach its budget within the sequence (wave-uniform) -- otherwise an evaluation without a
+  // violated condition anywhere in the wave goes on with two scalar branches.
   int room = c.max_nfev;
+  bool tight = true;
   auto eval = [&](bool first, int k) {
-    const int term = rhs_quad(c, a, Q, first, (const T*)ys, (T*)K);
+    int term = 0;
+    const bool viol = rhs_quad(c, a, Q, first, (const T*)ys, (T*)K, term);
+    if (!viol && !tight) return true;
     const bool stop = active && (term != 0 || k >= room);
     if (any_lane(stop)) {
       if (stop) {
@@ -504,6 +530,7 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
     }
     seeded = false;
     room = c.max_nfev - nfev;
+    tight = any_lane(active && room <= 6);
     if (!eval(false, 1)) break;  // K1
 #pragma unroll
     for (int p = 0; p < NQ; p++) {
@@ -641,7 +668,8 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
   for (;;) {
     if (!any_lane(active)) break;
     {
-      const int term = rhs_quad(c, a, Q, stage == 0, (const T*)ys, (T*)K);
+      int term = 0;
+      (void)rhs_quad(c, a, Q, stage == 0, (const T*)ys, (T*)K, term);
       if (active) {
         nfev++;
         if (term) {
@@ -806,7 +834,7 @@ __device__ __forceinline__ int rk45_quad(const C& c, const A& a, const StepCtx<T
                                          int r) {
   using V = V2<T>;
   constexpr int NQ = 3;
-  const QCtx<T> Q = qctx<T>(c, X, r);
+  const QCtx<T> Q = qctx<T>(c, a, X, r);
   V Y[NQ], F[NQ];
   {
     auto s3 = [r](T a0, T a1, T a2) { return r == 0 ? a0 : (r == 1 ? a1 : a2); };
@@ -883,7 +911,7 @@ __device__ __forceinline__ bool handoff(const C& c, const A& a, const StepCtx<T>
     const int src = st[k].src & 255;
     QRun Rq{st[k].t, st[k].t_new, st[k].h_abs, st[k].min_step, st[k].src >> 8, st[k].nfev, st[k].nacc};
     const StepCtx<T> Xs = st[k].X;
-    const QCtx<T> Q = qctx<T>(c, Xs, r);
+    const QCtx<T> Q = qctx<T>(c, a, Xs, r);
     V2<T>* const ysrc = sy - lane + src;
     V2<T>* const fsrc = sf - lane + src;
     auto el = [stride](V2<T>* base, int e) -> T& { return ((T*)(base + (e >> 1) * stride))[e & 1]; };
