@@ -123,8 +123,9 @@ int fw_policy_forward(const fw_mlp_policy* p, const float* obs, int64_t n, const
                       const float* high, float* actions, float* clipped, float* values, float* log_probs, void* stream);
 
 /* Two-pass merge of n_records moment records (1 + 2D doubles each: n_b, mean_b[D], M2_b[D], e.g. the
- * per-block records of fw_env_step's collect epilogue, fwsim.h fw_set_collect_epilogue) into one record
- * `out` of the same layout: mean = sum n_b mean_b / N, M2 = sum (M2_b + n_b (mean_b - mean)^2), every sum in
+ * per-block records of fw_env_step's collect epilogue, fwsim.h fw_set_collect_epilogue; stored
+ * column-major, field f of record b at records[f * n_records + b]) into one record `out` (1 + 2D doubles):
+ * mean = sum n_b mean_b / N, M2 = sum (M2_b + n_b (mean_b - mean)^2), every sum in
  * a fixed order.  The batch moments of RunningMeanStd.update (running_mean_std.py:20-24). */
 int fw_moments_merge(const double* records, int32_t n_records, int32_t D, double* out, void* stream);
 

@@ -264,7 +264,11 @@ enum fw_init_field {
 #define FW_BLK_COMMAND 5    /* 3 rows, T: last constrained commands (input order) */
 #define FW_BLK_PARAMS 6     /* FW_NPARAM rows, T: per-aircraft parameters (only with env->n_rand > 0) */
 #define FW_BLK_ACT_RING 7   /* window*3 rows, T: raw actions, action number k (1-based) in slot (k-1) % window,
-                               row slot*3 + component (the action-delta reward / action-window observation) */
+                               row slot*3 + component (the action-delta reward / action-window observation).
+                               This is the layout fw_get_state / fw_set_state exchange; on the device the ring
+                               is indexed by the aircraft's lifetime step count (slots stay aligned across
+                               aircraft whose episodes started at different steps, so a wave's ring accesses
+                               coalesce) and the two calls translate */
 #define FW_BLK_CMD_RING 8   /* window*3 rows, T: constrained commands, same layout (unscaled action windows) */
 #define FW_BLK_GOAL 9       /* 4 rows, uint32: the last 128 goal-status bits ("all"), bit 0 of row 0 newest */
 #define FW_NBLK 10
@@ -377,10 +381,12 @@ int fw_set_metrics_output(fw_handle* h, void* metrics_dev);
  * batch moments):
  *   ret      [N] fp64 discounted return: ret = ret * gamma + reward (VecNormalize._update_reward,
  *            vec_normalize.py:126-129), then ret[done] = 0 (vec_normalize.py:130) -- or NULL (no return column)
- *   records  fp64 [fw_collect_records(h)][1 + 2 * (n_obs_values + (ret != NULL))]: one exact two-pass
- *            moment record per launch block (n_b, mean_b[D], M2_b[D]) of the float32 observation (the VecEnv
- *            output: the reset observation of an auto-reset env) and of ret before its reset -- or NULL.
- *            Merge with fw_moments_merge / fw_vecnorm_merge_update (fwrollout.h).
+ *   records  fp64, D = n_obs_values + (ret != NULL): one exact two-pass moment record per launch block
+ *            (n_b, mean_b[D], M2_b[D]) of the float32 observation (the VecEnv output: the reset observation
+ *            of an auto-reset env) and of ret before its reset -- or NULL.  COLUMN-major: field f of block b
+ *            at records[f * R + b], R = fw_collect_records(h)'s n_records (so each field's loads coalesce);
+ *            size the buffer (1 + 2D) * max_records.  Merge with fw_moments_merge / fw_vecnorm_merge_update
+ *            (fwrollout.h), which read this layout.
  *   row_ctrl optional device int32: the launch does row_ctrl[0] += 1 after every block read its inputs
  *            (the rollout row of a captured collect step, fw_collect_policy in fwrollout.h).
  * Applies to fw_env_step only (not fw_env_rollout); NULL (or all fields NULL) turns it off. */
