@@ -275,6 +275,29 @@ FW_HD float fpow(float a, float p) {  // a > 0
 #endif
 }
 
+// max / min of |a|, |b| as ONE v_max_f32 / v_min_f32 with abs source modifiers.  fmaxf / fminf (and
+// v_med3 against +-inf, which the backend folds back into them) canonicalise each input first in IEEE
+// mode: three instructions for what the hardware does in one (NaN behaviour is the same: the other input).
+FW_HD float fmax_abs(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  float r;
+  asm("v_max_f32_e64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+#else
+  return fmaxf(fabsf(a), fabsf(b));
+#endif
+}
+FW_HD float fmin_abs(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  float r;
+  asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+#else
+  return fminf(fabsf(a), fabsf(b));
+#endif
+}
+FW_HD double fmax_abs(double a, double b) { return fmax(fabs(a), fabs(b)); }
+
 // atan2 for the RHS.  fp64: libm.  fp32: octant reduction + a degree-8 polynomial
 // in t^2 for atan(t), t in [0, 1] (fitted by tools/atan_fit in DESIGN.md; max abs
 // error 1.0e-7 rad, i.e. ~1 ulp at pi/4) -- ~20 instructions instead of the ~45 of
@@ -282,11 +305,7 @@ FW_HD float fpow(float a, float p) {  // a > 0
 FW_HD double fatan2(double y, double x) { return atan2(y, x); }
 FW_HD float fatan2(float y, float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  // max / min of |x|, |y| as v_med3 against -+inf: the abs folds into source modifiers and, unlike
-  // fmaxf / fminf in IEEE mode, no canonicalising v_max per input is emitted
-  const float inf = __builtin_inff();
-  const float mx = __builtin_amdgcn_fmed3f(fabsf(x), fabsf(y), inf);
-  const float mn = __builtin_amdgcn_fmed3f(fabsf(x), fabsf(y), -inf);
+  const float mx = fmax_abs(x, y), mn = fmin_abs(x, y);
   const float t = mn * __builtin_amdgcn_rcpf(mx);
   const float q = t * t;
   float p = 0.0029030926525592804f;
@@ -317,11 +336,8 @@ FW_HD void fatan2_2(double y0, double x0, double y1, double x1, double& r0, doub
 FW_HD void fatan2_2(float y0, float x0, float y1, float x1, float& r0, float& r1) {
 #if defined(__HIP_DEVICE_COMPILE__)
   typedef float F2 __attribute__((ext_vector_type(2)));
-  const float inf = __builtin_inff();
-  const float mx0 = __builtin_amdgcn_fmed3f(fabsf(x0), fabsf(y0), inf);
-  const float mn0 = __builtin_amdgcn_fmed3f(fabsf(x0), fabsf(y0), -inf);
-  const float mx1 = __builtin_amdgcn_fmed3f(fabsf(x1), fabsf(y1), inf);
-  const float mn1 = __builtin_amdgcn_fmed3f(fabsf(x1), fabsf(y1), -inf);
+  const float mx0 = fmax_abs(x0, y0), mn0 = fmin_abs(x0, y0);
+  const float mx1 = fmax_abs(x1, y1), mn1 = fmin_abs(x1, y1);
   F2 t;
   t.x = mn0 * __builtin_amdgcn_rcpf(mx0);
   t.y = mn1 * __builtin_amdgcn_rcpf(mx1);
@@ -372,7 +388,16 @@ FW_HD T clipv(T x, T lo, T hi) {
   // clamps to lo instead of propagating: NaN states fail the step via the step-size
   // control anyway (rk45: !(h_abs >= min_step)).
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (sizeof(T) == 4) return __builtin_amdgcn_fmed3f(x, lo, hi);
+  if constexpr (sizeof(T) == 4) {
+    if (__builtin_constant_p(hi) && hi == __builtin_inff()) {
+      // a lower bound only (a constant +inf upper bound of a specialised configuration): the backend turns
+      // the med3 into fmaxf, which canonicalises x first in IEEE mode -- one v_max instead of two
+      float r;
+      asm("v_max_f32_e64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(lo));
+      return r;
+    }
+    return __builtin_amdgcn_fmed3f(x, lo, hi);
+  }
 #endif
   return fmin(fmax(x, lo), hi);
 }
@@ -918,8 +943,8 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
         const V e = (ERV(p) + K[p] * T(E6)) * ht;
         const V y0 = Y(p), y1 = ys[p];
         V sc;
-        sc.x = frcp(atol + fmax(fabs(y0.x), fabs(y1.x)) * rtol);
-        sc.y = frcp(atol + fmax(fabs(y0.y), fabs(y1.y)) * rtol);
+        sc.x = frcp(atol + fmax_abs(y0.x, y1.x) * rtol);
+        sc.y = frcp(atol + fmax_abs(y0.y, y1.y) * rtol);
         es += sq2(e * sc);
       }
       const T en = fsqrt(es) * inv_sqrt_n;
@@ -1074,8 +1099,8 @@ rk_done:
         const V e = (ERV(p) + K[p] * T(E6)) * ht;
         const V y0 = YR(p), y1 = ys[p];
         V sc;
-        sc.x = frcp(atol + fmax(fabs(y0.x), fabs(y1.x)) * rtol);
-        sc.y = frcp(atol + fmax(fabs(y0.y), fabs(y1.y)) * rtol);
+        sc.x = frcp(atol + fmax_abs(y0.x, y1.x) * rtol);
+        sc.y = frcp(atol + fmax_abs(y0.y, y1.y) * rtol);
         es += sq2(e * sc);
       }
       const T en = fsqrt(es) * inv_sqrt_n;

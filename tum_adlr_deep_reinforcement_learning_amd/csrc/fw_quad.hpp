@@ -118,6 +118,7 @@ struct QCtx {
   // torque-row formula (tK, t0 .. tda, the propeller torque tpr); computed once here: with the products in
   // the arms of a per-lane select, the compiler branched on the lane in every RHS evaluation
   T fK, tK, t0, tb, tp, tr, tda, tpr;
+  T kprop;  // the propeller force's factor on row 0 (it acts along body x), 0 on the other rows
 };
 
 template <typename T, typename C, typename A>
@@ -196,6 +197,7 @@ __device__ __forceinline__ QCtx<T> qctx(const C& c, const A& a, const StepCtx<T>
   Q.tda = tq(a.Clda, a.Cnda, a.CYda);
   const T k3 = -a.kTP2 * g3, k4 = -a.kTP2 * g4;
   Q.tpr = s3r(k3, z, k4);
+  Q.kprop = r == 0 ? a.prop_k : z;
   return Q;
 }
 
@@ -354,8 +356,7 @@ __device__ __forceinline__ bool rhs_quad(const C& c, const A& a, const QCtx<T>& 
   const T Dr = er * er + e0 * e0 - er1 * er1 - er2 * er2;
   const T fg = a.mg * (r0 ? Rr2 : (r1 ? Rr1 : Dr));
   const T Vd = Va + thr * (a.kmotor - Va);
-  const T fprop = a.prop_k * Vd * (Vd - Va);
-  const T fr = (r0 ? fprop : T(0)) + fg + fa;
+  const T fr = Q.kprop * Vd * (Vd - Va) + fg + fa;  // propeller force on row 0 only (QCtx)
 
   const T om1 = nx1(om), om2 = nx2(om), vel1 = nx1(vel), vel2 = nx2(vel);
   // _f_attitude_dot (pyfly.py:1645-1657): row r = d eps_r, lane 3 = d e0 = -(P e1 + Q e2 + R e3) / 2, the
@@ -581,8 +582,8 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
       const V e = (ER[p] + K[p] * T(E6)) * ht;
       const V y0 = Y[p], y1 = ys[p];
       V sc;
-      sc.x = frcp(atol + fmax(fabs(y0.x), fabs(y1.x)) * rtol);
-      sc.y = frcp(atol + fmax(fabs(y0.y), fabs(y1.y)) * rtol);
+      sc.x = frcp(atol + fmax_abs(y0.x, y1.x) * rtol);
+      sc.y = frcp(atol + fmax_abs(y0.y, y1.y) * rtol);
       es += sq2(e * sc);
     }
     const T en = fsqrt(qd::sum4(es)) * inv_sqrt_n;
@@ -764,8 +765,8 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
         const V e = (ER[p] + K[p] * T(E6)) * ht;
         const V y0 = Y[p], y1 = ys[p];
         V sc;
-        sc.x = frcp(atol + fmax(fabs(y0.x), fabs(y1.x)) * rtol);
-        sc.y = frcp(atol + fmax(fabs(y0.y), fabs(y1.y)) * rtol);
+        sc.x = frcp(atol + fmax_abs(y0.x, y1.x) * rtol);
+        sc.y = frcp(atol + fmax_abs(y0.y, y1.y) * rtol);
         es += sq2(e * sc);
       }
       const T en = fsqrt(qd::sum4(es)) * inv_sqrt_n;
