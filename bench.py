@@ -620,7 +620,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32" if args.precision == "float32" else "f64",
-            "data": "synthetic: seeded Philox initial states, U(-1,1) actions pre-generated on device; timed in the "
+            "data": "synthetic: seeded Philox initial states, U(-1,1) actions pre-generated on device (a pool of 16 "
+                    "batches replayed cyclically); timed in the "
                     "steady state (%d untimed steps after the global reset, then %d warm-up steps)"
                     % (args.prep, args.warmup),
             "config": {"workload": "FixedWingAircraft.step x %d aircraft in total, %d per GPU (attitude task, "
