@@ -1,6 +1,8 @@
 #!/bin/bash
-# Policy-launch timing diagnostics (wrong results, timing only): shipped kernel vs no tanh (FW_POL_DIAG=1) vs no
-# hidden-layer MFMA (FW_POL_DIAG=2), tools/pol_bench.py per library variant.
+# Policy-launch timing diagnostics (results wrong, timing only).  Build the variants first (CPU):
+#   for k in 1 2 3 4; do python tools/ab.py build diag$k -DFW_POL_DIAG=$k; done
+# (1 = no tanh, 2 = no hidden-layer MFMA, 3 = no LDS weight fill, 4 = no output stores; fw_rollout.hip), then
+# drop ./tools/_build/variants from .gpurunignore for the run.  tools/pol_bench.py per library variant.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 OUT=gpurun_out/${1:-poldiag}
 mkdir -p "$OUT"

@@ -776,6 +776,11 @@ struct PolArgs {
 };
 
 constexpr int PM_WAVES = 4;  // waves per block; two blocks per CU (two waves per SIMD)
+#ifndef FW_POL_DIAG
+// timing diagnostics only (tools/r04_poldiag.sh builds library variants; their results are wrong): 1 = no tanh,
+// 2 = no hidden-layer MFMA, 3 = no LDS weight fill, 4 = no row / output stores, 5 = no observation normalisation
+#define FW_POL_DIAG 0
+#endif
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -866,7 +871,7 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
   const int64_t n = G.n;
   // ---- the block's A-operand image in LDS (two blocks per CU, two waves per SIMD: one wave's MFMAs overlap
   // the other's tanh / loads; with the weights in registers a wave took 430 VGPRs and ran alone on its SIMD)
-  pol_fill_lds<S>(G.P, Wl);
+  if (FW_POL_DIAG != 3) pol_fill_lds<S>(G.P, Wl);
   const float* W0 = Wl + L::L0 + lane * S;
   const float* W1 = Wl + L::L1 + lane * 4;
   const float* WH = Wl + L::HD + lane * 4;
@@ -949,15 +954,15 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
     for (int s = 0; s < S; s++) {
       const int f = 4 * s + g;
       float o = (valid && f < d) ? cur.o[s] : 0.0f;
-      if (nobs && valid && f < d) o = norm_obs_val(o, mean[s], den[s], G.clip_obs);
+      if (FW_POL_DIAG != 5 && nobs && valid && f < d) o = norm_obs_val(o, mean[s], den[s], G.clip_obs);
       x[s] = o;
-      if (obs_rows && valid && f < d) obs_rows[env * d + f] = o;
+      if (FW_POL_DIAG != 4 && obs_rows && valid && f < d) obs_rows[env * d + f] = o;
     }
     // ---- the previous step's reward row (normalised) and the episode starts of this row
     if (rows_prev && g == 1 && valid) {
       double r = (double)cur.r;
       if (G.rms && G.norm_rew) r = fmin(fmax(r / rden, -G.clip_rew), G.clip_rew);
-      G.rew_rows[(row - 1) * n + env] = (float)r;
+      if (FW_POL_DIAG != 4) G.rew_rows[(row - 1) * n + env] = (float)r;
       G.start_rows[row * n + env] = (uint8_t)cur.dn;
     }
     asm volatile("" ::: "memory");  // the A operands are re-read from LDS every tile (not hoisted into VGPRs)
@@ -985,8 +990,8 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
     for (int T = 0; T < 4; T++)
 #pragma unroll
       for (int v = 0; v < 4; v++) {
-        hpv[T][v] = ftanh2(cp[T][v]);
-        hvv[T][v] = ftanh2(cv[T][v]);
+        hpv[T][v] = FW_POL_DIAG == 1 ? cp[T][v] : ftanh2(cp[T][v]);
+        hvv[T][v] = FW_POL_DIAG == 1 ? cv[T][v] : ftanh2(cv[T][v]);
       }
     // ---- layer 1
 #pragma unroll
@@ -998,6 +1003,11 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
     for (int T = 0; T < 4; T++)
 #pragma unroll
       for (int O = 0; O < 4; O++) {
+        if (FW_POL_DIAG == 2) {
+          cp[O] += hpv[T];
+          cv[O] += hvv[T];
+          continue;
+        }
         const f32x4 ap = lds4(W1 + ((0 * 4 + O) * 4 + T) * 256), av = lds4(W1 + ((1 * 4 + O) * 4 + T) * 256);
 #pragma unroll
         for (int v = 0; v < 4; v++) {
@@ -1009,8 +1019,8 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
     for (int T = 0; T < 4; T++)
 #pragma unroll
       for (int v = 0; v < 4; v++) {
-        hpv[T][v] = ftanh2(cp[T][v]);
-        hvv[T][v] = ftanh2(cv[T][v]);
+        hpv[T][v] = FW_POL_DIAG == 1 ? cp[T][v] : ftanh2(cp[T][v]);
+        hvv[T][v] = FW_POL_DIAG == 1 ? cv[T][v] : ftanh2(cv[T][v]);
       }
     // ---- heads: actor rows 0..A-1 and the value row 15 of one tile (two accumulators, disjoint rows)
     f32x4 ha = {0.0f, 0.0f, 0.0f, 0.0f}, hc = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -1031,7 +1041,7 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
     f32x4 hi;
 #pragma unroll
     for (int v = 0; v < 4; v++) hi[v] = __shfl(out[v], (lane + 16) & 63);
-    if (g == 3 && valid) val[env] = out[3];
+    if (FW_POL_DIAG != 4 && g == 3 && valid) val[env] = out[3];
     if (g == 0 && valid) {
       float lp = 0.0f;
 #pragma unroll
@@ -1044,11 +1054,11 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
           const float ac = noise ? m + sd * cur.z[a] : m;
           const float dv = ac - m;
           lp = lp + (((-(dv * dv)) / ((2.0f * sd) * sd) - ls) - half_log_2pi);
-          act[env * A + a] = ac;
-          if (G.clipped) G.clipped[env * A + a] = fmaxf(fminf(ac, hiA[a]), loA[a]);
+          if (FW_POL_DIAG != 4) act[env * A + a] = ac;
+          if (FW_POL_DIAG != 4 && G.clipped) G.clipped[env * A + a] = fmaxf(fminf(ac, hiA[a]), loA[a]);
         }
       }
-      logp[env] = lp;
+      if (FW_POL_DIAG != 4) logp[env] = lp;
     }
   }
 }
