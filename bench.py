@@ -199,6 +199,7 @@ def rollout_leg(spec, n, T, dev, rank, world, precision):
     gae_bytes = (4 + 4 + 1 + 4 + 4) * T * n + (4 + 1) * n
     out = {"horizon": T, "envs_per_gpu": n, "global_envs": n * world, "collect_graphed": graph,
            "host_launches_per_step": col.host_launches_per_step(), "fused_step": bool(getattr(col, "_fused_graph", False)),
+           "capture_error": getattr(col, "capture_error", None),
            "graph_kernel_nodes": [t.count(0) for t in col.graph_nodes()] if getattr(col, "_fused_graph", False) else None,
            "collect_s": collect_s,
            "allgather_s": gather_s if world > 1 else 0.0, "env_steps_per_s": n * world * T / total_s,

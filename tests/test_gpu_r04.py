@@ -377,3 +377,49 @@ def test_fused_collect_rccl_world1_single_graph():
         runs.append(snaps)
     for x, y in zip(*runs):
         assert torch.equal(x, y)
+
+
+def test_fused_collect_falls_back_when_the_collective_cannot_be_captured():
+    """If the RCCL exchange refuses stream capture (forced here: the all-gather raises while the stream is
+    capturing), the fused sharded step is recaptured as two graphs around an eager all-gather, says why in
+    `capture_error`, and still equals the eager collection bit for bit (world-1 nccl group)."""
+    import socket
+    import torch.distributed as dist
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
+                            device_id=torch.device(DEV))
+    try:
+        va, ea, ba, ca = _collect_setup(4096, 32)
+        vb, eb, bb, cb = _collect_setup(4096, 32)
+        gather = eb._gather
+
+        def refusing_gather(rec):
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("collective not capturable (forced by the test)")
+            return gather(rec)
+
+        eb._gather = refusing_gather
+        for c in (ca, cb):
+            torch.manual_seed(40)
+            c.collect(8)
+        for i in range(2):
+            torch.manual_seed(41 + i)
+            ca.collect()
+            torch.manual_seed(41 + i)
+            if i == 0:  # the first graphed collection captures (and falls back), the second replays
+                with pytest.warns(UserWarning, match="could not be captured"):
+                    cb.collect(graph=True)
+            else:
+                cb.collect(graph=True)
+            for x, y in zip((ba.slab, ba.rewards, ba.dones, ca.last_obs, ca.last_dones, ea.rms, ea.ret),
+                            (bb.slab, bb.rewards, bb.dones, cb.last_obs, cb.last_dones, eb.rms, eb.ret)):
+                assert torch.equal(x, y)
+        assert cb._fused_graph and len(cb._graphs) == 2 and "forced by the test" in cb.capture_error
+        assert cb.host_launches_per_step() == 3
+        va.close()
+        vb.close()
+    finally:
+        dist.destroy_process_group()

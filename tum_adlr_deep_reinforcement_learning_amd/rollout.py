@@ -18,6 +18,7 @@ episode starts live outside the slab (inputs of the scan, not of the update).
 """
 import collections
 import ctypes
+import warnings
 
 import numpy as np
 import torch
@@ -575,12 +576,9 @@ class RolloutCollector:
             if grouped:
                 vn._merge()
 
-        if vn is not None:
-            vn.set_epilogue(row_ctrl=self._ctrl)
-        else:
-            eng.set_collect_epilogue(row_ctrl=self._ctrl)
-        try:  # keep_graph: graph_nodes() can list what a step launches
-            self._graphs = [torch.cuda.CUDAGraph(keep_graph=True)]
+        def capture(split):
+            self._graphs = [torch.cuda.CUDAGraph(keep_graph=True)]  # keep_graph: graph_nodes() lists the launches
+            self._graphK = None
             if split:
                 self._graphs.append(torch.cuda.CUDAGraph(keep_graph=True))
                 with torch.cuda.graph(self._graphs[0]):
@@ -601,18 +599,35 @@ class RolloutCollector:
                 # and K steps in one graph: one host replay (and one inter-graph gap) per K steps; the rows,
                 # noise row and counter advance on the device, so the K copies are the same launches
                 K = max(1, int(self.steps_per_graph))
-                self._graphK = None
                 if K > 1:
                     self._graphK = torch.cuda.CUDAGraph(keep_graph=True)
                     with torch.cuda.graph(self._graphK):
                         for _ in range(K):
                             step()
+            for g in self._graphs:
+                g.instantiate()
+            if self._graphK is not None:
+                self._graphK.instantiate()
+
+        if vn is not None:
+            vn.set_epilogue(row_ctrl=self._ctrl)
+        else:
+            eng.set_collect_epilogue(row_ctrl=self._ctrl)
+        self.capture_error = None
+        try:
+            try:
+                capture(split)
+            except Exception as e:  # noqa: BLE001 -- the collective would not capture: split around it instead
+                if split or not grouped:
+                    raise
+                self.capture_error = "%s: %s" % (type(e).__name__, e)
+                warnings.warn("the RCCL exchange could not be captured into the collect graph (%s); "
+                              "replaying two graphs around an eager all-gather" % self.capture_error)
+                torch.cuda.synchronize(dev)
+                split = True
+                capture(split)
         finally:
             eng.set_collect_epilogue()
-        for g in self._graphs:
-            g.instantiate()
-        if getattr(self, "_graphK", None) is not None:
-            self._graphK.instantiate()
         self._fused_graph = True
         self._fused_parts = (vn, eng, grouped, stats_exchange)
         self._key = self.graph_key()
