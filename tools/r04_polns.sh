@@ -1,4 +1,5 @@
 #!/bin/bash
+# (The net-split kernel was not adopted and is no longer in fw_rollout.hip; profiles/r04_ab_collect.log has the result.)
 # Net-split policy kernel (k_policy_mfma_ns) vs the two-net kernel (FW_POL_NS=0): standalone launch time,
 # the policy / collect GPU tests, and the collect legs (64-step bench leg and configs[2] 2048).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
