@@ -303,12 +303,14 @@ __device__ __forceinline__ void merge_records(const double* __restrict__ part, i
 // butterflies serialised ~100 dependent LDS round trips per pass (tools/merge_bench.py: 19 us at 64 records).
 constexpr int MERGE16_THREADS = 256, MERGE16_BATCH = 4;
 __device__ __forceinline__ double sum16_cols(double (*tp)[MERGE16_THREADS + 1], double (*pp)[17], int ncols) {
-  // column j (< ncols) of tp summed over the 256 threads: thread 16 j + h sums threads 16 h .. 16 h + 15
+  // column j (< ncols) of tp summed over the 256 threads: thread 16 j + h sums threads h, h + 16, ..., h + 240
+  // (the 16 lanes of a column read 16 consecutive doubles per step: no LDS bank conflicts; contiguous runs of
+  // 16 per lane, 128 B apart, conflicted 16 ways)
   const int tid = threadIdx.x, j = tid >> 4, h = tid & 15;
   if (j < ncols) {
     double a = 0.0;
 #pragma unroll
-    for (int k = 0; k < 16; k++) a += tp[j][16 * h + k];
+    for (int k = 0; k < 16; k++) a += tp[j][h + 16 * k];
     pp[j][h] = a;
   }
   __syncthreads();
