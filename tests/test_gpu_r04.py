@@ -426,12 +426,13 @@ def test_fused_collect_falls_back_when_the_collective_cannot_be_captured():
 
 
 def test_fused_collect_ragged_batch_equals_eager():
-    """A ragged batch (1036 envs -- graphed collects need a multiple of 4: a partial last policy tile, a partial
-    last env block) through the fused collect step, 40 steps = two 16-step graph replays + 8 single-step replays:
-    graphed == eager bit for bit, GAE == oracle, the statistics' count advances by 1036 per step."""
+    """A ragged batch (1037 envs: a partial last policy tile, a partial last env block, an env count the unfused
+    graphed step -- dword row copies -- cannot take) through the fused collect step, 40 steps = two 16-step
+    graph replays + 8 single-step replays: graphed == eager bit for bit, GAE == oracle, and the statistics'
+    count advances by 1037 per step."""
     from oracle import rollout_oracle as R
-    va, ea, ba, ca = _collect_setup(1036, 40, True, seed=33)
-    vb, eb, bb, cb = _collect_setup(1036, 40, True, seed=33)
+    va, ea, ba, ca = _collect_setup(1037, 40, True, seed=33)
+    vb, eb, bb, cb = _collect_setup(1037, 40, True, seed=33)
     for c in (ca, cb):
         torch.manual_seed(50)
         c.collect(8)
@@ -445,7 +446,7 @@ def test_fused_collect_ragged_batch_equals_eager():
     for f in ("slab", "rewards", "dones"):
         assert torch.equal(getattr(ba, f), getattr(bb, f)), f
     assert torch.equal(ca.last_obs, cb.last_obs) and torch.equal(ea.rms, eb.rms) and torch.equal(ea.ret, eb.ret)
-    assert abs(float(eb.rms[2 * d]) - (count0 + 40 * 1036)) < 1e-6  # (the count starts at SB3's epsilon)
+    assert abs(float(eb.rms[2 * d]) - (count0 + 40 * 1037)) < 1e-6  # (the count starts at SB3's epsilon)
     with torch.no_grad():
         lv = cb.policy.predict_values(cb.last_obs).reshape(-1).cpu().numpy()
     a_ref, _ = R.gae(bb.rewards.cpu().numpy(), bb.values.cpu().numpy(), bb.dones.cpu().numpy(), lv,

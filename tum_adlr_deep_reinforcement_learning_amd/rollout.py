@@ -353,10 +353,14 @@ class RolloutCollector:
     # ------------------------------------------------------------ graphed collection
     def _graph_ok(self):
         buf = self.buffer
-        if buf.device.type != "cuda" or buf.n_envs % 4:  # fw_rollout_store moves whole dwords (uint8 rows)
+        if buf.device.type != "cuda":
             return False
         venv = getattr(self.env, "venv", self.env)
-        return getattr(venv, "_hists", None) is None  # a history recorder syncs to the host every step
+        if getattr(venv, "_hists", None) is not None:  # a history recorder syncs to the host every step
+            return False
+        # the unfused captured step's fw_rollout_store moves whole dwords (uint8 rows); the fused step's
+        # fw_collect_policy stores each env's episode start on its own
+        return buf.n_envs % 4 == 0 or self._fused_collect_ok()
 
     def _split(self):
         """The env exchanges statistics between shards every step: capture around the collective."""
