@@ -503,12 +503,12 @@ def main():
     ap.add_argument("--no-open-loop", action="store_true", help="skip the open-loop rollout line (fw_env_rollout)")
     ap.add_argument("--long-window", type=int, default=1000,
                     help="after the timed steps, time this many more for the long-window steady-state line")
-    ap.add_argument("--rollout-steps", type=int, default=-1,
-                    help="also run one PPO collect_rollouts of this horizon (2048 = BASELINE configs[2]/[3]); "
-                         "default 64 (on N > 1 GPUs configs[3]: sharded collection + the RCCL all-gather); "
-                         "0 = skip")
-    ap.add_argument("--sac-fill-steps", type=int, default=0,
-                    help="also run a SAC replay-buffer fill of this many steps (BASELINE configs[4])")
+    ap.add_argument("--rollout-steps", type=int, default=2048,
+                    help="also run one PPO collect_rollouts of this horizon (default 2048 = BASELINE configs[2]; on "
+                         "N > 1 GPUs configs[3]: sharded collection + the RCCL all-gather of the slab); 0 = skip")
+    ap.add_argument("--sac-fill-steps", type=int, default=1000,
+                    help="also run a SAC replay-buffer fill of this many steps (BASELINE configs[4], default 1000 "
+                         "steps of --sac-envs envs); 0 = skip")
     ap.add_argument("--sac-envs", type=int, default=262144, help="global envs of the SAC fill leg")
     ap.add_argument("--no-replay", action="store_true",
                     help="skip the stats-enabled replay of the timed window (per-launch times, nfev, budget hits)")
@@ -582,7 +582,7 @@ def main():
                                  "env_steps_per_s_per_gpu": n / (f_early * 1e-3)},
                 "long_window": ({"steps": args.long_window, "kernel_ms": f_long,
                                  "env_steps_per_s": args.envs / (f_long * 1e-3)} if f_long > 0 else None),
-                "isa": "profiles/r03_isa_resources.txt (VGPR / spill counts per kernel instance)"}
+                "isa": "profiles/r05_isa_resources.txt (VGPR / spill counts per kernel instance)"}
 
     esz = 4 if args.precision == "float32" else 8
     rd, wr = algorithmic_bytes_per_env_step(spec, esz)
@@ -599,14 +599,25 @@ def main():
                      "source": "SQ_INSTS_VALU per k_env_step dispatch from profiles/pmc_env_step.json (%s) over "
                                "this window's kernel_ms" % pm.get("dispatches")}
 
+    # the configs[2]/[3] and configs[4] legs come last: a failure there is reported in the line instead of
+    # costing the headline (an error that strikes every rank alike; a one-rank failure inside a collective
+    # still hangs the job)
     rollout = None
-    if args.rollout_steps < 0:  # configs[2]/[3]-shaped PPO collection, short horizon by default
-        args.rollout_steps = 64
     if args.rollout_steps > 0:
-        rollout = rollout_leg(spec, n, args.rollout_steps, dev, rank, world, args.precision)
+        _log("rollout leg (%d steps)" % args.rollout_steps)
+        try:
+            rollout = rollout_leg(spec, n, args.rollout_steps, dev, rank, world, args.precision)
+        except Exception as e:  # noqa: BLE001
+            rollout = {"horizon": args.rollout_steps, "error": "%s: %s" % (type(e).__name__, e)}
+        torch.cuda.empty_cache()
     sac = None
     if args.sac_fill_steps > 0:
-        sac = sac_fill_leg(args.sac_envs // world, args.sac_fill_steps, dev, rank, world, args.precision)
+        _log("SAC fill leg (%d envs x %d steps)" % (args.sac_envs, args.sac_fill_steps))
+        try:
+            sac = sac_fill_leg(args.sac_envs // world, args.sac_fill_steps, dev, rank, world, args.precision)
+        except Exception as e:  # noqa: BLE001
+            sac = {"steps": args.sac_fill_steps, "error": "%s: %s" % (type(e).__name__, e)}
+        torch.cuda.empty_cache()
 
     if rank == 0:
         out = {

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FWSIM_ABI_VERSION 8
+#define FWSIM_ABI_VERSION 9
 
 /* ---- error codes ---------------------------------------------------------- */
 #define FW_OK 0
@@ -294,7 +294,8 @@ int fw_seed(fw_handle* h, uint64_t seed, int64_t env_offset);
  * Wind.reset hands to DrydenGustModel.reset, dryden.py:174-188): N(0,1) samples, SoA [4][len][N],
  * read from index 0 at each reset; step k of an episode reads sample k mod len (dryden.py:209-236
  * wraps a sequence shorter than the episode).  NULL reverts to the on-device Philox generator.  The
- * buffer must stay alive while the handle uses it.                                                 */
+ * buffer must stay alive while the handle uses it.  Every call drops the per-env lengths
+ * (fw_set_noise_lengths), which describe a buffer: set them again after it.                        */
 int fw_set_noise(fw_handle* h, const void* noise_dev, int64_t len);
 
 /* Per-env injection (env_method("reset", indices=..., turbulence_noise=...) -> FixedWingAircraft.reset
@@ -386,15 +387,25 @@ int fw_set_metrics_output(fw_handle* h, void* metrics_dev);
  *            of an auto-reset env) and of ret before its reset -- or NULL.  COLUMN-major: field f of block b
  *            at records[f * R + b], R = fw_collect_records(h)'s n_records (so each field's loads coalesce);
  *            size the buffer (1 + 2D) * max_records.  Merge with fw_moments_merge / fw_vecnorm_merge_update
- *            (fwrollout.h), which read this layout.
+ *            (fwrollout.h), which read this layout -- or inside the launch (merged).
  *   row_ctrl optional device int32: the launch does row_ctrl[0] += 1 after every block read its inputs
  *            (the rollout row of a captured collect step, fw_collect_policy in fwrollout.h).
+ *   merged   (ABI 9; needs records) fp64 [1 + 2D]: the launch itself merges its block records (a tree of
+ *            64-record nodes, each merged in block order by the last block to reach it, so the result is
+ *            deterministic) into one record (N, mean[D], M2[D]), the layout fw_rms_update reads -- what
+ *            fw_moments_merge returns, to rounding (another summation tree).  NULL: merge later.
+ *   rms      (ABI 9; needs merged) the fw_rms_update statistics buffer [2d + 4]: the launch also applies
+ *            RunningMeanStd.update_from_moments (running_mean_std.py:26-40) with the merged record, the
+ *            same arithmetic as fw_rms_update of that one record.  A collect step under one VecNormalize is
+ *            then policy + env step, two launches.  NULL: update later (sharded: after the exchange).
  * Applies to fw_env_step only (not fw_env_rollout); NULL (or all fields NULL) turns it off. */
 typedef struct fw_collect_epilogue {
   double* ret;
   double gamma;
   double* records;
   int32_t* row_ctrl;
+  double* merged;
+  double* rms;
 } fw_collect_epilogue;
 int fw_set_collect_epilogue(fw_handle* h, const fw_collect_epilogue* epi);
 /* Records the next fw_env_step writes (its block count: depends on N and fw_get_lanes) and the most any

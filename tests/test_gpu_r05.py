@@ -1,0 +1,240 @@
+"""GPU tests of round 5, all through the C ABI.
+
+  in-launch merge tree  fw_env_step's collect epilogue with ``merged`` / ``rms`` (ABI 9): the merged record
+                        equals a numpy restatement of the same tree over the launch's own block records BIT
+                        FOR BIT on every step (one, two and three tree levels; one lane and quads), numpy's
+                        mean / var of the step's observations and returns to 1e-12, and the in-launch
+                        update_from_moments equals fw_rms_update of that record bit for bit; two engines with
+                        the same seed produce the same bits (the tree does not depend on block timing)
+  fused collect         one graph of TWO kernels per step (policy, env step) with VecNormalize; graphed ==
+                        eager bit for bit; GAE == oracle
+  noise injection       set_noise after set_env_noise replaces the per-env lengths (no stale pointer: every
+                        env reads the shared sequence); a full VecEnv reset and a recording-mode auto-reset end
+                        a per-env injection (the env draws Philox again, as Dryden.reset(None) draws fresh noise)
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from tum_adlr_deep_reinforcement_learning_amd import config as C
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+FANIN = 64  # fw_stats::MERGE_FANIN
+
+
+def _P(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _merge_node(n, m, q):
+    """k_env_step's merge_node: sums in record order, each product and sum rounded (no FMA)."""
+    D = m.shape[1]
+    S, N = np.zeros(D), 0.0
+    for k in range(len(n)):
+        S = S + n[k] * m[k]
+        N = N + n[k]
+    mean = S / N
+    M2 = np.zeros(D)
+    for k in range(len(n)):
+        dm = m[k] - mean
+        M2 = M2 + (q[k] + n[k] * (dm * dm))
+    return N, mean, M2
+
+
+def _merge_tree(n, m, q):
+    """fw_stats' tree: levels of 64-record groups until at most 64 records remain, then the final node."""
+    levels = 0
+    while len(n) > FANIN:
+        out = [_merge_node(n[g:g + FANIN], m[g:g + FANIN], q[g:g + FANIN]) for g in range(0, len(n), FANIN)]
+        n = np.array([o[0] for o in out])
+        m = np.stack([o[1] for o in out])
+        q = np.stack([o[2] for o in out])
+        levels += 1
+    return _merge_node(n, m, q), levels + 1
+
+
+@pytest.mark.parametrize("n,lanes,levels", [(1000, 4, 1), (20037, 1, 2), (70001, 4, 3)])
+def test_in_launch_merge_tree_bitwise(n, lanes, levels):
+    from tum_adlr_deep_reinforcement_learning_amd import _native
+    from tum_adlr_deep_reinforcement_learning_amd.vec_env import FixedWingVecEnv
+    lib = _native.load()
+    envs = [FixedWingVecEnv(n, config_kw={"steps_max": 12}, sim_config_kw={"turbulence": False}, device=DEV, seed=9,
+                            return_tensors=True, info_target=False, lanes=lanes) for _ in range(2)]
+    for v in envs:
+        v.reset()
+    eng = envs[0].engine
+    d = eng.n_obs_values
+    D = d + 1
+    nrec, nmax = eng.collect_records()
+    g = torch.Generator(device=DEV)
+    g.manual_seed(n)
+    ret0 = torch.randn(n, generator=g, device=DEV, dtype=torch.float64)
+    rms0 = torch.rand(2 * d + 4, generator=g, device=DEV, dtype=torch.float64) + 0.5
+    bufs = []
+    for v in envs:
+        bufs.append(dict(ret=ret0.clone(), rms=rms0.clone(),
+                         rec=torch.full((nmax * (1 + 2 * D),), float("nan"), dtype=torch.float64, device=DEV),
+                         merged=torch.full((1 + 2 * D,), float("nan"), dtype=torch.float64, device=DEV),
+                         ctrl=torch.zeros(2, dtype=torch.int32, device=DEV)))
+    gamma = 0.99
+    for k in range(14):  # episodes end at step 12: done envs reset inside the window
+        a = torch.rand(n, 3, generator=g, device=DEV) * 2 - 1
+        ret_before = bufs[0]["ret"].clone()
+        rms_before = bufs[0]["rms"].clone()
+        outs = []
+        for v, b in zip(envs, bufs):
+            v.engine.set_collect_epilogue(ret=b["ret"], gamma=gamma, records=b["rec"], row_ctrl=b["ctrl"],
+                                          merged=b["merged"], rms=b["rms"])
+            outs.append(v.engine.env_step(a))
+            v.engine.set_collect_epilogue()
+        torch.cuda.synchronize()
+        b = bufs[0]
+        # the tree over the launch's own block records, restated in numpy: bit for bit
+        R = b["rec"][:nrec * (1 + 2 * D)].reshape(1 + 2 * D, nrec).cpu().numpy()
+        (N, mean, M2), lv = _merge_tree(R[0], R[1:D + 1].T, R[D + 1:].T)
+        assert lv == levels
+        got = b["merged"].cpu().numpy()
+        assert got[0] == N == n
+        assert np.array_equal(got[1:D + 1], mean) and np.array_equal(got[D + 1:], M2), k
+        # ... and numpy's statistics of the step
+        obs, rew, done, _ = outs[0]
+        r_new = ret_before.cpu().numpy() * gamma + rew.cpu().numpy().astype(np.float32).astype(np.float64)
+        xs = np.concatenate([obs.cpu().numpy().astype(np.float32).astype(np.float64), r_new[:, None]], 1)
+        np.testing.assert_allclose(got[1:D + 1], xs.mean(0), rtol=1e-12, atol=1e-13)
+        np.testing.assert_allclose(got[D + 1:] / n, xs.var(0), rtol=1e-12, atol=1e-13)
+        # the in-launch update_from_moments == fw_rms_update of the merged record
+        want = rms_before.clone()
+        _native.check(lib.fw_rms_update(_P(b["merged"]), 1, d, 1, _P(want), 1, 1, None), "fw_rms_update")
+        torch.cuda.synchronize()
+        assert torch.equal(b["rms"], want) and not torch.equal(b["rms"], rms_before)
+        # the second engine (same seed, same actions): the same bits
+        for f in ("merged", "rms", "ret"):
+            assert torch.equal(bufs[1][f], b[f]), f
+        assert int(b["ctrl"][0]) == k + 1
+    for v in envs:
+        v.close()
+
+
+def test_fused_collect_is_two_launches_and_equals_eager():
+    """With VecNormalize the fused collect step is one graph of two kernels (fw_collect_policy, fw_env_step
+    merging + updating the statistics in its own launch); graphed == eager bit for bit; GAE == oracle; the
+    statistics equal the three-launch form (merge as its own launch) to rounding."""
+    from oracle import rollout_oracle as R
+    from test_gpu_r04 import _collect_setup
+    va, ea, ba, ca = _collect_setup(2048, 40)
+    vb, eb, bb, cb = _collect_setup(2048, 40)
+    vc, ec, bc, cc = _collect_setup(2048, 40)
+    ec.merge_in_launch = False
+    for c in (ca, cb, cc):
+        torch.manual_seed(40)
+        c.collect(8)
+    for i in range(2):
+        for c, gr in ((ca, False), (cb, True), (cc, True)):
+            torch.manual_seed(41 + i)
+            c.collect(graph=gr)
+        for f in ("slab", "rewards", "dones"):
+            assert torch.equal(getattr(ba, f), getattr(bb, f)), f
+        assert torch.equal(ca.last_obs, cb.last_obs) and torch.equal(ea.rms, eb.rms) and torch.equal(ea.ret, eb.ret)
+        np.testing.assert_allclose(eb.rms.cpu().numpy(), ec.rms.cpu().numpy(), rtol=1e-9, atol=1e-12)
+    nodes = cb.graph_nodes()
+    assert len(nodes) == 1 and nodes[0].count(0) == 2, nodes
+    assert cc.graph_nodes()[0].count(0) == 3
+    with torch.no_grad():
+        lv = cb.policy.predict_values(cb.last_obs).reshape(-1).cpu().numpy()
+    a_ref, _ = R.gae(bb.rewards.cpu().numpy(), bb.values.cpu().numpy(), bb.dones.cpu().numpy(), lv,
+                     cb.last_dones.cpu().numpy(), 0.99, 0.95)
+    assert np.array_equal(bb.advantages.cpu().numpy(), a_ref)
+    for v in (va, vb, vc):
+        v.close()
+
+
+# ---------------------------------------------------------------------------- noise injection lifetime
+_STATE = {"roll": 0.2, "pitch": 0.05, "yaw": 0.0, "omega_p": 0.0, "omega_q": 0.0, "omega_r": 0.0,
+          "position_n": 0.0, "position_e": 0.0, "position_d": -50.0, "velocity_u": 19.0, "velocity_v": 0.0,
+          "velocity_w": 0.5, "wind": [0.0, 0.0, 0.0],
+          "elevon_right": (0.0, 0.0), "elevon_left": (0.0, 0.0), "throttle": (0.5, 0.0)}
+
+
+def test_set_noise_after_set_env_noise_reads_the_shared_sequence():
+    """set_env_noise on a subset, then set_noise(shared): every env flies on the shared sequence (the
+    handle drops the per-env lengths with the old buffer), equal to an engine that only saw set_noise."""
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
+    spec = C.build_sim(config_kw={"turbulence": True, "turbulence_sim_length": 300, "turbulence_intensity": "severe"})
+    n = 64
+    z = np.random.RandomState(5).standard_normal((4, 300))
+    zj = np.random.RandomState(6).standard_normal((4, 40))
+    a, b = (Engine(spec, None, n, device=DEV, precision="float64") for _ in range(2))
+    a.set_env_noise([3, 17], zj)
+    a.set_noise(z)
+    b.set_noise(z)
+    for e in (a, b):
+        e.seed(1)
+        e.reset(want_obs=False)
+    rng = np.random.RandomState(0)
+    for _ in range(60):
+        cmd = torch.tensor(rng.uniform(-0.2, 0.2, (n, 3)) + [0.0, 0.0, 0.6], device=DEV)
+        a.sim_step(cmd)
+        b.sim_step(cmd)
+    assert torch.equal(a.get_block(C.FW_BLK_ODE), b.get_block(C.FW_BLK_ODE))
+    a.close()
+    b.close()
+
+
+def test_set_env_noise_keeps_a_set_noise_injection():
+    """A per-env injection on top of a set_noise buffer: the other envs keep reading the set_noise sequence."""
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
+    spec = C.build_sim(config_kw={"turbulence": True, "turbulence_sim_length": 300, "turbulence_intensity": "severe"})
+    n = 64
+    z = np.random.RandomState(5).standard_normal((4, 300))
+    zj = np.random.RandomState(6).standard_normal((4, 40))
+    a, b = (Engine(spec, None, n, device=DEV, precision="float64") for _ in range(2))
+    for e in (a, b):
+        e.set_noise(z)
+    a.set_env_noise([3], zj)
+    for e in (a, b):
+        e.seed(1)
+        e.reset(want_obs=False)
+    rng = np.random.RandomState(0)
+    for _ in range(60):
+        cmd = torch.tensor(rng.uniform(-0.2, 0.2, (n, 3)) + [0.0, 0.0, 0.6], device=DEV)
+        a.sim_step(cmd)
+        b.sim_step(cmd)
+    ya, yb = a.get_block(C.FW_BLK_ODE), b.get_block(C.FW_BLK_ODE)
+    others = torch.arange(n, device=DEV) != 3
+    assert torch.equal(ya[:, others], yb[:, others]) and not torch.equal(ya[:, 3], yb[:, 3])
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("record", [False, True])
+def test_reset_ends_per_env_injection(record):
+    """After env_method("reset", indices=[j], turbulence_noise=Z): a full VecEnv reset (record=False) or the
+    recording step's auto-reset (record=True) ends the injection -- env j's next episode equals the one of a
+    run that never injected, as the reference's worker resets with Dryden.reset(None)."""
+    from tum_adlr_deep_reinforcement_learning_amd.vec_env import FixedWingVecEnv
+    n, j, steps_max = 8, 5, 120  # (turbulence chunk = steps_max; shorter chunks need the stateful filter)
+    z = np.random.RandomState(2).standard_normal((4, 50))
+    runs = []
+    for inject in (True, False):
+        env = FixedWingVecEnv(n, config_kw={"steps_max": steps_max},
+                              sim_config_kw={"turbulence": True, "turbulence_intensity": "moderate"},
+                              device=DEV, precision="float64", seed=3, return_tensors=True, info_target=False,
+                              record_history=record)
+        env.reset()
+        env.env_method("reset", state=_STATE, indices=[j], **({"turbulence_noise": z} if inject else {}))
+        rng = np.random.RandomState(9)
+        obs = []
+        if record:  # run env j's episode out: the recording step resets it (eng.reset(mask=done))
+            for _ in range(steps_max):
+                env.step(torch.tensor(rng.uniform(-1, 1, (n, 3)), device=DEV))
+        else:
+            env.reset()
+        for _ in range(30):
+            o, _, _, _ = env.step(torch.tensor(rng.uniform(-1, 1, (n, 3)), device=DEV))
+            obs.append(o.cpu().numpy().copy())
+        runs.append(np.array(obs))
+        env.close()
+    assert np.array_equal(runs[0][:, j], runs[1][:, j])

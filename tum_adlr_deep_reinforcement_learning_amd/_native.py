@@ -18,11 +18,11 @@ LIB_PATH = os.path.join(LIB_DIR, "libfwsim.so")
 HEADER = os.path.join(ROOT, "include", "fwsim.h")
 HEADERS = [HEADER, os.path.join(ROOT, "include", "fwrollout.h")]
 UNITS = [os.path.join(CSRC, "fw_kernels.hip"), os.path.join(CSRC, "fw_rollout.hip")]
-SOURCES = UNITS + [os.path.join(CSRC, "fw_device.hpp"), os.path.join(CSRC, "fw_quad.hpp"), os.path.join(CSRC, "fw_x8_consts.inc")] + HEADERS
+SOURCES = UNITS + [os.path.join(CSRC, "fw_device.hpp"), os.path.join(CSRC, "fw_quad.hpp"), os.path.join(CSRC, "fw_stats.hpp"), os.path.join(CSRC, "fw_x8_consts.inc")] + HEADERS
 ARCH = os.environ.get("FWSIM_ARCH", "gfx950")
 
 _lib = None
-ABI_VERSION = 8  # include/fwsim.h FWSIM_ABI_VERSION
+ABI_VERSION = 9  # include/fwsim.h FWSIM_ABI_VERSION
 
 
 class FwError(RuntimeError):
@@ -170,7 +170,8 @@ class FwMlpPolicy(ctypes.Structure):  # include/fwrollout.h fw_mlp_policy
 
 
 class FwCollectEpilogue(ctypes.Structure):  # include/fwsim.h fw_collect_epilogue
-    _fields_ = [("ret", _vp), ("gamma", _c.c_double), ("records", _vp), ("row_ctrl", _vp)]
+    _fields_ = [("ret", _vp), ("gamma", _c.c_double), ("records", _vp), ("row_ctrl", _vp), ("merged", _vp),
+                ("rms", _vp)]
 
 
 class FwCollectIO(ctypes.Structure):  # include/fwrollout.h fw_collect_io

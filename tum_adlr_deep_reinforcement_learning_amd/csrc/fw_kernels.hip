@@ -24,6 +24,7 @@
 #include <string>
 
 #include "fw_device.hpp"
+#include "fw_stats.hpp"
 
 // Parallel build (_native.py): this file is compiled as several translation units.  FW_PART = 0 holds
 // the host code, the C ABI and the small kernels; FW_PART = 1..6 each instantiate one launch helper
@@ -117,6 +118,10 @@ struct State {
   double col_gamma;
   double* col_rec;    // [blocks][1 + 2 D] per-block moment records, or null
   int32_t* col_ctrl;  // rollout row counter advanced by the launch, or null
+  double* col_merged; // [1 + 2 D] the launch's merged record (in-launch merge tree), or null: merged later
+  double* col_rms;    // RunningMeanStd buffer update_from_moments is applied to (with col_merged), or null
+  double* col_lvl;    // merge-tree records above level 0 (handle workspace, fw_stats::merge_tree_size)
+  uint32_t* col_cnt;  // merge-tree arrival counters (handle workspace, zero between launches)
 };
 
 // streaming episode-metric state (fixed_wing.py:1644-1736 restated over running sums):
@@ -1124,18 +1129,176 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   FW_TSTAMP(4);
 }
 
+// ---- in-launch merge of the block records (fw_collect_epilogue.merged) ---------------------------------
+// Words handed to another block of the same launch go through agent-scope atomic read-modify-writes on
+// both sides (the producer's exchanges are performed before its ticket is drawn, the consumer's loads are
+// issued after its ticket returned): every such access is performed at the device's coherence point, so
+// neither the producer's L2 nor the consumer's L1 / L2 can hold a stale copy, and no cache write-back or
+// invalidate (release / acquire fence, several us each at four blocks per CU) is needed.  A publisher
+// folds the returned old values into one register that the ticket's wait consumes: the exchanges stay in
+// flight together (consumed one by one, each would wait out its own round trip).
+__device__ __forceinline__ void pub64(double* p, double v, unsigned long long& acc) {
+  acc ^= __hip_atomic_exchange((unsigned long long*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double get64(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_fetch_add((unsigned long long*)p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+constexpr int COL_MAXD = FW_MAX_OBS + 1;
+constexpr int MN_COLS = 16;  // columns staged per LDS pass of merge_node
+constexpr int MN_LD = 66;    // staging row stride (doubles): lane j reads row j with 16-B loads, 4 banks apart
+// LDS staging of merge_node: MN_COLS + 1 rows x 64 records, the column means, update_from_moments' counts
+constexpr size_t MN_BYTES = ((MN_COLS + 1) * MN_LD + COL_MAXD + 2) * sizeof(double);
+
+// sum of row[0 .. 64) in index order (row 16-B aligned): all loads issued first.  The slots of absent
+// records hold +0.0, and adding +0.0 leaves any partial sum that can occur here unchanged (it starts at
+// +0.0, so it is never -0.0): the same bits as summing only the present records, without 64 masks.
+__device__ __forceinline__ double row_sum(const double* row) {
+#pragma clang fp contract(off)
+  double v[64];
+#pragma unroll
+  for (int k = 0; k < 32; k++) {
+    const double2 t = reinterpret_cast<const double2*>(row)[k];
+    v[2 * k] = t.x;
+    v[2 * k + 1] = t.y;
+  }
+  double a = 0.0;
+#pragma unroll
+  for (int k = 0; k < 64; k++) a += v[k];
+  return a;
+}
+
+// One wave merges cnt <= 64 records (field f of record k at src[f * stride + k], published with pub64)
+// exactly as fw_moments_merge does, two-pass, every sum in record order: N = sum n_k,
+// mean_j = (sum n_k mean_kj) / N, M2_j = sum (M2_kj + n_k (mean_kj - mean_j)^2).  Lane k loads record k
+// (coalesced per field), MN_COLS columns at a time; the column sums go through LDS (lane j sums column
+// j).  Returns N on every lane, mean_j / M2_j on lane j < D.
+__device__ __forceinline__ void merge_node(const double* src, int64_t stride, int cnt, int D, double* st,
+                                           double& N, double& mean, double& m2) {
+#pragma clang fp contract(off)
+  const int l = (int)(threadIdx.x & 63);
+  const bool act = l < cnt;
+  // the record addresses are formed in VGPRs from a per-lane base and an opaque stride: as wave-uniform
+  // values the field addresses went to SGPRs (and spilled)
+  const double* pl = src + l;
+  int64_t sd = stride;
+  asm volatile("" : "+v"(pl), "+v"(sd));
+  const double nl = act ? get64(pl) : 0.0;
+  N = 0.0;
+  mean = 0.0;
+  m2 = 0.0;
+  for (int cb = 0; cb < D; cb += MN_COLS) {
+    double m[MN_COLS], q[MN_COLS];
+#pragma unroll
+    for (int jj = 0; jj < MN_COLS; jj++) {  // (in flight together with nl's load)
+      const bool v = act && cb + jj < D;
+      m[jj] = v ? get64(pl + (int64_t)(1 + cb + jj) * sd) : 0.0;
+      q[jj] = v ? get64(pl + (int64_t)(1 + D + cb + jj) * sd) : 0.0;
+    }
+    if (cb == 0) {
+      st[MN_COLS * MN_LD + l] = nl;
+      __syncthreads();
+      N = row_sum(st + MN_COLS * MN_LD);  // (a broadcast read)
+    }
+    const bool mine = l >= cb && l < cb + MN_COLS && l < D;  // lane l owns column l
+#pragma unroll
+    for (int jj = 0; jj < MN_COLS; jj++) st[jj * MN_LD + l] = nl * m[jj];  // pass 1
+    __syncthreads();
+    double mu = 0.0;
+    if (mine) mu = row_sum(st + (l - cb) * MN_LD) / N;
+    __syncthreads();
+    if (l >= cb && l < cb + MN_COLS) st[(MN_COLS + 1) * MN_LD + (l - cb)] = mu;  // this block's means
+    if (mine) mean = mu;
+    __syncthreads();
+#pragma unroll
+    for (int jj = 0; jj < MN_COLS; jj++) {  // pass 2
+      const double dm = m[jj] - st[(MN_COLS + 1) * MN_LD + jj];
+      st[jj * MN_LD + l] = q[jj] + nl * (dm * dm);
+    }
+    __syncthreads();
+    if (mine) m2 = row_sum(st + (l - cb) * MN_LD);
+    __syncthreads();
+  }
+}
+
+// After this block published its record (level 0, column-major at col_rec with stride gridDim.x): draw a
+// ticket on the block's node; the last block to arrive at a node merges the node's records in order and
+// publishes the node's record one level up (fw_stats::merge_tree_size), until the final node, whose last
+// arriver writes col_merged and -- with col_rms -- applies RunningMeanStd.update_from_moments
+// (running_mean_std.py:26-40) through the same function fw_rms_update runs.  The node a block merges and
+// the order inside it are fixed by block index, so the bits do not depend on the order blocks finish in;
+// each node's counter is reset by its last arriver, for the next launch.  The merged record equals the one
+// merge over all block records (fw_moments_merge) to rounding, not bit for bit (another summation tree).
+__device__ __forceinline__ void collect_merge(const double* rec0, double* lvl, uint32_t* cnt, double* merged, double* rms,
+                                           int D, int d, bool has_ret, double* st, unsigned long long pacc) {
+  const int l = (int)(threadIdx.x & 63);
+  int64_t nodes = gridDim.x, idx = blockIdx.x, stride = gridDim.x;
+  const double* src = rec0;
+  while (true) {
+    const bool fin = nodes <= fw_stats::MERGE_FANIN;
+    const int64_t g = fin ? 0 : idx / fw_stats::MERGE_FANIN;
+    const int gs = fin ? (int)nodes : (int)std::min<int64_t>(fw_stats::MERGE_FANIN, nodes - g * fw_stats::MERGE_FANIN);
+    asm volatile("s_waitcnt vmcnt(0)" ::"v"(pacc) : "memory");  // this block's published words are performed
+    uint32_t t = 0;
+    if (l == 0) t = __hip_atomic_fetch_add(cnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = __shfl(t, 0);
+    if (t != (uint32_t)(gs - 1)) return;  // not the last arrival: the node's last block merges it
+    if (l == 0) __hip_atomic_store(cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+    double N, mean, m2;
+    double warm = 0.0;  // the statistics' lines, fetched under the merge (update_from_moments re-reads them)
+    if (fin && rms && l < 2 * d + 4) warm = rms[l];
+    merge_node(src + g * fw_stats::MERGE_FANIN, stride, gs, D, st, N, mean, m2);
+    asm volatile("" ::"v"(warm));
+    if (fin) {
+      double* out = merged;
+      if (l < D) {
+        out[1 + l] = mean;
+        out[1 + D + l] = m2;
+      }
+      if (l == 0) out[0] = N;
+      if (rms) {
+        __syncthreads();  // (merge_node's last reads of st are done)
+        if (l < D) {
+          st[1 + l] = mean;
+          st[1 + D + l] = m2;
+        }
+        if (l == 0) st[0] = N;
+        __syncthreads();
+        fw_stats::rms_update(st, 1, d, has_ret ? 1 : 0, rms, 1, 1, st + (MN_COLS + 1) * MN_LD + COL_MAXD);
+      }
+      return;
+    }
+    const int64_t up = fw_stats::merge_ceil(nodes, fw_stats::MERGE_FANIN);
+    pacc = 0;
+    if (l < D) {
+      pub64(lvl + (1 + l) * up + g, mean, pacc);
+      pub64(lvl + (1 + D + l) * up + g, m2, pacc);
+    }
+    if (l == 0) pub64(lvl + g, N, pacc);
+    src = lvl;
+    stride = up;
+    lvl += up * (1 + 2 * COL_MAXD);
+    cnt += up;
+    nodes = up;
+    idx = g;
+  }
+}
+
 // The env-side half of VecNormalize.step_wait (vec_normalize.py:106-131) after the env step, while the
 // block's observations are still in cache (fw_set_collect_epilogue): per env ret = ret * gamma + reward
 // (vec_normalize.py:126-129, multiply and add kept separate as numpy does) then ret[done] = 0 (:130), and
 // per block one exact two-pass moment record (n_b, mean_b, M2_b) of the float32 observation columns and of
 // ret before its reset -- the batch moments of RunningMeanStd.update (running_mean_std.py:20-24), merged
-// over the blocks by fw_moments_merge / fw_vecnorm_merge_update.  Row lanes: one per aircraft (lane 0 of
-// each quad when Q = 4).  Four lanes per column, each summing 16 rows in order, then a quad butterfly:
-// every sum in a fixed order, so the records are deterministic.  Every lane of the block calls this.
-constexpr int COL_MAXD = FW_MAX_OBS + 1;
+// over the blocks by the in-launch tree above (col_merged) or later by fw_moments_merge /
+// fw_vecnorm_merge_update.  Row lanes: one per aircraft (lane 0 of each quad when Q = 4).  Four lanes per
+// column, each summing 16 rows in order, then a quad butterfly: every sum in a fixed order, so the records
+// are deterministic.  Every lane of the block calls this.
 template <typename T>
 __device__ __forceinline__ void collect_epilogue(const State<T>& s, int64_t i, bool row, int ow, const T* obs_out,
-                                                 const T* rew_out, const uint8_t* done_out, float* sx, double* sr) {
+                                                 const T* rew_out, const uint8_t* done_out, float* sx, double* sr,
+                                                 double* mst) {
   const int lane = (int)(threadIdx.x & 63);
   const bool has_ret = s.col_ret != nullptr;
   double ret = 0.0;
@@ -1147,12 +1310,14 @@ __device__ __forceinline__ void collect_epilogue(const State<T>& s, int64_t i, b
   }
   if (s.col_rec) {
     const int D = ow + (has_ret ? 1 : 0);
+    const bool tree = s.col_merged != nullptr;
     if (row) {
       for (int j = 0; j < ow; j++) sx[lane * COL_MAXD + j] = (float)obs_out[i * ow + j];
       sr[lane] = ret;
     }
     const unsigned long long rm = __ballot(row);
     const double nb = (double)__popcll(rm);
+    unsigned long long pacc = 0;  // returned words of this block's publications (pub64)
     __syncthreads();
     double* rec = s.col_rec + blockIdx.x;  // column-major: field q at rec[q * blocks] (coalesced merge reads)
     const int64_t qs = gridDim.x;
@@ -1182,11 +1347,25 @@ __device__ __forceinline__ void collect_epilogue(const State<T>& s, int64_t i, b
       q += __shfl_xor(q, 1);
       q += __shfl_xor(q, 2);
       if (cv && p == 0) {
-        rec[(1 + col) * qs] = mean;
-        rec[(1 + D + col) * qs] = q;
+        if (tree) {
+          pub64(rec + (1 + col) * qs, mean, pacc);
+          pub64(rec + (1 + D + col) * qs, q, pacc);
+        } else {
+          rec[(1 + col) * qs] = mean;
+          rec[(1 + D + col) * qs] = q;
+        }
       }
     }
-    if (lane == 0) rec[0] = nb;
+    if (lane == 0) {
+      if (tree)
+        pub64(rec, nb, pacc);
+      else
+        rec[0] = nb;
+    }
+    if (tree) {
+      __syncthreads();  // (the staging area is reused by the merge)
+      collect_merge(s.col_rec, s.col_lvl, s.col_cnt, s.col_merged, s.col_rms, D, ow, has_ret, mst, pacc);
+    }
   }
   if (s.col_ctrl && blockIdx.x == 0 && lane == 0) s.col_ctrl[0] += 1;  // the stream's next launch sees it
 }
@@ -1203,15 +1382,16 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_env_step(const DevCfg<T>
   const bool collect = s.col_rec || s.col_ret || s.col_ctrl;
   if (i >= s.n && !collect) return;
   const C& c = *reinterpret_cast<const C*>(cfgp);  // structural specialisation view (fw_device.hpp SpecCfg)
-  __shared__ V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];  // y, f (+ error sum) of the block's aircraft (pairs)
+  __shared__ __attribute__((aligned(16))) V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];  // y, f (+ error sum) of the block's aircraft (pairs)
   static_assert(Q != 1 || RP || FW_TAIL_QUAD == 0 || BLOCK == 64, "the tail handoff works per one-wave block");
   __shared__ qd::HoSlot<T> ho[Q == 1 && !RP ? BLOCK : 1];
   static_assert(BLOCK == 64, "collect_epilogue: one-wave blocks");
   // the epilogue's staging (64 rows x COL_MAXD floats + 64 doubles) reuses the integrator's LDS slots once
   // the step is done (one-lane instances; LDS bounds how many fp64 blocks fit a CU); quads get their own
-  constexpr size_t COL_BYTES = 64 * COL_MAXD * sizeof(float) + 64 * sizeof(double);
+  constexpr size_t COL_STAGE = 64 * COL_MAXD * sizeof(float) + 64 * sizeof(double);
+  constexpr size_t COL_BYTES = COL_STAGE > MN_BYTES ? COL_STAGE : MN_BYTES;  // the merge tree reuses it
   constexpr bool COL_ALIAS = sizeof(lds) >= COL_BYTES;
-  __shared__ double col_sep[COL_ALIAS ? 1 : COL_BYTES / sizeof(double)];
+  __shared__ __attribute__((aligned(16))) double col_sep[COL_ALIAS ? 1 : COL_BYTES / sizeof(double)];
   char* const col_base = COL_ALIAS ? (char*)lds : (char*)col_sep;
   float* const col_x = (float*)col_base;
   double* const col_r = (double*)(col_base + 64 * COL_MAXD * sizeof(float));
@@ -1220,7 +1400,8 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_env_step(const DevCfg<T>
                                                     episode_out, stats, auto_reset, (int)(tid % Q), ho);
   if (collect) {
     if (COL_ALIAS) __syncthreads();  // (one wave: orders the slot reuse after the integrator's last accesses)
-    collect_epilogue<T>(s, i, i < s.n && tid % Q == 0, c.n_obs * c.obs_len, obs_out, rew_out, done_out, col_x, col_r);
+    collect_epilogue<T>(s, i, i < s.n && tid % Q == 0, c.n_obs * c.obs_len, obs_out, rew_out, done_out, col_x, col_r,
+                        (double*)col_base);
   }
 }
 
@@ -1332,6 +1513,7 @@ struct fw_handle {
   int lanes_opt = FW_LANES_AUTO;  // fw_set_lanes: 0 = automatic, 1, 4
   int quad_ok = 1;          // the config allows the quad integrator (no wrapped ODE-state variable)
   fw_collect_epilogue col{};  // fw_set_collect_epilogue (all null: off)
+  size_t o_colws = 0, o_colcnt = 0;  // in-launch merge tree workspace (records above level 0, counters)
 };
 
 namespace {
@@ -1690,6 +1872,10 @@ State<T> state_of(const fw_handle* h) {
   s.col_gamma = h->col.gamma;
   s.col_rec = h->col.records;
   s.col_ctrl = h->col.row_ctrl;
+  s.col_merged = h->col.merged;
+  s.col_rms = h->col.rms;
+  s.col_lvl = h->o_colws ? (double*)(b + h->o_colws) : nullptr;
+  s.col_cnt = h->o_colws ? (uint32_t*)(b + h->o_colcnt) : nullptr;
   return s;
 }
 
@@ -1829,6 +2015,12 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
     h->o_obs_init = off; off += (size_t)env->n_obs * row;
     h->o_obs_ring = off; off += (size_t)h->obs_hist * env->n_obs * row;
   }
+  if (env) {  // the collect epilogue's in-launch merge tree (fw_collect_epilogue.merged), sized for 4 lanes
+    int64_t mr = 0, mc = 0;
+    fw_stats::merge_tree_size((h->n * 4 + BLOCK - 1) / BLOCK, &mr, &mc);
+    h->o_colws = off; off += align_up((size_t)mr * (1 + 2 * COL_MAXD) * sizeof(double), 256);
+    h->o_colcnt = off; off += align_up((size_t)mc * sizeof(uint32_t), 256);  // zeroed below, reset by the tree
+  }
   // rows are ld elements apart: the padding above is folded into ld for simplicity
   h->base_bytes = off;
   e = hipMalloc(&h->base, off);
@@ -1890,7 +2082,7 @@ int fw_set_noise(fw_handle* h, const void* noise_dev, int64_t len) {
   if (len > INT32_MAX) return set_err(FW_E_INVALID, "noise length must be < 2^31");
   h->noise = noise_dev;
   h->noise_len = noise_dev ? len : 0;
-  if (!noise_dev) h->noise_env_len = nullptr;
+  h->noise_env_len = nullptr;  // lengths belong to a buffer: set them again with fw_set_noise_lengths
   return FW_OK;
 }
 
@@ -2036,6 +2228,9 @@ int fw_set_collect_epilogue(fw_handle* h, const fw_collect_epilogue* epi) {
     return set_err(FW_E_INVALID, "fw_set_collect_epilogue: handle has no env");
   if (h->has_env && h->env.n_obs * std::max(h->env.obs_length, 1) + 1 > FW_MAX_OBS + 1 && epi->records)
     return set_err(FW_E_UNSUPPORTED, "fw_set_collect_epilogue: more than FW_MAX_OBS observation values per env");
+  if (epi->merged && !epi->records)
+    return set_err(FW_E_INVALID, "fw_set_collect_epilogue: merged needs the records buffer (the tree's level 0)");
+  if (epi->rms && !epi->merged) return set_err(FW_E_INVALID, "fw_set_collect_epilogue: rms needs merged");
   h->col = *epi;
   return FW_OK;
 }

@@ -26,6 +26,7 @@
 
 #include "../../include/fwrollout.h"
 #include "../../include/fwsim.h"
+#include "fw_stats.hpp"
 
 #pragma clang fp contract(off)
 
@@ -119,21 +120,9 @@ __global__ __launch_bounds__(BLOCK) void k_gae(const float* __restrict__ rew, co
 // ---------------------------------------------------------------------------
 // batch moments
 // ---------------------------------------------------------------------------
-struct Mom {
-  double n, mean, m2;
-};
-
-__device__ __forceinline__ Mom chan(Mom a, Mom b) {  // parallel-variance merge, a then b
-  if (b.n == 0.0) return a;
-  if (a.n == 0.0) return b;
-  const double n = a.n + b.n;
-  const double delta = b.mean - a.mean;
-  Mom r;
-  r.n = n;
-  r.mean = a.mean + delta * (b.n / n);
-  r.m2 = a.m2 + b.m2 + delta * delta * (a.n * b.n / n);
-  return r;
-}
+using fw_stats::Mom;  // (fw_stats.hpp: shared with k_env_step's in-launch merge)
+using fw_stats::chan;
+using fw_stats::rms_update;
 
 // Batch moments in two kernels, both exact two-pass (numpy's np.mean then np.var of the deviations):
 //   k_moments_partial  one block per MROWS rows: the rows staged column-major in LDS, the block's mean
@@ -393,48 +382,6 @@ __global__ __launch_bounds__(MERGE16_THREADS) void k_moments_merge16(const doubl
 __global__ __launch_bounds__(MERGE_THREADS) void k_moments_merge(const double* __restrict__ part, int parts, int D,
                                                                     double* __restrict__ out) {
   merge_records(part, parts, D, out);
-}
-
-// RunningMeanStd.update_from_moments, one thread per column; parts merged in rank order.  Every thread of
-// the block calls it (old_count is read by thread 0 and shared through LDS behind a barrier).
-__device__ __forceinline__ void rms_update(const double* __restrict__ parts, int n_parts, int d, int has_ret,
-                                           double* __restrict__ rms, int update_obs, int update_ret,
-                                           double* old_count) {
-  const int D = d + (has_ret ? 1 : 0);
-  const int S = 1 + 2 * D;
-  const int j = threadIdx.x;
-  if (j == 0) {
-    old_count[0] = rms[2 * d];
-    old_count[1] = rms[2 * d + 3];
-  }
-  __syncthreads();
-  if (j < D) {
-    const bool is_ret = j == d;
-    if ((is_ret && update_ret) || (!is_ret && update_obs)) {
-      Mom m{0.0, 0.0, 0.0};
-      for (int k = 0; k < n_parts; k++) m = chan(m, Mom{parts[k * S], parts[k * S + 1 + j], parts[k * S + 1 + D + j]});
-      const double bmean = m.mean, bvar = m.m2 / m.n, bc = m.n;
-      double* mean_p = is_ret ? rms + 2 * d + 1 : rms + j;
-      double* var_p = is_ret ? rms + 2 * d + 2 : rms + d + j;
-      const double count = old_count[is_ret ? 1 : 0];
-      const double mean = *mean_p, var = *var_p;
-      // running_mean_std.py:26-40, same operation order
-      const double delta = bmean - mean;
-      const double tot = count + bc;
-      const double new_mean = mean + delta * bc / tot;
-      const double m_a = var * count;
-      const double m_b = bvar * bc;
-      const double m_2 = m_a + m_b + delta * delta * count * bc / (count + bc);
-      *mean_p = new_mean;
-      *var_p = m_2 / (count + bc);
-      if (j == (is_ret ? d : 0)) {
-        if (is_ret)
-          rms[2 * d + 3] = bc + count;
-        else
-          rms[2 * d] = bc + count;
-      }
-    }
-  }
 }
 
 __global__ void k_rms_update(const double* __restrict__ parts, int n_parts, int d, int has_ret, double* __restrict__ rms,

@@ -111,13 +111,28 @@ class Engine:
                       "fw_update_config")
         self.config_version += 1
 
+    def _push_noise(self):
+        """Hand the current noise buffer (and per-env lengths) to the handle.  A captured step bakes in the
+        buffer's address and length (not the per-env lengths, which the kernel reads from device memory), so
+        config_version moves only when those change."""
+        buf, lens = self._noise, getattr(self, "_env_len", None)
+        key = (buf.data_ptr() if buf is not None else None, int(buf.shape[1]) if buf is not None else 0,
+               lens.data_ptr() if lens is not None else None)
+        _native.check(self.lib.fw_set_noise(self.h, _ptr(buf), key[1]), "fw_set_noise")  # (clears the lengths)
+        if lens is not None:
+            _native.check(self.lib.fw_set_noise_lengths(self.h, _ptr(lens)), "fw_set_noise_lengths")
+        if key != getattr(self, "_noise_key", (None, 0, None)):
+            self._noise_key = key
+            self.config_version += 1
+
     def set_noise(self, noise):
         """Inject N(0,1) turbulence noise for every env, array-like [n][4][len] or [4][len] (shared), or None.
-        Step k of an episode reads sample k mod len (dryden.py:209-236)."""
+        Step k of an episode reads sample k mod len (dryden.py:209-236).  Replaces any per-env injection
+        (set_env_noise)."""
         self._env_len = None
         if noise is None:
             self._noise = None
-            _native.check(self.lib.fw_set_noise(self.h, None, 0), "fw_set_noise")
+            self._push_noise()
             return
         a = torch.as_tensor(np.asarray(noise), dtype=self.dtype)
         if a.dim() == 2:
@@ -129,19 +144,25 @@ class Engine:
         buf = torch.zeros(4, L, ld, dtype=self.dtype, device=self.device)
         buf[:, :, :self.n] = a.permute(1, 2, 0).to(self.device)
         self._noise = buf
-        _native.check(self.lib.fw_set_noise(self.h, _ptr(buf), L), "fw_set_noise")
+        self._push_noise()
 
     def set_env_noise(self, indices, noise):
         """Per-env injection (PyFly.reset(turbulence_noise=...) of the envs in ``indices``, pyfly.py:1262):
         ``noise`` [4][len] N(0,1) samples for all of them, or None = those envs draw from Philox again.
-        The other envs keep what they had; an env's injection ends at its next VecEnv auto-reset
-        (fw_set_noise_lengths).  Applies to the envs' next reset (call before ``reset(mask=...)``)."""
+        The other envs keep what they had (a set_noise injection included); an env's injection ends at its
+        next VecEnv auto-reset (fw_set_noise_lengths) or at a reset of it without noise (FixedWingVecEnv).
+        Applies to the envs' next reset (call before ``reset(mask=...)``)."""
         idx = torch.as_tensor(np.asarray(list(indices), dtype=np.int64))
         if getattr(self, "_env_len", None) is None:
             if noise is None:
                 return
-            self._env_len = torch.zeros(self.n, dtype=torch.int32, device=self.device)
-            self._noise = torch.zeros(4, 1, (self.n + 63) // 64 * 64, dtype=self.dtype, device=self.device)
+            ld = (self.n + 63) // 64 * 64
+            if self._noise is not None:  # a set_noise buffer: every env keeps reading it until its own injection
+                self._env_len = torch.full((self.n,), int(self._noise.shape[1]), dtype=torch.int32, device=self.device)
+                self._noise = self._noise.clone()
+            else:
+                self._env_len = torch.zeros(self.n, dtype=torch.int32, device=self.device)
+                self._noise = torch.zeros(4, 1, ld, dtype=self.dtype, device=self.device)
         if noise is None:
             self._env_len[idx.to(self.device)] = 0
         else:
@@ -157,9 +178,7 @@ class Engine:
             self._noise[:, :L, cols] = a.to(self.device)[:, :, None]
             self._env_len[cols] = L
         torch.cuda.current_stream(self.device).synchronize()  # host -> device copies of the pageable input
-        _native.check(self.lib.fw_set_noise(self.h, _ptr(self._noise), self._noise.shape[1]), "fw_set_noise")
-        _native.check(self.lib.fw_set_noise_lengths(self.h, _ptr(self._env_len)), "fw_set_noise_lengths")
-        self.config_version += 1
+        self._push_noise()
 
     # ------------------------------------------------------------------
     def reset(self, mask=None, init=None, target=None, want_obs=True):
@@ -233,30 +252,36 @@ class Engine:
         _native.check(self.lib.fw_observe(self.h, _ptr(self.obs), self.stream()), "fw_observe")
         return self.obs
 
-    def set_collect_epilogue(self, ret=None, gamma=0.0, records=None, row_ctrl=None):
+    def set_collect_epilogue(self, ret=None, gamma=0.0, records=None, row_ctrl=None, merged=None, rms=None):
         """fw_set_collect_epilogue: every following ``env_step`` also updates VecNormalize's discounted return
         ``ret`` (fp64 [n]: ret*gamma + reward, then 0 where done) and writes one moment record per launch block
         of (observation, ret) into ``records`` (fp64, ``collect_records()[1]`` x (1 + 2 D) rows); ``row_ctrl``
-        (int32 device tensor) gets ``[0] += 1`` per launch.  All None turns it off.  A captured step keeps the
+        (int32 device tensor) gets ``[0] += 1`` per launch.  ``merged`` (fp64 [1 + 2 D]): the launch merges its
+        block records itself (in-launch tree) into that record; ``rms`` (the fw_rms_update buffer, with
+        ``merged``): it also applies update_from_moments.  All None turns it off.  A captured step keeps the
         setting it was captured with."""
         if ret is None and records is None and row_ctrl is None:
             _native.check(self.lib.fw_set_collect_epilogue(self.h, None), "fw_set_collect_epilogue")
             self._collect = None
             return
-        for t, dt in ((ret, torch.float64), (records, torch.float64), (row_ctrl, torch.int32)):
+        for t, dt in ((ret, torch.float64), (records, torch.float64), (row_ctrl, torch.int32),
+                      (merged, torch.float64), (rms, torch.float64)):
             if t is not None and (t.dtype != dt or t.device != self.device or not t.is_contiguous()):
-                raise ValueError("set_collect_epilogue: ret / records fp64, row_ctrl int32, contiguous on the device")
+                raise ValueError("set_collect_epilogue: ret / records / merged / rms fp64, row_ctrl int32, "
+                                 "contiguous on the device")
         if ret is not None and ret.numel() != self.n:
             raise ValueError("set_collect_epilogue: ret must hold one value per env")
-        if records is not None:
-            D = self.n_obs_values + (1 if ret is not None else 0)
-            if records.numel() < self.collect_records()[1] * (1 + 2 * D):
-                raise ValueError("set_collect_epilogue: records buffer too small")
-        e = _native.FwCollectEpilogue(ret.data_ptr() if ret is not None else None, float(gamma),
-                                      records.data_ptr() if records is not None else None,
-                                      row_ctrl.data_ptr() if row_ctrl is not None else None)
+        D = self.n_obs_values + (1 if ret is not None else 0)
+        if records is not None and records.numel() < self.collect_records()[1] * (1 + 2 * D):
+            raise ValueError("set_collect_epilogue: records buffer too small")
+        if merged is not None and merged.numel() < 1 + 2 * D:
+            raise ValueError("set_collect_epilogue: merged must hold 1 + 2 D values")
+        if rms is not None and rms.numel() < 2 * self.n_obs_values + 4:
+            raise ValueError("set_collect_epilogue: rms must hold 2 d + 4 values")
+        ptr = (lambda t: t.data_ptr() if t is not None else None)
+        e = _native.FwCollectEpilogue(ptr(ret), float(gamma), ptr(records), ptr(row_ctrl), ptr(merged), ptr(rms))
         _native.check(self.lib.fw_set_collect_epilogue(self.h, ctypes.byref(e)), "fw_set_collect_epilogue")
-        self._collect = (ret, records, row_ctrl)  # keep the buffers alive while the handle writes them
+        self._collect = (ret, records, row_ctrl, merged, rms)  # keep the buffers alive while the handle writes them
 
     def collect_records(self):
         """(records the next env_step writes, the most any lanes setting writes)."""

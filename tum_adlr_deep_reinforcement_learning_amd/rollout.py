@@ -565,7 +565,7 @@ class RolloutCollector:
             eng.env_step(self.s_clip, auto_reset=True, stats=True)
 
         def stats_local():
-            if vn is None:
+            if vn is None or vn.merge_in_launch:  # the env step's launch merged (and, unsharded, updated)
                 return
             if grouped:
                 vn.merge_records(vn._rec)

@@ -214,6 +214,9 @@ class FixedWingVecEnv(VecEnv):
         return [s + i for i in range(self.num_envs)]
 
     def reset(self):
+        # every SubprocVecEnv worker resets without turbulence_noise (Dryden.reset(None) draws fresh noise,
+        # dryden.py:174-188): a per-env injection ends here
+        self.engine.set_env_noise(range(self.num_envs), None)
         obs = self.engine.reset()
         self._reset_pending = False
         if self._hists is not None:
@@ -245,6 +248,7 @@ class FixedWingVecEnv(VecEnv):
         for i, h in enumerate(self._hists):
             h.step(a[i], step_succeeded(tm[i]), to[i] if dn[i] else o[i], r[i], self._tgt[:, i], t[:, i], v[:, i])
         if dn.any():
+            eng.set_env_noise(np.nonzero(dn)[0], None)  # as the auto-reset of fw_env_step: the injection ends
             obs = eng.reset(mask=dn)
             o = self._shaped(obs.cpu().numpy().astype(np.float32))
             t, v = self._targets_vals()

@@ -223,7 +223,7 @@ class VecNormalize:
         if self.training:
             if not epi:
                 self._moments(obs, rews)
-            elif self.exchanged():  # this shard's record, for the exchange
+            elif self.exchanged() and not self.merge_in_launch:  # this shard's record, for the exchange
                 self.merge_records(self._rec)
 
     def step_exchange(self):
@@ -233,7 +233,8 @@ class VecNormalize:
     def step_wait_finish(self):
         if self.training:
             if self._epi_last and not self.exchanged():
-                self.merge_update()
+                if not self.merge_in_launch:
+                    self.merge_update()
             else:
                 self._merge()
         self._apply(self.old_obs, self.old_reward, self._done_u8)
@@ -253,11 +254,21 @@ class VecNormalize:
         """The env step writes this wrapper's moment records and return update (training on the engine)."""
         return self._epi_ok and self.training
 
+    # the env step's own launch merges its block records (and, unsharded, updates the statistics): a
+    # collect step is then two launches (fwsim.h fw_collect_epilogue.merged / .rms); False = the merge (+
+    # update) as a separate launch after the env step (fw_vecnorm_merge_update / fw_moments_merge)
+    merge_in_launch = True
+
     def set_epilogue(self, row_ctrl=None):
         """Point the engine's collect epilogue at this wrapper's return and record buffers (and, for a
-        captured collect step, the rollout row counter)."""
+        captured collect step, the rollout row counter).  With ``merge_in_launch`` the launch also writes the
+        merged record into ``_rec`` and, without an exchange, applies it to ``rms``."""
         eng = self.venv.engine
-        eng.set_collect_epilogue(ret=self.ret, gamma=self.gamma, records=self._records, row_ctrl=row_ctrl)
+        self._ensure_parts()
+        merged = self._rec if self.merge_in_launch else None
+        rms = self.rms if (self.merge_in_launch and not self.exchanged()) else None
+        eng.set_collect_epilogue(ret=self.ret, gamma=self.gamma, records=self._records, row_ctrl=row_ctrl,
+                                 merged=merged, rms=rms)
         self._n_rec = eng.collect_records()[0]
 
     def merge_records(self, out):
@@ -277,7 +288,7 @@ class VecNormalize:
         """Host-side choices a captured step bakes in (RolloutCollector recaptures when this changes)."""
         inner = self.venv.graph_key() if hasattr(self.venv, "graph_key") else None
         return (self.training, self.norm_obs, self.norm_reward, self.clip_obs, self.clip_reward, self.gamma,
-                self.epsilon, self._world(), self._epi_ok, inner)
+                self.epsilon, self._world(), self._epi_ok, self.merge_in_launch, inner)
 
     def step(self, actions):
         self.step_async(actions)
