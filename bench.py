@@ -53,31 +53,38 @@ def algorithmic_bytes_per_env_step(spec, esz=4):
     """HBM bytes one aircraft moves per env step in k_env_step (steady state, no reset).
 
     reads : ODE state 19, elevator/aileron 2, steady wind 3, targets 3, action 3,
-            previous actions ring (act_window*3), ep_return 1            -> T
-            steps word, episode word, goal history 4 words, life word    -> u32
-    writes: ODE state 19, derived 8, targets 3, ring slot 3, ep_return 1,
-            observation n_obs, reward 1                                  -> T
-            steps word, goal history 4 words, term code, life word       -> u32
-            done flag                                                    -> u8
+            the previous actions the step reads (act_need*3: window - 1), ep_return 1   -> T
+            steps word, goal history 4 words, life word (+ episode word with turbulence
+            or observation noise: the Philox key)                                       -> u32
+    writes: ODE state 19, derived 8, the targets that can change (compensate class; a
+            constant-class row is stored only when some lane changed it), ring slot 3,
+            last command 3, ep_return 1, observation n_obs, reward 1                    -> T
+            steps word, goal history 4 words, term code, life word                      -> u32
+            done flag                                                                   -> u8
     (life: the lifetime step counter the ring slots are indexed by, round 4.)  Not counted: the kernel's
     deliberate re-reads after the RK loop (pre-step state 19, targets 3, actions 3 -- held across the
     integration they would cost VGPRs), which PMC shows partly served from HBM (profiles/r04_traffic_split.json).
     """
-    act_window = 1
+    act_need = 0
     for o in spec.cfg["observation"]["states"]:
         if o["type"] == "action" and spec.scale_actions:
-            act_window = max(act_window, int(o.get("window_size", 1)))
+            act_need = max(act_need, int(o.get("window_size", 1)) - 1)
     for f in spec.cfg["reward"]["factors"]:
         if f["class"] == "action" and f["type"] == "delta":
-            act_window = max(act_window, int(f["window_size"]) - 1)
-    rd = (19 + 2 + 3 + 3 + 3 + act_window * 3 + 1) * esz + (1 + 1 + 4 + 1) * 4
-    wr = (19 + 8 + 3 + 3 + 3 + 1 + spec.n_obs + 1) * esz + (1 + 4 + 1 + 1) * 4 + 1  # incl. last command
+            act_need = max(act_need, int(f["window_size"]) - 1)
+    tgt_var = sum(1 for t in spec.cfg["target"]["states"] if t.get("class", "constant") != "constant")
+    philox = bool(spec.sim.cfg.get("turbulence")) or bool(spec.obs_noise)
+    rd = (19 + 2 + 3 + 3 + 3 + act_need * 3 + 1) * esz + (1 + 4 + 1 + (1 if philox else 0)) * 4
+    wr = (19 + 8 + tgt_var + 3 + 3 + 1 + spec.n_obs + 1) * esz + (1 + 4 + 1 + 1) * 4 + 1
     if spec.cfg.get("metrics") and spec.metrics_enabled:
-        # streaming episode metrics (csrc/fw_kernels.hip metrics_step): previous command, control
-        # variation, e0/sum/|sum|/min/max x3, previous ring error x3 (T); count, 3 goal registers x4,
-        # goal counts x4, settling x4, rise crossings x6 (u32)
-        rd += (3 + 1 + 15 + 3) * esz + (1 + 12 + 4 + 4 + 6) * 4
-        wr += (1 + 12 + 3) * esz + (1 + 12 + 4) * 4
+        # streaming episode metrics, packed (round 5; csrc/fw_kernels.hip Met): previous command 3, control
+        # variation 1, e0 / sum / |sum| / overshoot extremum x3, the ring's previous error x3 (T); the goal-buffer
+        # words holding the new and the leaving status x3 + the window counts (u32); entry count, goal counts,
+        # settling x4, rise crossings x6 (u16).  Written: control variation, sum / |sum| x3, ring entry x3 (T); the
+        # new-status words x3 + the counts (u32); the entry count (u16).  Rows that change now and then (extrema,
+        # goal counts, settling and rise indices) are stored only when a lane changed them and are not counted.
+        rd += (3 + 1 + 12 + 3) * esz + (6 + 1) * 4 + 15 * 2
+        wr += (1 + 6 + 3) * esz + (3 + 1) * 4 + 1 * 2
     return rd, wr
 
 

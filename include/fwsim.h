@@ -129,6 +129,15 @@ typedef struct fw_sim_config {
   int32_t turbulence;              /* Dryden on/off */
   int32_t turb_len;                  /* chunk length L (turbulence_sim_length) */
   double dryden_g0[6], dryden_g1[6]; /* FIR taps, channels (u v w p q r) */
+  /* ABI 9: turbulence chunks too short for the FIR (L below ~45): the shaping filters' discretised state-space
+   * form, block-diagonal per filter u v w p q r (orders 1 2 2 1 3 3: 12 states; each block's matrix row-major).
+   * Within a chunk x[j] = Ad x[j-1] + Bd0 u[j-1] + Bd1 u[j] and the output is C x[j] (scipy lsim, first-order
+   * hold, step L^2 / (L - 1)); chunk c >= 1 starts from E1^c x (lsim's zero-input step to t[0] = c L^2, E1 =
+   * e^{A L^2}), which is 0 from chunk dryden_ncut on.                                                        */
+  int32_t dryden_state;              /* 0: the FIR above; 1: the filter bank below */
+  int32_t dryden_ncut;               /* first chunk whose carried-over state is negligible (E1^c < 1e-30) */
+  double dryden_ad[28], dryden_e1[28];
+  double dryden_b0[12], dryden_b1[12], dryden_c[12];
 } fw_sim_config;
 
 /* ---- gym env configuration (fixed_wing_config.json) ------------------------ */

@@ -427,9 +427,61 @@ static int constrain_commands(const fw_sim_config* c, double* cmd, double* sp) {
 /* Dryden FIR turbulence at step k (dryden.py:193-261 as wired by pyfly.py:781-783;
  * lsim FOH with vanishing Ad): chunk-local index j = k % L; j == 0 -> 0.
  * noise: [4][len] N(0,1) samples (already NOT scaled; scale sqrt(pi/L) applied). */
+/* Chunks too short for the FIR (fw_sim_config.dryden_state): the shaping filters' state-space recurrence
+ * (scipy 1.15.3 lsim, first-order hold: x[j] = Ad x[j-1] + Bd0 u[j-1] + Bd1 u[j], y = C x; each chunk c >= 1
+ * starts from expm(A c L^2) x_last, _ltisys.py lsim's zero-input step to t[0]), as wired by
+ * pyfly.py:781-783 / dryden.py:193-261.  Restated from scratch up to step k (a pure function of k, like
+ * the FIR; O(k) per call -- test sizes only). */
+static void orc_turbulence_bank(const fw_sim_config* c, const double* noise, int64_t len, int64_t k, double* turb) {
+  static const int ord[6] = {1, 2, 2, 1, 3, 3}, chan[6] = {0, 1, 2, 3, 1, 2};
+  const int64_t L = c->turb_len;
+  const double s = sqrt(PI_ / (double)L);
+  int oa = 0, ox = 0;
+  for (int f = 0; f < 6; f++) {
+    const int n = ord[f];
+    const double *Ad = c->dryden_ad + oa, *E1 = c->dryden_e1 + oa;
+    double x[3] = {0, 0, 0}, t[3];
+    for (int64_t i = 0; i <= k; i++) {
+      const int64_t ch = i / L, j = i % L;
+      if (j == 0) {
+        if (ch > 0) {
+          if (ch >= c->dryden_ncut) {
+            x[0] = x[1] = x[2] = 0;
+          } else {
+            for (int64_t p = 0; p < ch; p++) {
+              for (int r = 0; r < n; r++) {
+                t[r] = 0;
+                for (int q = 0; q < n; q++) t[r] += E1[r * n + q] * x[q];
+              }
+              for (int r = 0; r < n; r++) x[r] = t[r];
+            }
+          }
+        }
+      } else {
+        const double um1 = len > 0 ? s * noise[chan[f] * len + (i - 1) % len] : 0.0;
+        const double u0 = len > 0 ? s * noise[chan[f] * len + i % len] : 0.0;
+        for (int r = 0; r < n; r++) {
+          t[r] = c->dryden_b0[ox + r] * um1 + c->dryden_b1[ox + r] * u0;
+          for (int q = 0; q < n; q++) t[r] += Ad[r * n + q] * x[q];
+        }
+        for (int r = 0; r < n; r++) x[r] = t[r];
+      }
+    }
+    double y = 0;
+    for (int r = 0; r < n; r++) y += c->dryden_c[ox + r] * x[r];
+    turb[f] = y;
+    oa += n * n;
+    ox += n;
+  }
+}
+
 void orc_turbulence(const fw_sim_config* c, const double* noise, int64_t len, int64_t k, double* turb) {
   for (int i = 0; i < 6; i++) turb[i] = 0;
   if (!c->turbulence) return;
+  if (c->dryden_state) {
+    orc_turbulence_bank(c, noise, len, k, turb);
+    return;
+  }
   int64_t L = c->turb_len;
   if (k % L == 0) return;
   if (len < 1) return;

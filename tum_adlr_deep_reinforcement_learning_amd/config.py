@@ -109,7 +109,11 @@ class FwSimConfig(ctypes.Structure):
                 ("wind_mag_min", ctypes.c_double), ("wind_mag_max", ctypes.c_double),
                 ("wind_init_min", ctypes.c_double * 3), ("wind_init_max", ctypes.c_double * 3),
                 ("turbulence", ctypes.c_int32), ("turb_len", ctypes.c_int32),
-                ("dryden_g0", ctypes.c_double * 6), ("dryden_g1", ctypes.c_double * 6)]
+                ("dryden_g0", ctypes.c_double * 6), ("dryden_g1", ctypes.c_double * 6),
+                ("dryden_state", ctypes.c_int32), ("dryden_ncut", ctypes.c_int32),
+                ("dryden_ad", ctypes.c_double * 28), ("dryden_e1", ctypes.c_double * 28),
+                ("dryden_b0", ctypes.c_double * 12), ("dryden_b1", ctypes.c_double * 12),
+                ("dryden_c", ctypes.c_double * 12)]
 
 
 class FwObsEntry(ctypes.Structure):
@@ -307,6 +311,86 @@ def _tf2ss(num, den):
     return A, B, C
 
 
+DRYDEN_NAMES = ["H_u", "H_v", "H_w", "H_p", "H_q", "H_r"]
+DRYDEN_CHAN = [0, 1, 2, 3, 1, 2]  # noise channel of each filter (dryden.py:238-252)
+DRYDEN_ORDERS = [1, 2, 2, 1, 3, 3]
+
+
+def _foh(A, B, dT):
+    """scipy lsim's first-order-hold discretisation (scipy/signal/_ltisys.py lsim, interp=True): Ad, Bd0, Bd1
+    with x[i] = Ad x[i-1] + Bd0 u[i-1] + Bd1 u[i] (column-vector form)."""
+    from scipy.linalg import expm  # host-side config only
+    n = A.shape[0]
+    M = np.zeros((n + 2, n + 2))
+    M[:n, :n] = A * dT
+    M[:n, n:n + 1] = B * dT
+    M[n, n + 1] = 1.0
+    E = expm(M)
+    Bd1 = E[:n, n + 1:n + 2]
+    return E[:n, :n], E[:n, n:n + 1] - Bd1, Bd1
+
+
+def dryden_bank(turb_len, dt, wingspan, intensity):
+    """The six shaping filters as wired by pyfly.py:781-783 in discretised state-space form, for chunks too short
+    for the FIR reduction (dryden_fir): per filter (Ad, Bd0, Bd1, C, E1) with E1 = e^{A L^2}, the zero-input
+    propagation lsim applies between chunks (X0 carried from the previous chunk's last state over
+    t[0] = c L^2, scipy lsim: ``xout[0] = X0 @ expm(A.T * T[0])``).  Returns the flat fw_sim_config arrays and
+    ncut, the first chunk from which the carried state is negligible (max |E1^c| < 1e-30)."""
+    from scipy.linalg import expm  # host-side config only
+    L = int(turb_len)
+    if L < 2:
+        raise NotImplementedError("Dryden chunk length %d: lsim of a single sample" % L)
+    filt = dryden_filters(turb_len, dt, wingspan, 25.0, intensity)
+    dT = (L * float(turb_len)) / (L - 1)
+    T0 = L * float(turb_len)
+    ad, e1, b0, b1, cc, ncut = [], [], [], [], [], 1
+    for name in DRYDEN_NAMES:
+        A, B, C = _tf2ss(*filt[name])
+        Ad, Bd0, Bd1 = _foh(A, B, dT)
+        E1 = expm(A * T0)
+        ad += list(Ad.ravel())
+        e1 += list(E1.ravel())
+        b0 += list(Bd0[:, 0])
+        b1 += list(Bd1[:, 0])
+        cc += list(C[0])
+        P, c = E1.copy(), 1
+        while np.max(np.abs(P)) >= 1e-30:
+            c += 1
+            P = P @ E1
+            if c > 64:
+                raise NotImplementedError("Dryden chunk length %d: the carried filter state does not decay within "
+                                          "64 chunks" % L)
+        ncut = max(ncut, c)
+    return dict(ad=ad, e1=e1, b0=b0, b1=b1, c=cc, ncut=ncut)
+
+
+def dryden_bank_sim(bank, noise, L, k_end):
+    """Restatement of the filter bank for tests: outputs [6][k_end] for N(0,1) noise [4][len] (wrapped)."""
+    noise = np.asarray(noise, dtype=np.float64)
+    ln = noise.shape[1]
+    s = math.sqrt(math.pi / L)
+    out = np.zeros((6, k_end))
+    off_a = off_x = 0
+    for f, n in enumerate(DRYDEN_ORDERS):
+        Ad = np.array(bank["ad"][off_a:off_a + n * n]).reshape(n, n)
+        E1 = np.array(bank["e1"][off_a:off_a + n * n]).reshape(n, n)
+        B0 = np.array(bank["b0"][off_x:off_x + n])
+        B1 = np.array(bank["b1"][off_x:off_x + n])
+        Cf = np.array(bank["c"][off_x:off_x + n])
+        x = np.zeros(n)
+        for k in range(k_end):
+            c, j = divmod(k, L)
+            if j == 0:
+                if c > 0:
+                    x = np.linalg.matrix_power(E1, c) @ x if c < bank["ncut"] else np.zeros(n)
+            else:
+                x = Ad @ x + B0 * (s * noise[DRYDEN_CHAN[f], (k - 1) % ln]) + B1 * (s * noise[DRYDEN_CHAN[f], k % ln])
+            out[f, k] = Cf @ x
+        off_a += n * n
+        off_x += n
+    return out
+
+
 def dryden_fir(turb_len, dt, wingspan, intensity):
     """FIR taps g0 (u[k-1]) and g1 (u[k]) of the six Dryden outputs for the reference's wiring.
 
@@ -427,9 +511,17 @@ class SimSpec:
         c.turbulence = int(bool(cfg["turbulence"]))
         c.turb_len = int(cfg.get("turbulence_sim_length", 300))
         if c.turbulence:
-            g0, g1 = dryden_fir(c.turb_len, c.dt, float(self.params["b"]), cfg["turbulence_intensity"])
-            for i in range(6):
-                c.dryden_g0[i], c.dryden_g1[i] = g0[i], g1[i]
+            try:
+                g0, g1 = dryden_fir(c.turb_len, c.dt, float(self.params["b"]), cfg["turbulence_intensity"])
+                for i in range(6):
+                    c.dryden_g0[i], c.dryden_g1[i] = g0[i], g1[i]
+            except NotImplementedError:  # short chunks: the stateful filter bank (fw_sim_config.dryden_state)
+                bank = dryden_bank(c.turb_len, c.dt, float(self.params["b"]), cfg["turbulence_intensity"])
+                c.dryden_state, c.dryden_ncut = 1, int(bank["ncut"])
+                for name, n in (("ad", 28), ("e1", 28), ("b0", 12), ("b1", 12), ("c", 12)):
+                    arr = getattr(c, "dryden_" + name)
+                    for i in range(n):
+                        arr[i] = bank[name][i]
         return c
 
 

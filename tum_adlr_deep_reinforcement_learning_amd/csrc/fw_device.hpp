@@ -119,12 +119,18 @@ struct DevCfg {
   int euler_exact;                     // roll/pitch/yaw limited -> Euler-angle rotation post step
   T wind_mag_min, wind_mag_max, wind_init_min[3], wind_init_max[3];
   T g0[6], g1[6], noise_scale;
+  // chunks too short for the FIR (fw_sim_config.dryden_state): the shaping filters' discretised state-space
+  // blocks (orders 1 2 2 1 3 3), per-aircraft state in State::dry (fw_kernels.hip turbulence_at)
+  int dry_state, dry_ncut;
+  T dry_ad[28], dry_e1[28], dry_b0[12], dry_b1[12], dry_c[12];
   // ---- env ----
   int has_env;
   int steps_max, n_obs, scale_actions, has_bounds, streak_req, on_success, n_rew;
   int step_fail_timesteps;
   int act_window;                      // ring length of raw actions kept (max window - 1, >= 1)
   int cmd_window;                      // ring length of commands kept (0 if unused)
+  int act_need, cmd_need;              // previous actions / commands an env step reads (the rings keep one more
+                                       // for fw_observe, which re-reads the newest)
   T scale_low, scale_high, bmax, bmin;
   T act_low[3], act_high[3];
   int target_class[3], target_wrap[3];

@@ -75,6 +75,9 @@ constexpr int BLOCK = FW_BLOCK;
 // rows spill (339 VGPRs): 8192 aircraft 0.137 -> 0.099 ms per step without it (profiles/r03_ab_pref64.log)
 #define FW_PREF_Q4_F64 0
 #endif
+#ifndef FW_PREF_Q4_F32
+#define FW_PREF_Q4_F32 1  // 0: the fp32 quad instances load the epilogue's inputs after the integration (A/B)
+#endif
 #ifndef FW_PREF_Q1
 #define FW_PREF_Q1 0  // 1: the one-lane k_env_step instances prefetch the epilogue's loads too (A/B)
 #endif
@@ -102,13 +105,15 @@ struct State {
   uint32_t* episode;  // [ld]
   uint32_t* life;     // [ld] env steps since the handle was created (never reset): every launch steps every
                       // aircraft, so the value is the same on all lanes -- ring slots are indexed by it (below)
+  T* dry;             // [12][ld] Dryden filter-bank state of the current step (short chunks; null: FIR or off)
   const T* noise;     // injected N(0,1) turbulence noise [4][noise_len][ld] or null
   int64_t noise_len;
   int32_t* noise_env_len;  // [ld] per-env injected length (0: Philox; zeroed by the auto-reset) or null: all
   uint32_t key0, key1;  // Philox key = seed
   uint32_t env_offset;
   T* met;             // [MT_ROWS][ld] streaming episode-metric sums (null: metrics off)
-  uint32_t* metu;     // [MU_ROWS][ld] their counters / indices
+  uint32_t* metu;     // [MU_ROWS][ld] goal-status buffers and window counts
+  uint16_t* metu16;   // [M16_ROWS][ld] counters / indices
   T* met_out;         // [FW_NMETRIC][N] (SoA) record of done envs (null: not requested)
   T* obs_init;        // [n_obs][ld] raw observation row at the episode's reset (null: length-1 observations)
   T* obs_ring;        // [obs_hist][n_obs][ld] raw rows of past steps, slot = (L_ep + step) % obs_hist
@@ -124,19 +129,24 @@ struct State {
   uint32_t* col_cnt;  // merge-tree arrival counters (handle workspace, zero between launches)
 };
 
-// streaming episode-metric state (fixed_wing.py:1644-1736 restated over running sums):
-// T rows: e0, sum, |sum|, min, max, previous error, sum of the last FW_M_END_WINDOW errors
-// (x3 targets), control variation, ring of the last FW_M_END_WINDOW errors
-constexpr int MR_E0 = 0, MR_ESUM = 3, MR_EABS = 6, MR_EMIN = 9, MR_EMAX = 12, MR_PREV = 15, MR_WSUM = 18, MR_CV = 21,
-              MR_RING = 22;
+// streaming episode-metric state (fixed_wing.py:1644-1736 restated over running sums), packed (round 5):
+// T rows: e0, sum, |sum|, the extremum overshoot reads (the minimum where e0 > 0, else the maximum) (x3 targets),
+// control variation, ring of the last FW_M_END_WINDOW errors.  Not kept: the previous error (the ring's previous
+// entry) and the end-error window sum (summed from the ring when the episode ends).
+constexpr int MR_E0 = 0, MR_ESUM = 3, MR_EABS = 6, MR_EXT = 9, MR_CV = 12, MR_RING = 13;
 constexpr int MT_ROWS = MR_RING + 3 * FW_M_END_WINDOW;
-// uint32 rows: error count, goal registers (roll/pitch/Va x 128 bit), goal counts (4),
-// settling index (4, ~0u = none), first crossings below the high / low rise limits (3 x 2)
-constexpr int MU_N = 0, MU_GB = 1, MU_GC = 13, MU_SET = 17, MU_RISE = 21;
-constexpr int MU_ROWS = MU_RISE + 6;
-constexpr uint32_t M_NONE = 0xFFFFFFFFu;
-constexpr int MD_MINMAX = 0, MD_U = 6;  // Met::dirty bits: 6 min/max rows, then the MU_ROWS - MU_GC rare u32 rows
-static_assert(MD_U + (MU_ROWS - MU_GC) <= 32, "Met::dirty holds one bit per rarely-changing row");
+// uint32 rows: per target (roll / pitch / Va) a 128-bit circular buffer of goal statuses indexed by the LIFETIME
+// step (entry e of the episode at bit (lep + e) % 128: every lane of a wave touches the same word rows), and the
+// three window counts (ones among the last success_streak_req entries) as bytes of one word
+constexpr int MU_GB = 0, MU_CNT = 12;
+constexpr int MU_ROWS = MU_CNT + 1;
+// uint16 rows: entry count, goal counts (4), settling index (4, 0xFFFF = none), first crossings below the high /
+// low rise limits (3 x 2)
+constexpr int M16_N = 0, M16_GC = 1, M16_SET = 5, M16_RISE = 9;
+constexpr int M16_ROWS = M16_RISE + 6;
+constexpr uint32_t M_NONE = 0xFFFFu;
+constexpr int MD_EXT = 0, MD_U = 3;  // Met::dirty bits: 3 extremum rows, then the M16_ROWS - M16_GC rare u16 rows
+static_assert(MD_U + (M16_ROWS - M16_GC) <= 32, "Met::dirty holds one bit per rarely-changing row");
 
 // Debug build only (-DFW_TIMING, tools/phase_timing.py): lane 0 of every wave stamps the
 // 100 MHz real-time clock at phase boundaries into the episode_out buffer (8 x u64 per wave),
@@ -183,11 +193,95 @@ __device__ __forceinline__ void noise4(const State<T>& s, int64_t i, uint32_t ep
   normal4<T>(r, u);
 }
 
+// The Dryden filter bank for chunks too short for the FIR (fw_sim_config.dryden_state, fwsim.h): State::dry
+// holds x_k, the filters' state at step k (0 at reset); the turbulence of step k is C x_k, and the step
+// (lead lane only: a quad's four lanes compute the same) stores x_{k+1} = Ad x_k + Bd0 u_k + Bd1 u_{k+1} --
+// scipy lsim's first-order hold inside a chunk (dryden.py:238-252 as wired by pyfly.py:781-783) -- or, at
+// a chunk boundary, E1^c x_k (lsim's zero-input step to t[0] = c L^2 for chunk c; 0 from dryden_ncut on).
+template <typename T>
+__device__ __forceinline__ void dryden_bank_at(const DevCfg<T>& c, const State<T>& s, int64_t i, uint32_t episode,
+                                               int k, T tl[3], T ta[3], bool lead) {
+  constexpr int ord[6] = {1, 2, 2, 1, 3, 3}, chan[6] = {0, 1, 2, 3, 1, 2};
+  T x[12], out[6];
+#pragma unroll
+  for (int r = 0; r < 12; r++) x[r] = ld_(s.dry, r, s.ld, i);
+  {
+    int ox = 0;
+#pragma unroll
+    for (int f = 0; f < 6; f++) {
+      T y = T(0);
+#pragma unroll
+      for (int r = 0; r < ord[f]; r++) y += c.dry_c[ox + r] * x[ox + r];
+      out[f] = y;
+      ox += ord[f];
+    }
+  }
+  tl[0] = out[0];
+  tl[1] = out[1];
+  tl[2] = out[2];
+  ta[0] = out[3];
+  ta[1] = out[4];
+  ta[2] = out[5];
+  if (!lead) return;
+  const int kn = k + 1;
+  T xn[12];
+  if (kn % c.turb_len == 0) {  // the next step opens chunk ch: zero-input propagation of the last state
+    const int ch = kn / c.turb_len;
+#pragma unroll
+    for (int r = 0; r < 12; r++) xn[r] = T(0);
+    if (ch < c.dry_ncut) {
+#pragma unroll
+      for (int r = 0; r < 12; r++) xn[r] = x[r];
+      for (int p = 0; p < ch; p++) {
+        int oa = 0, ox = 0;
+#pragma unroll
+        for (int f = 0; f < 6; f++) {
+          T t[3];
+#pragma unroll
+          for (int r = 0; r < ord[f]; r++) {
+            t[r] = T(0);
+#pragma unroll
+            for (int q = 0; q < ord[f]; q++) t[r] += c.dry_e1[oa + r * ord[f] + q] * xn[ox + q];
+          }
+#pragma unroll
+          for (int r = 0; r < ord[f]; r++) xn[ox + r] = t[r];
+          oa += ord[f] * ord[f];
+          ox += ord[f];
+        }
+      }
+    }
+  } else {
+    T u0[4], u1[4];
+    noise4(s, i, episode, k, u0);
+    noise4(s, i, episode, kn, u1);
+    int oa = 0, ox = 0;
+#pragma unroll
+    for (int f = 0; f < 6; f++) {
+      const T a = c.noise_scale * u0[chan[f]], b = c.noise_scale * u1[chan[f]];
+#pragma unroll
+      for (int r = 0; r < ord[f]; r++) {
+        T t = c.dry_b0[ox + r] * a + c.dry_b1[ox + r] * b;
+#pragma unroll
+        for (int q = 0; q < ord[f]; q++) t += c.dry_ad[oa + r * ord[f] + q] * x[ox + q];
+        xn[ox + r] = t;
+      }
+      oa += ord[f] * ord[f];
+      ox += ord[f];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 12; r++) st_(s.dry, r, s.ld, i, xn[r]);
+}
+
 template <typename T>
 __device__ __forceinline__ void turbulence_at(const DevCfg<T>& c, const State<T>& s, int64_t i, uint32_t episode, int k,
-                                              T tl[3], T ta[3]) {
+                                              T tl[3], T ta[3], bool lead = true) {
   tl[0] = tl[1] = tl[2] = ta[0] = ta[1] = ta[2] = T(0);
   if (!c.turbulence) return;
+  if (c.dry_state && s.dry) {  // (fw_update_config refuses the filter bank on a handle without its rows)
+    dryden_bank_at(c, s, i, episode, k, tl, ta, lead);
+    return;
+  }
   if (k % c.turb_len == 0) return;
   T un1[4], u0[4];
   noise4(s, i, episode, k - 1, un1);
@@ -425,6 +519,21 @@ __device__ __forceinline__ bool settled(const DevCfg<T>& c, const uint32_t g[4],
   return (double)cnt / (double)req >= (double)c.streak_frac;
 }
 
+// the deque condition of success / settling_time from a window count: `n` entries so far, `cnt` ones among
+// the last success_streak_req of them
+template <typename T>
+__device__ __forceinline__ bool settled_n(const DevCfg<T>& c, uint32_t cnt, uint32_t n) {
+  const int req = c.streak_req;
+  return req > 0 && (int64_t)n >= req && (double)cnt / (double)req >= (double)c.streak_frac;
+}
+
+// bit `pos` (0..127) of target k's goal-status buffer lives in word row MU_GB + 4 k + pos / 32
+__device__ __forceinline__ int gb_row(int k, uint32_t pos) { return MU_GB + 4 * k + (int)((pos & 127u) >> 5); }
+__device__ __forceinline__ uint32_t gb_set(uint32_t w, uint32_t pos, uint32_t bit) {
+  const uint32_t m = 1u << (pos & 31u);
+  return (w & ~m) | (bit ? m : 0u);
+}
+
 template <typename T>
 __device__ __forceinline__ void metrics_init(const DevCfg<T>& c, const State<T>& s, int64_t i, const T* tgt,
                                              const T* vals, uint32_t lep) {
@@ -437,26 +546,26 @@ __device__ __forceinline__ void metrics_init(const DevCfg<T>& c, const State<T>&
     st_(s.met, MR_E0 + k, ld, i, err);
     st_(s.met, MR_ESUM + k, ld, i, err);
     st_(s.met, MR_EABS + k, ld, i, T(fabs(err)));
-    st_(s.met, MR_EMIN + k, ld, i, err);
-    st_(s.met, MR_EMAX + k, ld, i, err);
-    st_(s.met, MR_PREV + k, ld, i, err);
-    st_(s.met, MR_WSUM + k, ld, i, err);
+    st_(s.met, MR_EXT + k, ld, i, err);
     st_(s.met, MR_RING + 3 * slot0 + k, ld, i, err);
   }
   st_(s.met, MR_CV, ld, i, T(0));
-  st_(s.metu, MU_N, ld, i, 1u);
+  st_(s.metu16, M16_N, ld, i, (uint16_t)1);
+  uint32_t cnt = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const uint32_t bit = (gb >> k) & 1u;
-    uint32_t g[4] = {bit, 0u, 0u, 0u};
-    if (k < 3)
-#pragma unroll
-      for (int w = 0; w < 4; w++) st_(s.metu, MU_GB + 4 * k + w, ld, i, g[w]);
-    st_(s.metu, MU_GC + k, ld, i, bit);
-    st_(s.metu, MU_SET + k, ld, i, (c.streak_req > 0 && settled(c, g, 1u)) ? 0u : M_NONE);
+    if (k < 3) {  // entry 0 of the buffer; the other bits belong to earlier episodes and are never counted
+      const int row = gb_row(k, lep);
+      st_(s.metu, row, ld, i, gb_set(ld_(s.metu, row, ld, i), lep, bit));
+      cnt |= bit << (8 * k);
+    }
+    st_(s.metu16, M16_GC + k, ld, i, (uint16_t)bit);
+    st_(s.metu16, M16_SET + k, ld, i, (uint16_t)(settled_n(c, bit, 1u) ? 0u : M_NONE));
   }
+  st_(s.metu, MU_CNT, ld, i, cnt);
 #pragma unroll
-  for (int r = 0; r < 6; r++) st_(s.metu, MU_RISE + r, ld, i, M_NONE);
+  for (int r = 0; r < 6; r++) st_(s.metu16, M16_RISE + r, ld, i, (uint16_t)M_NONE);
 }
 
 __device__ __forceinline__ bool bits_differ(float a, float b) { return __float_as_uint(a) != __float_as_uint(b); }
@@ -468,136 +577,151 @@ __device__ __forceinline__ bool bits_differ(double a, double b) {
 // (no load depends on another, none follows a store) and written back in one batch.
 template <typename T>
 struct Met {
-  T row[MR_RING];          // e0 / sum / |sum| / min / max / prev / window sum (x3), cv
-  uint32_t u[MU_ROWS];     // count, goal registers, goal counts, settling, rise
-  T old[3];                // ring entries the next error overwrites (slot `slot`)
-  int slot;
-  // rows that change only now and then (the minima / maxima, goal counts, settling and rise indices): a set
+  T row[MR_RING];          // e0 / sum / |sum| / extremum (x3), cv
+  uint32_t u[M16_ROWS];    // count, goal counts, settling, rise (uint16 rows)
+  uint32_t cnt;            // window counts, one byte per target
+  T prev[3];               // the previous entry's errors (ring)
+  uint32_t gw_new[3], gw_old[3];  // goal-buffer words holding the new entry's bit / the leaving entry's bit
+  uint32_t b;              // the entry index the loads assumed (steps0 + 1)
+  // rows that change only now and then (the extrema, goal counts, settling and rise indices): a set
   // bit k marks row MD_* k as changed in this lane; store() writes such a row when some lane of the wave
   // changed it (whole-row coalesced stores), so a steady step writes the rows the traffic accounting counts
   uint32_t dirty;
-  // `slot` is known before the count is loaded: within an episode every step but a terminal
-  // failure appends an error, so the new entry's index is steps0 + 1; entry b lives in ring slot
-  // (lep + b) % FW_M_END_WINDOW (lep = the episode's first `life`: the same on every lane, so coalesced)
-  __device__ __forceinline__ void load(const State<T>& s, int64_t i, uint32_t lep, int steps0) {
+  // within an episode every step but a terminal failure appends an entry, so the new entry's index is
+  // steps0 + 1; entry e lives in ring slot (lep + e) % FW_M_END_WINDOW and goal bit (lep + e) % 128 (lep = the
+  // episode's first `life`, the same on every lane for the same e: coalesced rows)
+  __device__ __forceinline__ void fetch_entry(const DevCfg<T>& c, const State<T>& s, int64_t i, uint32_t lep) {
+    const int ps = (int)((lep + b - 1u) % (uint32_t)FW_M_END_WINDOW);
+#pragma unroll
+    for (int k = 0; k < 3; k++) prev[k] = ld_(s.met, MR_RING + 3 * ps + k, s.ld, i);
+    const uint32_t pn = lep + b, po = pn - (uint32_t)(c.streak_req > 0 ? c.streak_req : 0);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      gw_new[k] = ld_(s.metu, gb_row(k, pn), s.ld, i);
+      gw_old[k] = ld_(s.metu, gb_row(k, po), s.ld, i);
+    }
+  }
+  __device__ __forceinline__ void load(const DevCfg<T>& c, const State<T>& s, int64_t i, uint32_t lep, int steps0) {
 #pragma unroll
     for (int r = 0; r < MR_RING; r++) row[r] = ld_(s.met, r, s.ld, i);
 #pragma unroll
-    for (int r = 0; r < MU_ROWS; r++) u[r] = ld_(s.metu, r, s.ld, i);
-    slot = (int)((lep + (uint32_t)steps0 + 1u) % (uint32_t)FW_M_END_WINDOW);
+    for (int r = 0; r < M16_ROWS; r++) u[r] = ld_(s.metu16, r, s.ld, i);
+    cnt = ld_(s.metu, MU_CNT, s.ld, i);
+    b = (uint32_t)steps0 + 1u;
     dirty = 0u;
-#pragma unroll
-    for (int k = 0; k < 3; k++) old[k] = ld_(s.met, MR_RING + 3 * slot + k, s.ld, i);
+    fetch_entry(c, s, i, lep);
   }
   __device__ __forceinline__ void store(const State<T>& s, int64_t i) const {
     // MR_E0 (the episode's initial errors) never changes after metrics_init: not written back
 #pragma unroll
     for (int r = MR_ESUM; r < MR_RING; r++) {
-      const bool rare = r >= MR_EMIN && r < MR_EMIN + 6;  // the minima and maxima
-      if (!rare || __ballot((dirty >> (MD_MINMAX + r - MR_EMIN)) & 1u)) st_(s.met, r, s.ld, i, row[r]);
+      const bool rare = r >= MR_EXT && r < MR_EXT + 3;  // the extrema
+      if (!rare || __ballot((dirty >> (MD_EXT + r - MR_EXT)) & 1u)) st_(s.met, r, s.ld, i, row[r]);
     }
 #pragma unroll
-    for (int r = 0; r < MU_ROWS; r++) {
-      const bool rare = r >= MU_GC;  // goal counts, settling, rise indices
-      if (!rare || __ballot((dirty >> (MD_U + r - MU_GC)) & 1u)) st_(s.metu, r, s.ld, i, u[r]);
+    for (int r = 0; r < M16_ROWS; r++) {
+      const bool rare = r >= M16_GC;  // goal counts, settling, rise indices
+      if (!rare || __ballot((dirty >> (MD_U + r - M16_GC)) & 1u)) st_(s.metu16, r, s.ld, i, (uint16_t)u[r]);
     }
+    st_(s.metu, MU_CNT, s.ld, i, cnt);
   }
 };
 
 // one successful step: errors w.r.t. the NEW targets (fixed_wing.py:575-579), goal statuses
 // `gb` w.r.t. the old ones (:534-537); gall = the updated "all" register.  Writes the new
-// error into the end-error ring.
+// error into the end-error ring and the new goal bits into the goal buffers.
 template <typename T>
 __device__ __forceinline__ void metrics_step(const DevCfg<T>& c, const State<T>& s, int64_t i, Met<T>& M,
                                              const T* tgt, const T* vals, uint32_t gb, const uint32_t gall[4],
                                              uint32_t lep) {
-  const uint32_t n0 = M.u[MU_N], b = n0;  // index of the new history entry
-  const int slot = (int)((lep + n0) % (uint32_t)FW_M_END_WINDOW);
-  if (slot != M.slot) {  // stepping on after a failed (done) step without reset: re-read
-    M.slot = slot;
-#pragma unroll
-    for (int k = 0; k < 3; k++) M.old[k] = ld_(s.met, MR_RING + 3 * slot + k, s.ld, i);
+  const uint32_t n0 = M.u[M16_N], b = n0;  // index of the new history entry
+  if (b != M.b) {  // stepping on after a failed (done) step without reset: the entry's slots moved
+    M.b = b;
+    M.fetch_entry(c, s, i, lep);
   }
+  const int slot = (int)((lep + b) % (uint32_t)FW_M_END_WINDOW);
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     const T err = target_error(c, k, tgt[k], vals[k]);
-    const T prev = M.row[MR_PREV + k], e0 = M.row[MR_E0 + k];
+    const T prev = M.prev[k], e0 = M.row[MR_E0 + k];
     M.row[MR_ESUM + k] += err;
     M.row[MR_EABS + k] += T(fabs(err));
-    {
-      const T mn = fmin(M.row[MR_EMIN + k], err), mx = fmax(M.row[MR_EMAX + k], err);
-      if (bits_differ(mn, M.row[MR_EMIN + k])) M.dirty |= 1u << (MD_MINMAX + k);
-      if (bits_differ(mx, M.row[MR_EMAX + k])) M.dirty |= 1u << (MD_MINMAX + 3 + k);
-      M.row[MR_EMIN + k] = mn;
-      M.row[MR_EMAX + k] = mx;
+    {  // overshoot's extremum (fixed_wing.py:1722-1730): the minimum where e0 > 0, else the maximum
+      const T x = e0 > T(0) ? fmin(M.row[MR_EXT + k], err) : fmax(M.row[MR_EXT + k], err);
+      if (bits_differ(x, M.row[MR_EXT + k])) M.dirty |= 1u << (MD_EXT + k);
+      M.row[MR_EXT + k] = x;
     }
-    M.row[MR_PREV + k] = err;
-    M.row[MR_WSUM + k] += n0 >= (uint32_t)FW_M_END_WINDOW ? err - M.old[k] : err;
     st_(s.met, MR_RING + 3 * slot + k, s.ld, i, err);
     // rise_time: earliest downward crossing of |error| through each limit
     const T lims[2] = {T(fabs(c.rise_high * e0)), T(fabs(c.rise_low * e0))};
 #pragma unroll
     for (int w = 0; w < 2; w++) {
-      uint32_t& r = M.u[MU_RISE + 2 * k + w];
+      uint32_t& r = M.u[M16_RISE + 2 * k + w];
       if (r == M_NONE && fabs(prev) >= lims[w] && fabs(err) < lims[w]) {
         r = b;
-        M.dirty |= 1u << (MD_U + MU_RISE - MU_GC + 2 * k + w);
+        M.dirty |= 1u << (MD_U + M16_RISE - M16_GC + 2 * k + w);
       }
     }
   }
   if (c.streak_req > 0) {
+    const uint32_t pn = lep + b, po = pn - (uint32_t)c.streak_req;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t bit = (gb >> k) & 1u;
-      uint32_t g[4];
-      if (k < 3) {
-        uint32_t* R = M.u + MU_GB + 4 * k;
-        R[3] = (R[3] << 1) | (R[2] >> 31);
-        R[2] = (R[2] << 1) | (R[1] >> 31);
-        R[1] = (R[1] << 1) | (R[0] >> 31);
-        R[0] = (R[0] << 1) | bit;
-#pragma unroll
-        for (int w = 0; w < 4; w++) g[w] = R[w];
+      bool set;
+      if (k < 3) {  // the window count: + the new status, - the one leaving the req-deep window
+        uint32_t ck = (M.cnt >> (8 * k)) & 0xFFu;
+        if (b >= (uint32_t)c.streak_req) ck -= (M.gw_old[k] >> (po & 31u)) & 1u;
+        ck += bit;
+        M.cnt = (M.cnt & ~(0xFFu << (8 * k))) | (ck << (8 * k));
+        st_(s.metu, gb_row(k, pn), s.ld, i, gb_set(M.gw_new[k], pn, bit));
+        set = settled_n(c, ck, n0 + 1u);
       } else {
-#pragma unroll
-        for (int w = 0; w < 4; w++) g[w] = gall[w];
+        set = settled(c, gall, n0 + 1u);
       }
-      M.u[MU_GC + k] += bit;
+      M.u[M16_GC + k] += bit;
       M.dirty |= bit << (MD_U + k);
-      if (M.u[MU_SET + k] == M_NONE && settled(c, g, n0 + 1u)) {
-        M.u[MU_SET + k] = b;
-        M.dirty |= 1u << (MD_U + MU_SET - MU_GC + k);
+      if (M.u[M16_SET + k] == M_NONE && set) {
+        M.u[M16_SET + k] = b;
+        M.dirty |= 1u << (MD_U + M16_SET - M16_GC + k);
       }
     }
   }
-  M.u[MU_N] = n0 + 1u;
+  M.u[M16_N] = n0 + 1u;
 }
 
 // the record of a done episode (get_metric for every cfg metric), layout FW_M_* of fwsim.h
-// out: column of the SoA record [FW_NMETRIC][N] (element m at out[m * stride])
+// out: column of the SoA record [FW_NMETRIC][N] (element m at out[m * stride]).  end_error sums the ring's
+// last min(n, FW_M_END_WINDOW) entries oldest first (np.mean(v[-50:]), fixed_wing.py:1665-1668).
 template <typename T>
-__device__ __forceinline__ void metrics_final(const DevCfg<T>& c, const Met<T>& M, int n_commands, T* out,
-                                              int64_t stride) {
+__device__ __forceinline__ void metrics_final(const DevCfg<T>& c, const State<T>& s, int64_t i, const Met<T>& M,
+                                              uint32_t lep, int n_commands, T* out, int64_t stride) {
   const T nan = T(NAN);
-  const uint32_t n = M.u[MU_N];
+  const uint32_t n = M.u[M16_N];
   const int cnt = n < (uint32_t)FW_M_END_WINDOW ? (int)n : FW_M_END_WINDOW;
+  T wsum[3] = {T(0), T(0), T(0)};
+  for (int e = (int)n - cnt; e < (int)n; e++) {
+    const int sl = (int)((lep + (uint32_t)e) % (uint32_t)FW_M_END_WINDOW);
+#pragma unroll
+    for (int k = 0; k < 3; k++) wsum[k] += ld_(s.met, MR_RING + 3 * sl + k, s.ld, i);
+  }
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     const T e0 = M.row[MR_E0 + k];
-    const uint32_t rs = M.u[MU_RISE + 2 * k], re = M.u[MU_RISE + 2 * k + 1];
+    const uint32_t rs = M.u[M16_RISE + 2 * k], re = M.u[M16_RISE + 2 * k + 1];
     out[(FW_M_RISE_TIME + k) * stride] = (rs != M_NONE && re != M_NONE) ? T((double)re - (double)rs) : nan;
-    const T m = e0 > T(0) ? M.row[MR_EMIN + k] : M.row[MR_EMAX + k];
+    const T m = M.row[MR_EXT + k];
     out[(FW_M_OVERSHOOT + k) * stride] = sgn(m) == sgn(e0) ? nan : T(fabs(m / e0));
     out[(FW_M_TOTAL_ERROR + k) * stride] = M.row[MR_EABS + k];
     out[(FW_M_AVG_ERROR + k) * stride] = fabs(e0) >= T(0.01) ? T(fabs(M.row[MR_ESUM + k] / (T)n / e0)) : nan;
-    out[(FW_M_END_ERROR + k) * stride] = T(fabs(M.row[MR_WSUM + k] / (T)cnt));
+    out[(FW_M_END_ERROR + k) * stride] = T(fabs(wsum[k] / (T)cnt));
   }
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    const uint32_t st = M.u[MU_SET + k];
+    const uint32_t st = M.u[M16_SET + k];
     out[(FW_M_SETTLING_TIME + k) * stride] = st != M_NONE ? (T)st : nan;
     out[(FW_M_SUCCESS + k) * stride] = st != M_NONE ? T(1) : T(0);
-    out[(FW_M_SUCCESS_TIME_FRAC + k) * stride] = (T)((double)M.u[MU_GC + k] / (double)n);
+    out[(FW_M_SUCCESS_TIME_FRAC + k) * stride] = (T)((double)M.u[M16_GC + k] / (double)n);
   }
   out[FW_M_CONTROL_VARIATION * stride] = n_commands >= 2 ? M.row[MR_CV] / (T(3) * c.dt * (T)(n_commands - 1)) : nan;
 }
@@ -736,6 +860,9 @@ __device__ __forceinline__ void store_env_fresh(const DevCfg<T>& c, const State<
   for (int k = 0; k < 8; k++) st_(s.der, k, ld, i, der[k]);
 #pragma unroll
   for (int k = 0; k < 3; k++) st_(s.wind, k, ld, i, wind[k]);
+  if (s.dry)  // Dryden.reset: lsim restarts from X0 = None (dryden.py:41-48, 190-191)
+#pragma unroll
+    for (int r = 0; r < 12; r++) st_(s.dry, r, ld, i, T(0));
   if (c.has_env) {
 #pragma unroll
     for (int k = 0; k < 3; k++) st_(s.target, k, ld, i, tgt[k]);
@@ -849,7 +976,7 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_sim_step(const DevCfg<T>
   const uint32_t sw = s.steps[i];
   const int k = (int)(sw & 0xFFFFu);
   T tl[3], ta[3];
-  turbulence_at(c, s, i, s.episode[i], k, tl, ta);
+  turbulence_at(c, s, i, s.episode[i], k, tl, ta, qr == 0);
   int nfev = 0, nacc = 0;
   uint32_t dmask = 0;
   __shared__ V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];  // y, f (+ error sum) of the block's aircraft (pairs)
@@ -915,7 +1042,9 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   const uint32_t sw = s.steps[i];
   const int steps0 = (int)(sw & 0xFFFFu);
   const int steps_tgt0 = (int)(sw >> 16);
-  const uint32_t episode = s.episode[i];
+  // the episode counter keys the Philox streams of turbulence and observation noise (the reset path reads it
+  // itself): without either it is not loaded
+  const uint32_t episode = (c.turbulence || c.obs_noise) ? s.episode[i] : 0u;
   // ring slots by `life` (the same on every lane: coalesced rows however the episodes are staggered; slots by
   // the episode step scattered a wave's ring accesses over up to 64 rows once resets desynchronised the
   // episodes, +30 % HBM traffic per launch at the bench's steady state, profiles/r04_traffic_split.json)
@@ -940,12 +1069,12 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
 #pragma unroll
       for (int q = 0; q < 3; q++) seqA[j][q] = seqC[j][q] = T(0);
       // previous action j = action number steps-j (1-based) -> slot (life0 - j) % window
-      if (j <= c.act_window && steps - j >= 1) {
+      if (j <= c.act_need && steps - j >= 1) {
         const int slot = (int)((life0 - (uint32_t)j) % (uint32_t)c.act_window);
 #pragma unroll
         for (int q = 0; q < 3; q++) seqA[j][q] = s.act_ring[((int64_t)slot * 3 + q) * ld + i];
       }
-      if (j <= c.cmd_window && steps - j >= 1) {
+      if (j <= c.cmd_need && steps - j >= 1) {
         const int slot = (int)((life0 - (uint32_t)j) % (uint32_t)c.cmd_window);
 #pragma unroll
         for (int q = 0; q < 3; q++) seqC[j][q] = s.cmd_ring[((int64_t)slot * 3 + q) * ld + i];
@@ -953,7 +1082,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
     }
     load_row(s.goal, 4, ld, i, g);
     if (c.metrics) {
-      M.load(s, i, lep, steps0);
+      M.load(c, s, i, lep, steps0);
       load_row(s.cmd, 3, ld, i, prev_cmd);
     }
     ep_ret0 = ld_(s.ep_ret, 0, ld, i);
@@ -962,7 +1091,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
 
   // ---- PyFly.step ----
   T tl[3], ta[3];
-  turbulence_at(c, s, i, episode, steps0, tl, ta);
+  turbulence_at(c, s, i, episode, steps0, tl, ta, qr == 0);
   FW_TSTAMP(1);
   int nfev = 0, nacc = 0;
   uint32_t dmask = 0;
@@ -1024,6 +1153,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   }
 #pragma unroll
   for (int q = 0; q < 3; q++) st_(s.cmd, q, ld, i, cmd[q]);
+  const T tgt_in[3] = {tgt[0], tgt[1], tgt[2]};  // a target row is stored only where some lane changed it
   if (sterm == 0) {
     const T vals[3] = {der[0], der[1], der[3]};
     uint32_t gb = 0;
@@ -1086,7 +1216,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
     M.store(s, i);
 #endif
 #ifndef FW_MET_SKIP_FINAL
-    if (done && s.met_out) metrics_final(c, M, steps, s.met_out + i, s.n);
+    if (done && s.met_out) metrics_final(c, s, i, M, lep, steps, s.met_out + i, s.n);
 #endif
   }
   FW_TSTAMP(3);
@@ -1106,7 +1236,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
       }
 #endif
       T seq0[RING + 1][3];
-      observe_env(c, s, i, episode + 1u, OBS_RESET, yr, dr, tr, 0, seq0, seq0, orow, life0 + 1u);
+      observe_env(c, s, i, s.episode[i], OBS_RESET, yr, dr, tr, 0, seq0, seq0, orow, life0 + 1u);  // (reset_lane's +1)
       s.life[i] = life0 + 1u;
       FW_TSTAMP(5);
       return;
@@ -1120,7 +1250,8 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
 #pragma unroll
   for (int r = 0; r < 8; r++) st_(s.der, r, ld, i, der[r]);
 #pragma unroll
-  for (int k = 0; k < 3; k++) st_(s.target, k, ld, i, tgt[k]);
+  for (int k = 0; k < 3; k++)  // (constant-class targets never change within an episode)
+    if (__ballot(bits_differ(tgt[k], tgt_in[k]))) st_(s.target, k, ld, i, tgt[k]);
 #pragma unroll
   for (int w = 0; w < 4; w++) st_(s.goal, w, ld, i, g[w]);
   st_(s.ep_ret, 0, ld, i, ep_ret);
@@ -1130,20 +1261,20 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
 }
 
 // ---- in-launch merge of the block records (fw_collect_epilogue.merged) ---------------------------------
-// Words handed to another block of the same launch go through agent-scope atomic read-modify-writes on
-// both sides (the producer's exchanges are performed before its ticket is drawn, the consumer's loads are
-// issued after its ticket returned): every such access is performed at the device's coherence point, so
-// neither the producer's L2 nor the consumer's L1 / L2 can hold a stale copy, and no cache write-back or
-// invalidate (release / acquire fence, several us each at four blocks per CU) is needed.  A publisher
-// folds the returned old values into one register that the ticket's wait consumes: the exchanges stay in
-// flight together (consumed one by one, each would wait out its own round trip).
-__device__ __forceinline__ void pub64(double* p, double v, unsigned long long& acc) {
-  acc ^= __hip_atomic_exchange((unsigned long long*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+// Hand-off between blocks of one launch (MI355X_MICROARCH.md, hand-off table row 1): every word handed over
+// is stored with an agent-scope store (write-through, `sc1`), every storing wave waits for its stores
+// (s_waitcnt vmcnt(0)) and then ONE lane adds to the node's agent-scope counter; the block whose add returns
+// the last count loads the words with agent-scope loads (`sc1`, L1 bypassed) only after that add returned.
+// No cache write-back / invalidate fence (several us each at four blocks per CU).  The first version moved
+// the words with agent-scope read-modify-write atomics instead: each lane's atomic is its own memory-side
+// transaction, and the tree cost 16 us per launch (tools/epilogue_ab.py).
+// (global address space: `global_` instructions -- the hand-off is not valid through `flat_` ones)
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+__device__ __forceinline__ void pub64(double* p, double v) {
+  __hip_atomic_store((g_u64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ double get64(const double* p) {
-  return __longlong_as_double(
-      (long long)__hip_atomic_fetch_add((unsigned long long*)p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  return __longlong_as_double((long long)__hip_atomic_load((const g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
 constexpr int COL_MAXD = FW_MAX_OBS + 1;
@@ -1232,7 +1363,7 @@ __device__ __forceinline__ void merge_node(const double* src, int64_t stride, in
 // each node's counter is reset by its last arriver, for the next launch.  The merged record equals the one
 // merge over all block records (fw_moments_merge) to rounding, not bit for bit (another summation tree).
 __device__ __forceinline__ void collect_merge(const double* rec0, double* lvl, uint32_t* cnt, double* merged, double* rms,
-                                           int D, int d, bool has_ret, double* st, unsigned long long pacc) {
+                                           int D, int d, bool has_ret, double* st) {
   const int l = (int)(threadIdx.x & 63);
   int64_t nodes = gridDim.x, idx = blockIdx.x, stride = gridDim.x;
   const double* src = rec0;
@@ -1240,7 +1371,7 @@ __device__ __forceinline__ void collect_merge(const double* rec0, double* lvl, u
     const bool fin = nodes <= fw_stats::MERGE_FANIN;
     const int64_t g = fin ? 0 : idx / fw_stats::MERGE_FANIN;
     const int gs = fin ? (int)nodes : (int)std::min<int64_t>(fw_stats::MERGE_FANIN, nodes - g * fw_stats::MERGE_FANIN);
-    asm volatile("s_waitcnt vmcnt(0)" ::"v"(pacc) : "memory");  // this block's published words are performed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's published words have left the CU
     uint32_t t = 0;
     if (l == 0) t = __hip_atomic_fetch_add(cnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     t = __shfl(t, 0);
@@ -1271,12 +1402,11 @@ __device__ __forceinline__ void collect_merge(const double* rec0, double* lvl, u
       return;
     }
     const int64_t up = fw_stats::merge_ceil(nodes, fw_stats::MERGE_FANIN);
-    pacc = 0;
     if (l < D) {
-      pub64(lvl + (1 + l) * up + g, mean, pacc);
-      pub64(lvl + (1 + D + l) * up + g, m2, pacc);
+      pub64(lvl + (1 + l) * up + g, mean);
+      pub64(lvl + (1 + D + l) * up + g, m2);
     }
-    if (l == 0) pub64(lvl + g, N, pacc);
+    if (l == 0) pub64(lvl + g, N);
     src = lvl;
     stride = up;
     lvl += up * (1 + 2 * COL_MAXD);
@@ -1317,7 +1447,6 @@ __device__ __forceinline__ void collect_epilogue(const State<T>& s, int64_t i, b
     }
     const unsigned long long rm = __ballot(row);
     const double nb = (double)__popcll(rm);
-    unsigned long long pacc = 0;  // returned words of this block's publications (pub64)
     __syncthreads();
     double* rec = s.col_rec + blockIdx.x;  // column-major: field q at rec[q * blocks] (coalesced merge reads)
     const int64_t qs = gridDim.x;
@@ -1348,8 +1477,8 @@ __device__ __forceinline__ void collect_epilogue(const State<T>& s, int64_t i, b
       q += __shfl_xor(q, 2);
       if (cv && p == 0) {
         if (tree) {
-          pub64(rec + (1 + col) * qs, mean, pacc);
-          pub64(rec + (1 + D + col) * qs, q, pacc);
+          pub64(rec + (1 + col) * qs, mean);
+          pub64(rec + (1 + D + col) * qs, q);
         } else {
           rec[(1 + col) * qs] = mean;
           rec[(1 + D + col) * qs] = q;
@@ -1358,13 +1487,13 @@ __device__ __forceinline__ void collect_epilogue(const State<T>& s, int64_t i, b
     }
     if (lane == 0) {
       if (tree)
-        pub64(rec, nb, pacc);
+        pub64(rec, nb);
       else
         rec[0] = nb;
     }
     if (tree) {
       __syncthreads();  // (the staging area is reused by the merge)
-      collect_merge(s.col_rec, s.col_lvl, s.col_cnt, s.col_merged, s.col_rms, D, ow, has_ret, mst, pacc);
+      collect_merge(s.col_rec, s.col_lvl, s.col_cnt, s.col_merged, s.col_rms, D, ow, has_ret, mst);
     }
   }
   if (s.col_ctrl && blockIdx.x == 0 && lane == 0) s.col_ctrl[0] += 1;  // the stream's next launch sees it
@@ -1396,7 +1525,7 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_env_step(const DevCfg<T>
   float* const col_x = (float*)col_base;
   double* const col_r = (double*)(col_base + 64 * COL_MAXD * sizeof(float));
   if (i < s.n)
-    env_step_lane<T, C, RP, Q, ((Q == 4 && (sizeof(T) == 4 || FW_PREF_Q4_F64)) || FW_PREF_Q1)>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out,
+    env_step_lane<T, C, RP, Q, ((Q == 4 && (sizeof(T) == 4 ? FW_PREF_Q4_F32 : FW_PREF_Q4_F64)) || FW_PREF_Q1)>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out,
                                                     episode_out, stats, auto_reset, (int)(tid % Q), ho);
   if (collect) {
     if (COL_ALIAS) __syncthreads();  // (one wave: orders the slot reuse after the integrator's last accesses)
@@ -1505,10 +1634,11 @@ struct fw_handle {
   void* met_out = nullptr;  // [FW_NMETRIC][N] done-episode records (fw_set_metrics_output)
   // offsets (bytes) of the SoA blocks inside base
   size_t o_y, o_der, o_wind, o_target, o_cmd, o_epret, o_act, o_cmdring, o_steps, o_goal, o_episode, o_life;
-  size_t o_met = 0, o_metu = 0;
+  size_t o_met = 0, o_metu = 0, o_metu16 = 0;
   int obs_hist = 0;         // past raw observation rows kept per env ((length - 1) * step + 2, 0 = none)
   size_t o_obs_init = 0, o_obs_ring = 0;
   size_t o_prm = 0;         // per-aircraft parameter rows (env->n_rand > 0 at create; 0 = none)
+  size_t o_dry = 0;         // Dryden filter-bank state rows (turbulence on at create; 0 = none)
   int rand_active = 0;      // the current config randomises parameters (kernels read the rows)
   int lanes_opt = FW_LANES_AUTO;  // fw_set_lanes: 0 = automatic, 1, 4
   int quad_ok = 1;          // the config allows the quad integrator (no wrapped ODE-state variable)
@@ -1632,12 +1762,33 @@ void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
     d.g1[k] = (T)s.dryden_g1[k];
   }
   d.noise_scale = (T)std::sqrt(3.141592653589793 / (double)d.turb_len);
+  d.dry_state = s.turbulence ? s.dryden_state : 0;
+  d.dry_ncut = s.dryden_ncut;
+  for (int k = 0; k < 28; k++) {
+    d.dry_ad[k] = (T)s.dryden_ad[k];
+    d.dry_e1[k] = (T)s.dryden_e1[k];
+  }
+  for (int k = 0; k < 12; k++) {
+    d.dry_b0[k] = (T)s.dryden_b0[k];
+    d.dry_b1[k] = (T)s.dryden_b1[k];
+    d.dry_c[k] = (T)s.dryden_c[k];
+  }
 
   d.has_env = h->has_env;
   d.act_window = h->act_window;
   d.cmd_window = h->cmd_window;
+  d.act_need = d.cmd_need = 0;
   if (h->has_env) {
     const fw_env_config& e = h->env;
+    // an env step reads previous action j for j < window (obs_raw / reward_of: entries 0 .. window - 1, entry 0
+    // the current action)
+    for (int o = 0; o < e.n_obs; o++)
+      if (e.obs[o].kind == FW_OBS_ACTION_WINDOW) {
+        if (e.scale_actions) d.act_need = std::max(d.act_need, e.obs[o].window - 1);
+        else d.cmd_need = std::max(d.cmd_need, e.obs[o].window - 1);
+      }
+    for (int r = 0; r < e.n_rew; r++)
+      if (e.rew[r].kind == FW_REW_ACTION_DELTA) d.act_need = std::max(d.act_need, e.rew[r].window - 1);
     d.steps_max = e.steps_max;
     d.n_obs = e.n_obs;
     d.scale_actions = e.scale_actions;
@@ -1703,6 +1854,8 @@ int validate(const fw_sim_config* s, const fw_env_config* e) {
     if (e->n_obs < 1 || e->n_obs > FW_MAX_OBS) return set_err(FW_E_INVALID, "n_obs out of range");
     if (e->n_rew < 0 || e->n_rew > FW_MAX_REW) return set_err(FW_E_INVALID, "n_rew out of range");
     if (e->steps_max > 65535) return set_err(FW_E_UNSUPPORTED, "steps_max > 65535");
+    if (e->metrics && (e->steps_max < 1 || e->steps_max > 65534))  // 16-bit entry indices, 0xFFFF = none
+      return set_err(FW_E_UNSUPPORTED, "episode metrics need 1 <= steps_max <= 65534");
     if (e->streak_req > 128) return set_err(FW_E_UNSUPPORTED, "success_streak_req > 128");
     if (e->obs_length < 0 || e->obs_length > FW_MAX_OBS_LEN || e->obs_step < 0 ||
         (e->obs_length > 1 && (e->obs_length - 1) * std::max(e->obs_step, 1) + 2 > FW_MAX_OBS_HIST))
@@ -1864,10 +2017,12 @@ State<T> state_of(const fw_handle* h) {
   s.env_offset = (uint32_t)h->env_offset;
   s.met = h->metrics ? (T*)(b + h->o_met) : nullptr;
   s.metu = h->metrics ? (uint32_t*)(b + h->o_metu) : nullptr;
+  s.metu16 = h->metrics ? (uint16_t*)(b + h->o_metu16) : nullptr;
   s.met_out = (T*)h->met_out;
   s.obs_init = h->obs_hist ? (T*)(b + h->o_obs_init) : nullptr;
   s.obs_ring = h->obs_hist ? (T*)(b + h->o_obs_ring) : nullptr;
   s.prm = h->o_prm ? (T*)(b + h->o_prm) : nullptr;
+  s.dry = (h->o_dry && h->sim.turbulence && h->sim.dryden_state) ? (T*)(b + h->o_dry) : nullptr;
   s.col_ret = h->col.ret;
   s.col_gamma = h->col.gamma;
   s.col_rec = h->col.records;
@@ -2005,6 +2160,10 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
   if (h->metrics) {
     h->o_met = off; off += (size_t)MT_ROWS * row;
     h->o_metu = off; off += (size_t)MU_ROWS * row32;
+    h->o_metu16 = off; off += (size_t)M16_ROWS * align_up((size_t)h->ld * 2, 256);
+  }
+  if (sim->turbulence) {  // Dryden filter-bank state (used when the chunk is too short for the FIR)
+    h->o_dry = off; off += (size_t)12 * row;
   }
   if (env && env->n_rand > 0) {  // per-aircraft parameters (simulator parameter randomisation)
     h->o_prm = off; off += (size_t)FW_NPARAM * row;
@@ -2120,6 +2279,8 @@ int fw_update_config(fw_handle* h, const fw_sim_config* sim, const fw_env_config
       return set_err(FW_E_UNSUPPORTED, "parameter randomisation must be enabled when the handle is created");
     h->env = *env;
   }
+  if (sim->turbulence && sim->dryden_state && !h->o_dry)
+    return set_err(FW_E_UNSUPPORTED, "turbulence must be enabled when the handle is created (Dryden filter state)");
   h->sim = *sim;
   FW_HIP(hipSetDevice(h->device));
   FW_HIP(hipDeviceSynchronize());

@@ -283,8 +283,20 @@ __device__ __forceinline__ bool rhs_quad(const C& c, const A& a, const QCtx<T>& 
   const T Va = ucond(c, FW_V_VA, Va_raw, key, 14);
   alpha = ucond(c, FW_V_ALPHA, alpha, key, 15);
   beta = ucond(c, FW_V_BETA, beta, key, 16);
-  const T rc = frcp(Q.r == 0 ? rxz : (l1 ? Va_raw : Va));  // 1 / rxz, 1 / Va_raw, 1 / Va on lanes 0, 1, 2
-  const T irxz = bc<0>(rc), iVr = bc<1>(rc), iVa = bc<2>(rc);
+  // 1 / rxz, 1 / Va_raw (, 1 / Va) on lanes 0, 1 (, 2).  A configuration that does not clip Va has Va ==
+  // Va_raw bit for bit, and the reciprocal is of this lane's own square root: no selects, one broadcast fewer
+  T irxz, iVr, iVa;
+  if (!((c.clipmask >> FW_V_VA) & 1u)) {  // (compile-time for the SpecCfg views)
+    const T rc = frcp(sq);
+    irxz = bc<0>(rc);
+    iVr = bc<1>(rc);
+    iVa = iVr;
+  } else {
+    const T rc = frcp(Q.r == 0 ? rxz : (l1 ? Va_raw : Va));
+    irxz = bc<0>(rc);
+    iVr = bc<1>(rc);
+    iVa = bc<2>(rc);
+  }
   T sa, ca, sb, cb;
   if (c.trig_alpha) {
     sa = sin(alpha);
@@ -302,15 +314,19 @@ __device__ __forceinline__ bool rhs_quad(const C& c, const A& a, const QCtx<T>& 
   }
   const T V2a = Va * Va;
   // lane 1: exp(M (alpha + a0)); the others: exp(-M (alpha - a0)) = exp(-M alpha + M a0)
-  T ex;
+  T ex, sigma;
   if constexpr (sizeof(T) == 4) {
+    // sigma = S / (S + C), S = 1 + e1 + e2, with ONE reciprocal: the exponent clamped at 2^120 keeps S + C
+    // finite and its reciprocal normal; where the clamp acts, C / S < 1e-15 and sigma rounds to 1 either way
     const T l2e = T(1.4426950408889634);
-    ex = __builtin_amdgcn_exp2f(fmaf(Q.sgn1 * (a.M * l2e), alpha, a.M * a.a0 * l2e));
+    ex = __builtin_amdgcn_exp2f(fminf(fmaf(Q.sgn1 * (a.M * l2e), alpha, a.M * a.a0 * l2e), T(120)));
+    const T S = T(1) + bc<0>(ex) + bc<1>(ex);
+    sigma = S * frcp(S + a.sig_c);
   } else {
     ex = fexp(l1 ? a.M * (alpha + a.a0) : -a.M * (alpha - a.a0));
+    const T ex1 = bc<0>(ex), ex2 = bc<1>(ex);
+    sigma = frcp(T(1) + a.sig_c * frcp(T(1) + ex1 + ex2));  // overflow-safe form, see rhs()
   }
-  const T ex1 = bc<0>(ex), ex2 = bc<1>(ex);
-  const T sigma = frcp(T(1) + a.sig_c * frcp(T(1) + ex1 + ex2));  // overflow-safe form, see rhs()
   const T osig = T(1) - sigma;
   // sgn(alpha) sin(alpha)^2 = sin(alpha) |sin(alpha)|: sin has alpha's sign on [-pi, pi] and the
   // product is 0 where it does not (pyfly.py:1547-1579 multiply by np.sign(alpha))
