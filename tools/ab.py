@@ -30,6 +30,8 @@ def run(names):
     names = names or sorted(f[:-3] for f in os.listdir(VDIR) if f.endswith(".so"))
     for nm in names:
         env = dict(os.environ, FWSIM_LIB=os.path.join(VDIR, nm + ".so"))
+        if nm == "default":  # the in-tree library
+            env.pop("FWSIM_LIB")
         r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "tail.py")], env=env, capture_output=True,
                            text=True, timeout=400)
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

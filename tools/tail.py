@@ -36,7 +36,7 @@ def step(a):
         eng.env_step(a, stats=True, auto_reset=(MODE == "env"))
 
 
-for s in range(20):
+for s in range(int(os.environ.get("TAIL_PREP", "20"))):  # (20: the round-2..4 protocol; 1000: steady state)
     step(pool[s % 16])
 torch.cuda.synchronize()
 ms, mx, p999, mean, wmax = [], [], [], [], []

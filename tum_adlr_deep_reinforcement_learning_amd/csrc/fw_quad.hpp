@@ -22,6 +22,13 @@
 // different order (rows before lanes), so results differ from the one-lane path by rounding.
 #pragma once
 
+#ifndef FW_QUAD_SIGMA_1RCP
+#define FW_QUAD_SIGMA_1RCP 1  // fp32 stall blend with one reciprocal (0: round 4's two; A/B)
+#endif
+#ifndef FW_QUAD_RC_NOSEL
+#define FW_QUAD_RC_NOSEL 1  // the front's reciprocals without lane selects when Va is not clipped (0: round 4; A/B)
+#endif
+
 namespace qd {
 
 // bound_ctrl set and no `old` operand: the form the backend's DPP combiner folds into a single-use
@@ -286,7 +293,7 @@ __device__ __forceinline__ bool rhs_quad(const C& c, const A& a, const QCtx<T>& 
   // 1 / rxz, 1 / Va_raw (, 1 / Va) on lanes 0, 1 (, 2).  A configuration that does not clip Va has Va ==
   // Va_raw bit for bit, and the reciprocal is of this lane's own square root: no selects, one broadcast fewer
   T irxz, iVr, iVa;
-  if (!((c.clipmask >> FW_V_VA) & 1u)) {  // (compile-time for the SpecCfg views)
+  if (FW_QUAD_RC_NOSEL && !((c.clipmask >> FW_V_VA) & 1u)) {  // (compile-time for the SpecCfg views)
     const T rc = frcp(sq);
     irxz = bc<0>(rc);
     iVr = bc<1>(rc);
@@ -315,13 +322,17 @@ __device__ __forceinline__ bool rhs_quad(const C& c, const A& a, const QCtx<T>& 
   const T V2a = Va * Va;
   // lane 1: exp(M (alpha + a0)); the others: exp(-M (alpha - a0)) = exp(-M alpha + M a0)
   T ex, sigma;
-  if constexpr (sizeof(T) == 4) {
+  if constexpr (sizeof(T) == 4 && FW_QUAD_SIGMA_1RCP) {
     // sigma = S / (S + C), S = 1 + e1 + e2, with ONE reciprocal: the exponent clamped at 2^120 keeps S + C
     // finite and its reciprocal normal; where the clamp acts, C / S < 1e-15 and sigma rounds to 1 either way
     const T l2e = T(1.4426950408889634);
     ex = __builtin_amdgcn_exp2f(fminf(fmaf(Q.sgn1 * (a.M * l2e), alpha, a.M * a.a0 * l2e), T(120)));
     const T S = T(1) + bc<0>(ex) + bc<1>(ex);
     sigma = S * frcp(S + a.sig_c);
+  } else if constexpr (sizeof(T) == 4) {  // (round 4: two reciprocals; A/B switch FW_QUAD_SIGMA_1RCP=0)
+    const T l2e = T(1.4426950408889634);
+    ex = __builtin_amdgcn_exp2f(fmaf(Q.sgn1 * (a.M * l2e), alpha, a.M * a.a0 * l2e));
+    sigma = frcp(T(1) + a.sig_c * frcp(T(1) + bc<0>(ex) + bc<1>(ex)));
   } else {
     ex = fexp(l1 ? a.M * (alpha + a.a0) : -a.M * (alpha - a.a0));
     const T ex1 = bc<0>(ex), ex2 = bc<1>(ex);

@@ -362,15 +362,37 @@ class FixedWingVecEnv(VecEnv):
             s, _ = self.engine.steps()
             s = s.cpu().numpy()
             return [int(s[i]) for i in idx]
+        if attr_name in ("scale_actions", "goal_enabled", "integration_window", "curriculum_level", "use_curriculum",
+                         "obs_norm"):
+            val = {"scale_actions": self.spec.scale_actions,
+                   "goal_enabled": self.spec.cfg["target"]["success_streak_req"] > 0,
+                   "integration_window": self.spec.cfg.get("integration_window", 0),
+                   "curriculum_level": getattr(self.spec, "curriculum_level", 1),
+                   "use_curriculum": True, "obs_norm": self.spec.cfg["observation"].get("normalize", False)}[attr_name]
+            return [val for _ in idx]
+        host = self._host_attrs()
+        if all(attr_name in host[i] for i in idx):  # set earlier by set_attr
+            return [host[i][attr_name] for i in idx]
         raise AttributeError("FixedWingVecEnv has no per-env attribute %r" % attr_name)
+
+    def _host_attrs(self):
+        """Per-env attributes set through set_attr that the device step does not read (a plain ``setattr`` on
+        the worker's FixedWingAircraft, subproc_vec_env.py:156-161): kept on the host, returned by get_attr."""
+        if getattr(self, "_hattrs", None) is None:
+            self._hattrs = [dict() for _ in range(self.num_envs)]
+        return self._hattrs
 
     def set_attr(self, attr_name, value, indices=None):
         """SubprocVecEnv.set_attr (subproc_vec_env.py:156-161: ``setattr(env, name, value)`` on each chosen
-        worker's FixedWingAircraft).  Settable here: ``training`` (the reference's callbacks,
-        train_rl_controller.py:320), ``target`` (a {"roll", "pitch", "Va"} dict, partial allowed: the
-        chosen envs track it from their next step), ``steps_count`` (their step counter) and ``steps_max``
-        (the episode limit of every env: one device configuration, so ``indices`` must cover all envs;
-        like the reference, the turbulence sequence length fixed at construction does not change)."""
+        worker's FixedWingAircraft).  Attributes the device step reads: ``training`` (the reference's
+        callbacks, train_rl_controller.py:320), ``target`` (a {"roll", "pitch", "Va"} dict, partial allowed:
+        the chosen envs track it from their next step), ``steps_count`` (their step counter), ``steps_max``
+        and ``curriculum_level`` (one device configuration, so ``indices`` must cover all envs; like the
+        reference, the turbulence sequence length fixed at construction does not change).  Configuration
+        attributes (cfg, spaces, simulator, ...) are refused: they are compiled into the device config.
+        Any other name is stored per env on the host and returned by get_attr, as a plain attribute of the
+        worker's env object would be (the device step never reads it); render_on_reset / save_on_reset may
+        be set False only (plotting is out of scope)."""
         idx = list(self._get_indices(indices))
         if attr_name == "training":
             self.training = value
@@ -393,9 +415,21 @@ class FixedWingVecEnv(VecEnv):
             self.spec.steps_max = int(value)
             self.engine.update_config(self.spec.sim, self.spec)
             return
-        if attr_name in ("render_on_reset", "save_on_reset"):
+        if attr_name in ("curriculum_level",):  # FixedWingAircraft.set_curriculum_level's state (fixed_wing.py:334)
+            if sorted(set(i % self.num_envs for i in idx)) != list(range(self.num_envs)):
+                raise NotImplementedError("curriculum_level is one device configuration: set it for all envs")
+            self.set_curriculum_level(value)
+            return
+        if attr_name in ("render_on_reset", "save_on_reset") and value:
             raise NotImplementedError("%s is host-side plotting; out of scope for the device engine" % attr_name)
-        raise AttributeError("setting %r is not supported on the device env" % attr_name)
+        if attr_name in ("cfg", "observation_space", "action_space", "simulator", "history", "scale_actions",
+                         "integration_window", "goal_enabled", "obs_norm"):
+            # attributes the reference reads while stepping: on the device they are the compiled configuration
+            raise AttributeError("setting %r would change the compiled device configuration: rebuild the env "
+                                 "(config_kw) or use update_config" % attr_name)
+        host = self._host_attrs()  # any other attribute: the device step does not read it (e.g. a callback's flag)
+        for i in idx:
+            host[i][attr_name] = value
 
     def env_method(self, method_name, *method_args, indices=None, **method_kwargs):
         idx = list(self._get_indices(indices))
