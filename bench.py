@@ -78,13 +78,14 @@ def algorithmic_bytes_per_env_step(spec, esz=4):
     wr = (19 + 8 + tgt_var + 3 + 3 + 1 + spec.n_obs + 1) * esz + (1 + 4 + 1 + 1) * 4 + 1
     if spec.cfg.get("metrics") and spec.metrics_enabled:
         # streaming episode metrics, packed (round 5; csrc/fw_kernels.hip Met): previous command 3, control
-        # variation 1, e0 / sum / |sum| / overshoot extremum x3, the ring's previous error x3 (T); the goal-buffer
-        # words holding the new and the leaving status x3 + the window counts (u32); entry count, goal counts,
-        # settling x4, rise crossings x6 (u16).  Written: control variation, sum / |sum| x3, ring entry x3 (T); the
-        # new-status words x3 + the counts (u32); the entry count (u16).  Rows that change now and then (extrema,
+        # variation 1, e0 / sum / |sum| / overshoot extremum / end-window sum x3, the ring's previous error and the
+        # entry the new error overwrites x3 each (T); the goal-buffer words holding the new and the leaving status
+        # x3 + the window counts (u32); entry count, goal counts, settling x4, rise crossings x6 (u16).  Written:
+        # control variation, sum / |sum| / window sum x3, ring entry x3 (T); the new-status words x3 + the counts
+        # (u32); the entry count (u16).  Rows that change now and then (extrema,
         # goal counts, settling and rise indices) are stored only when a lane changed them and are not counted.
-        rd += (3 + 1 + 12 + 3) * esz + (6 + 1) * 4 + 15 * 2
-        wr += (1 + 6 + 3) * esz + (3 + 1) * 4 + 1 * 2
+        rd += (3 + 1 + 15 + 3 + 3) * esz + (6 + 1) * 4 + 15 * 2
+        wr += (1 + 9 + 3) * esz + (3 + 1) * 4 + 1 * 2
     return rd, wr
 
 

@@ -130,10 +130,12 @@ struct State {
 };
 
 // streaming episode-metric state (fixed_wing.py:1644-1736 restated over running sums), packed (round 5):
-// T rows: e0, sum, |sum|, the extremum overshoot reads (the minimum where e0 > 0, else the maximum) (x3 targets),
-// control variation, ring of the last FW_M_END_WINDOW errors.  Not kept: the previous error (the ring's previous
-// entry) and the end-error window sum (summed from the ring when the episode ends).
-constexpr int MR_E0 = 0, MR_ESUM = 3, MR_EABS = 6, MR_EXT = 9, MR_CV = 12, MR_RING = 13;
+// T rows: e0, sum, |sum|, the extremum overshoot reads (the minimum where e0 > 0, else the maximum), the sum of
+// the last FW_M_END_WINDOW errors (x3 targets), control variation, ring of the last FW_M_END_WINDOW errors.  Not
+// kept: the previous error (the ring's previous entry).  The window sum stays streaming (+ the new error - the
+// one it overwrites in the ring): summed from the ring when the episode ends, the 150 scattered loads of every
+// done aircraft put ~16 us on the steady-state launch (long-window median 0.080 -> 0.096 ms, tools/r05_longwin_ab.sh).
+constexpr int MR_E0 = 0, MR_ESUM = 3, MR_EABS = 6, MR_EXT = 9, MR_WSUM = 12, MR_CV = 15, MR_RING = 16;
 constexpr int MT_ROWS = MR_RING + 3 * FW_M_END_WINDOW;
 // uint32 rows: per target (roll / pitch / Va) a 128-bit circular buffer of goal statuses indexed by the LIFETIME
 // step (entry e of the episode at bit (lep + e) % 128: every lane of a wave touches the same word rows), and the
@@ -547,6 +549,7 @@ __device__ __forceinline__ void metrics_init(const DevCfg<T>& c, const State<T>&
     st_(s.met, MR_ESUM + k, ld, i, err);
     st_(s.met, MR_EABS + k, ld, i, T(fabs(err)));
     st_(s.met, MR_EXT + k, ld, i, err);
+    st_(s.met, MR_WSUM + k, ld, i, err);
     st_(s.met, MR_RING + 3 * slot0 + k, ld, i, err);
   }
   st_(s.met, MR_CV, ld, i, T(0));
@@ -581,6 +584,7 @@ struct Met {
   uint32_t u[M16_ROWS];    // count, goal counts, settling, rise (uint16 rows)
   uint32_t cnt;            // window counts, one byte per target
   T prev[3];               // the previous entry's errors (ring)
+  T old[3];                // the ring entries the new error overwrites (leaving the end-error window)
   uint32_t gw_new[3], gw_old[3];  // goal-buffer words holding the new entry's bit / the leaving entry's bit
   uint32_t b;              // the entry index the loads assumed (steps0 + 1)
   // rows that change only now and then (the extrema, goal counts, settling and rise indices): a set
@@ -592,8 +596,12 @@ struct Met {
   // episode's first `life`, the same on every lane for the same e: coalesced rows)
   __device__ __forceinline__ void fetch_entry(const DevCfg<T>& c, const State<T>& s, int64_t i, uint32_t lep) {
     const int ps = (int)((lep + b - 1u) % (uint32_t)FW_M_END_WINDOW);
+    const int ns = (int)((lep + b) % (uint32_t)FW_M_END_WINDOW);
 #pragma unroll
-    for (int k = 0; k < 3; k++) prev[k] = ld_(s.met, MR_RING + 3 * ps + k, s.ld, i);
+    for (int k = 0; k < 3; k++) {
+      prev[k] = ld_(s.met, MR_RING + 3 * ps + k, s.ld, i);
+      old[k] = ld_(s.met, MR_RING + 3 * ns + k, s.ld, i);
+    }
     const uint32_t pn = lep + b, po = pn - (uint32_t)(c.streak_req > 0 ? c.streak_req : 0);
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -651,6 +659,7 @@ __device__ __forceinline__ void metrics_step(const DevCfg<T>& c, const State<T>&
       if (bits_differ(x, M.row[MR_EXT + k])) M.dirty |= 1u << (MD_EXT + k);
       M.row[MR_EXT + k] = x;
     }
+    M.row[MR_WSUM + k] += n0 >= (uint32_t)FW_M_END_WINDOW ? err - M.old[k] : err;
     st_(s.met, MR_RING + 3 * slot + k, s.ld, i, err);
     // rise_time: earliest downward crossing of |error| through each limit
     const T lims[2] = {T(fabs(c.rise_high * e0)), T(fabs(c.rise_low * e0))};
@@ -691,20 +700,13 @@ __device__ __forceinline__ void metrics_step(const DevCfg<T>& c, const State<T>&
 }
 
 // the record of a done episode (get_metric for every cfg metric), layout FW_M_* of fwsim.h
-// out: column of the SoA record [FW_NMETRIC][N] (element m at out[m * stride]).  end_error sums the ring's
-// last min(n, FW_M_END_WINDOW) entries oldest first (np.mean(v[-50:]), fixed_wing.py:1665-1668).
+// out: column of the SoA record [FW_NMETRIC][N] (element m at out[m * stride]).
 template <typename T>
-__device__ __forceinline__ void metrics_final(const DevCfg<T>& c, const State<T>& s, int64_t i, const Met<T>& M,
-                                              uint32_t lep, int n_commands, T* out, int64_t stride) {
+__device__ __forceinline__ void metrics_final(const DevCfg<T>& c, const Met<T>& M, int n_commands, T* out,
+                                              int64_t stride) {
   const T nan = T(NAN);
   const uint32_t n = M.u[M16_N];
   const int cnt = n < (uint32_t)FW_M_END_WINDOW ? (int)n : FW_M_END_WINDOW;
-  T wsum[3] = {T(0), T(0), T(0)};
-  for (int e = (int)n - cnt; e < (int)n; e++) {
-    const int sl = (int)((lep + (uint32_t)e) % (uint32_t)FW_M_END_WINDOW);
-#pragma unroll
-    for (int k = 0; k < 3; k++) wsum[k] += ld_(s.met, MR_RING + 3 * sl + k, s.ld, i);
-  }
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     const T e0 = M.row[MR_E0 + k];
@@ -714,7 +716,7 @@ __device__ __forceinline__ void metrics_final(const DevCfg<T>& c, const State<T>
     out[(FW_M_OVERSHOOT + k) * stride] = sgn(m) == sgn(e0) ? nan : T(fabs(m / e0));
     out[(FW_M_TOTAL_ERROR + k) * stride] = M.row[MR_EABS + k];
     out[(FW_M_AVG_ERROR + k) * stride] = fabs(e0) >= T(0.01) ? T(fabs(M.row[MR_ESUM + k] / (T)n / e0)) : nan;
-    out[(FW_M_END_ERROR + k) * stride] = T(fabs(wsum[k] / (T)cnt));
+    out[(FW_M_END_ERROR + k) * stride] = T(fabs(M.row[MR_WSUM + k] / (T)cnt));
   }
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -1216,7 +1218,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
     M.store(s, i);
 #endif
 #ifndef FW_MET_SKIP_FINAL
-    if (done && s.met_out) metrics_final(c, s, i, M, lep, steps, s.met_out + i, s.n);
+    if (done && s.met_out) metrics_final(c, M, steps, s.met_out + i, s.n);
 #endif
   }
   FW_TSTAMP(3);
