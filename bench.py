@@ -54,12 +54,14 @@ def algorithmic_bytes_per_env_step(spec, esz=4):
 
     reads : ODE state 19, elevator/aileron 2, steady wind 3, targets 3, action 3,
             the previous actions the step reads (act_need*3: window - 1), ep_return 1   -> T
-            steps word, goal history 4 words, life word (+ episode word with turbulence
-            or observation noise: the Philox key)                                       -> u32
+            steps word, life word (+ episode word with turbulence or observation noise:
+            the Philox key); goal history (success_streak_req > 0, round 5): the ring
+            words of the new and of the leaving entry, the window counts, the entry count -> u32
     writes: ODE state 19, derived 8, the targets that can change (compensate class; a
             constant-class row is stored only when some lane changed it), ring slot 3,
             last command 3, ep_return 1, observation n_obs, reward 1                    -> T
-            steps word, goal history 4 words, term code, life word                      -> u32
+            steps word, term code, life word; goal history: the new entry's ring word,
+            the counts, the entry count                                                 -> u32
             done flag                                                                   -> u8
     (life: the lifetime step counter the ring slots are indexed by, round 4.)  Not counted: the kernel's
     deliberate re-reads after the RK loop (pre-step state 19, targets 3, actions 3 -- held across the
@@ -74,18 +76,22 @@ def algorithmic_bytes_per_env_step(spec, esz=4):
             act_need = max(act_need, int(f["window_size"]) - 1)
     tgt_var = sum(1 for t in spec.cfg["target"]["states"] if t.get("class", "constant") != "constant")
     philox = bool(spec.sim.cfg.get("turbulence")) or bool(spec.obs_noise)
-    rd = (19 + 2 + 3 + 3 + 3 + act_need * 3 + 1) * esz + (1 + 4 + 1 + (1 if philox else 0)) * 4
-    wr = (19 + 8 + tgt_var + 3 + 3 + 1 + spec.n_obs + 1) * esz + (1 + 4 + 1 + 1) * 4 + 1
-    if spec.cfg.get("metrics") and spec.metrics_enabled:
-        # streaming episode metrics, packed (round 5; csrc/fw_kernels.hip Met): previous command 3, control
-        # variation 1, e0 / sum / |sum| / overshoot extremum / end-window sum x3, the ring's previous error and the
-        # entry the new error overwrites x3 each (T); the goal-buffer words holding the new and the leaving status
-        # x3 + the window counts (u32); entry count, goal counts, settling x4, rise crossings x6 (u16).  Written:
-        # control variation, sum / |sum| / window sum x3, ring entry x3 (T); the new-status words x3 + the counts
-        # (u32); the entry count (u16).  Rows that change now and then (extrema,
-        # goal counts, settling and rise indices) are stored only when a lane changed them and are not counted.
-        rd += (3 + 1 + 15 + 3 + 3) * esz + (6 + 1) * 4 + 15 * 2
-        wr += (1 + 9 + 3) * esz + (3 + 1) * 4 + 1 * 2
+    metrics = bool(spec.cfg.get("metrics") and spec.metrics_enabled)
+    goal = int(spec.cfg["target"].get("success_streak_req", 0)) > 0
+    rd = (19 + 2 + 3 + 3 + 3 + act_need * 3 + 1) * esz + (1 + 1 + (1 if philox else 0)) * 4
+    wr = (19 + 8 + tgt_var + 3 + 3 + 1 + spec.n_obs + 1) * esz + (1 + 1 + 1) * 4 + 1
+    rd += (4 if goal else 1 if metrics else 0) * 4
+    wr += (3 if goal else 1 if metrics else 0) * 4
+    if metrics:
+        # streaming episode metrics, packed (round 5; csrc/fw_kernels.hip Met): previous command 3 (recomputed
+        # from the previous action when the action ring delivers it), control variation 1, e0 / sum / |sum| /
+        # overshoot extremum / end-window sum x3, the ring's previous error and the entry the new error overwrites
+        # x3 each (T); goal counts, settling x4, rise crossings x6 (u16).  Written: control variation, sum / |sum| /
+        # window sum x3, ring entry x3 (T).  The goal statuses and the entry count are the goal history's (above).
+        # Rows that change now and then (extrema, goal counts, settling and rise indices) are stored only when a
+        # lane changed them and are not counted.
+        rd += ((0 if act_need >= 1 else 3) + 1 + 15 + 3 + 3) * esz + 14 * 2
+        wr += (1 + 9 + 3) * esz
     return rd, wr
 
 

@@ -279,7 +279,9 @@ enum fw_init_field {
                                aircraft whose episodes started at different steps, so a wave's ring accesses
                                coalesce) and the two calls translate */
 #define FW_BLK_CMD_RING 8   /* window*3 rows, T: constrained commands, same layout (unscaled action windows) */
-#define FW_BLK_GOAL 9       /* 4 rows, uint32: the last 128 goal-status bits ("all"), bit 0 of row 0 newest */
+#define FW_BLK_GOAL 9       /* 4 rows, uint32: the last 128 goal-status bits ("all"), bit 0 of row 0 newest (0 before
+                             * the episode's first entry).  Env handles only.  Setting it takes the episode's
+                             * history length from FW_BLK_STEPS (steps_count + 1 entries): set FW_BLK_STEPS first */
 #define FW_NBLK 10
 
 typedef struct fw_handle fw_handle;

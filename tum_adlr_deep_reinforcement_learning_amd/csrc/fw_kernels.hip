@@ -101,10 +101,12 @@ struct State {
   T* act_ring;     // [act_window][3][ld], action k of an episode in slot (L_ep + k - 1) % act_window
   T* cmd_ring;     // [cmd_window][3][ld] or null, the same slots
   uint32_t* steps;    // [ld]: steps_count | steps_for_current_target << 16
-  uint32_t* goal;     // [4][ld] 128-bit goal history shift register (bit 0 newest)
+  uint32_t* goal;     // [GB_ROWS][ld] goal-status history: nibble ring, window counts, entry count (below)
   uint32_t* episode;  // [ld]
-  uint32_t* life;     // [ld] env steps since the handle was created (never reset): every launch steps every
-                      // aircraft, so the value is the same on all lanes -- ring slots are indexed by it (below)
+  uint32_t* life;     // [ld] LIFE0 + env steps since the handle was created (never reset): every launch steps
+                      // every aircraft, so the value is the same on all lanes -- ring slots are indexed by it
+                      // (below).  Starting at LIFE0 >= 2^16 + any window keeps life - steps_count - window > 0
+                      // whatever FW_BLK_STEPS a caller sets, so no slot expression wraps below 0.
   T* dry;             // [12][ld] Dryden filter-bank state of the current step (short chunks; null: FIR or off)
   const T* noise;     // injected N(0,1) turbulence noise [4][noise_len][ld] or null
   int64_t noise_len;
@@ -112,7 +114,6 @@ struct State {
   uint32_t key0, key1;  // Philox key = seed
   uint32_t env_offset;
   T* met;             // [MT_ROWS][ld] streaming episode-metric sums (null: metrics off)
-  uint32_t* metu;     // [MU_ROWS][ld] goal-status buffers and window counts
   uint16_t* metu16;   // [M16_ROWS][ld] counters / indices
   T* met_out;         // [FW_NMETRIC][N] (SoA) record of done envs (null: not requested)
   T* obs_init;        // [n_obs][ld] raw observation row at the episode's reset (null: length-1 observations)
@@ -137,16 +138,27 @@ struct State {
 // done aircraft put ~16 us on the steady-state launch (long-window median 0.080 -> 0.096 ms, tools/r05_longwin_ab.sh).
 constexpr int MR_E0 = 0, MR_ESUM = 3, MR_EABS = 6, MR_EXT = 9, MR_WSUM = 12, MR_CV = 15, MR_RING = 16;
 constexpr int MT_ROWS = MR_RING + 3 * FW_M_END_WINDOW;
-// uint32 rows: per target (roll / pitch / Va) a 128-bit circular buffer of goal statuses indexed by the LIFETIME
-// step (entry e of the episode at bit (lep + e) % 128: every lane of a wave touches the same word rows), and the
-// three window counts (ones among the last success_streak_req entries) as bytes of one word
-constexpr int MU_GB = 0, MU_CNT = 12;
-constexpr int MU_ROWS = MU_CNT + 1;
-// uint16 rows: entry count, goal counts (4), settling index (4, 0xFFFF = none), first crossings below the high /
-// low rise limits (3 x 2)
-constexpr int M16_N = 0, M16_GC = 1, M16_SET = 5, M16_RISE = 9;
+// uint16 rows: goal counts (4), settling index (4, 0xFFFF = none), first crossings below the high / low rise
+// limits (3 x 2)
+constexpr int M16_GC = 0, M16_SET = 4, M16_RISE = 8;
 constexpr int M16_ROWS = M16_RISE + 6;
 constexpr uint32_t M_NONE = 0xFFFFu;
+// goal-status history of the env (round 5; s.goal, uint32 rows).  The history entry e of the episode (0 = the
+// reset state, one entry per successful step, fixed_wing.py:462-466, 536-538) keeps its four statuses
+// (goal_status_bits: roll / pitch / Va within bound, all) in nibble (lep + e) % 8 of ring word ((lep + e) % 128) / 8
+// -- indexed by the LIFETIME position, so every lane of a wave touches the same word row.  GB_CNT holds the ones
+// among the last success_streak_req entries per status (one byte each, "all" in byte 3), GB_N the entry count.
+// A step reads the word the new entry goes to, the word holding the entry that leaves the window, the counts and
+// the entry count (16 B) and writes three of them back: the 128-bit shift register of rounds 1-4 plus the
+// metrics' per-target bit buffers moved 76 B per step.
+constexpr int GB_RING = 0, GB_CNT = 16, GB_N = 17, GB_ROWS = 18;
+constexpr uint32_t LIFE0 = 1u << 20;  // State::life at handle creation
+__device__ __forceinline__ int gring_row(uint32_t pos) { return GB_RING + (int)((pos & 127u) >> 3); }
+__device__ __forceinline__ uint32_t gring_get(uint32_t w, uint32_t pos) { return (w >> (4u * (pos & 7u))) & 0xFu; }
+__device__ __forceinline__ uint32_t gring_set(uint32_t w, uint32_t pos, uint32_t nib) {
+  const uint32_t sh = 4u * (pos & 7u);
+  return (w & ~(0xFu << sh)) | (nib << sh);
+}
 constexpr int MD_EXT = 0, MD_U = 3;  // Met::dirty bits: 3 extremum rows, then the M16_ROWS - M16_GC rare u16 rows
 static_assert(MD_U + (M16_ROWS - M16_GC) <= 32, "Met::dirty holds one bit per rarely-changing row");
 
@@ -505,22 +517,6 @@ __device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* 
 // aircraft here (history["error"] / ["goal"] entry 0 = the reset state, one entry
 // per successful step; one command per step).
 // ---------------------------------------------------------------------------
-// success / settling_time: the deque of the last `req` statuses is full and its mean >= frac
-template <typename T>
-__device__ __forceinline__ bool settled(const DevCfg<T>& c, const uint32_t g[4], uint32_t n) {
-  const int req = c.streak_req;
-  if (req <= 0 || (int64_t)n < req) return false;
-  int cnt = 0, rem = req;
-#pragma unroll
-  for (int w = 0; w < 4; w++) {
-    const int take = rem >= 32 ? 32 : (rem > 0 ? rem : 0);
-    const uint32_t m = take == 32 ? 0xFFFFFFFFu : ((1u << take) - 1u);
-    cnt += __builtin_popcount(g[w] & m);
-    rem -= take;
-  }
-  return (double)cnt / (double)req >= (double)c.streak_frac;
-}
-
 // the deque condition of success / settling_time from a window count: `n` entries so far, `cnt` ones among
 // the last success_streak_req of them
 template <typename T>
@@ -529,19 +525,12 @@ __device__ __forceinline__ bool settled_n(const DevCfg<T>& c, uint32_t cnt, uint
   return req > 0 && (int64_t)n >= req && (double)cnt / (double)req >= (double)c.streak_frac;
 }
 
-// bit `pos` (0..127) of target k's goal-status buffer lives in word row MU_GB + 4 k + pos / 32
-__device__ __forceinline__ int gb_row(int k, uint32_t pos) { return MU_GB + 4 * k + (int)((pos & 127u) >> 5); }
-__device__ __forceinline__ uint32_t gb_set(uint32_t w, uint32_t pos, uint32_t bit) {
-  const uint32_t m = 1u << (pos & 31u);
-  return (w & ~m) | (bit ? m : 0u);
-}
-
 template <typename T>
 __device__ __forceinline__ void metrics_init(const DevCfg<T>& c, const State<T>& s, int64_t i, const T* tgt,
                                              const T* vals, uint32_t lep) {
   const int slot0 = (int)(lep % (uint32_t)FW_M_END_WINDOW);  // entry 0 of the episode
   const int64_t ld = s.ld;
-  const uint32_t gb = goal_status_bits(c, tgt, vals);
+  const uint32_t gb = goal_status_bits(c, tgt, vals);  // (the goal history itself: goal_init)
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     const T err = target_error(c, k, tgt[k], vals[k]);
@@ -553,20 +542,12 @@ __device__ __forceinline__ void metrics_init(const DevCfg<T>& c, const State<T>&
     st_(s.met, MR_RING + 3 * slot0 + k, ld, i, err);
   }
   st_(s.met, MR_CV, ld, i, T(0));
-  st_(s.metu16, M16_N, ld, i, (uint16_t)1);
-  uint32_t cnt = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const uint32_t bit = (gb >> k) & 1u;
-    if (k < 3) {  // entry 0 of the buffer; the other bits belong to earlier episodes and are never counted
-      const int row = gb_row(k, lep);
-      st_(s.metu, row, ld, i, gb_set(ld_(s.metu, row, ld, i), lep, bit));
-      cnt |= bit << (8 * k);
-    }
     st_(s.metu16, M16_GC + k, ld, i, (uint16_t)bit);
     st_(s.metu16, M16_SET + k, ld, i, (uint16_t)(settled_n(c, bit, 1u) ? 0u : M_NONE));
   }
-  st_(s.metu, MU_CNT, ld, i, cnt);
 #pragma unroll
   for (int r = 0; r < 6; r++) st_(s.metu16, M16_RISE + r, ld, i, (uint16_t)M_NONE);
 }
@@ -581,20 +562,17 @@ __device__ __forceinline__ bool bits_differ(double a, double b) {
 template <typename T>
 struct Met {
   T row[MR_RING];          // e0 / sum / |sum| / extremum (x3), cv
-  uint32_t u[M16_ROWS];    // count, goal counts, settling, rise (uint16 rows)
-  uint32_t cnt;            // window counts, one byte per target
+  uint32_t u[M16_ROWS];    // goal counts, settling, rise (uint16 rows)
   T prev[3];               // the previous entry's errors (ring)
   T old[3];                // the ring entries the new error overwrites (leaving the end-error window)
-  uint32_t gw_new[3], gw_old[3];  // goal-buffer words holding the new entry's bit / the leaving entry's bit
-  uint32_t b;              // the entry index the loads assumed (steps0 + 1)
+  uint32_t b;              // the entry index the loads assumed
   // rows that change only now and then (the extrema, goal counts, settling and rise indices): a set
   // bit k marks row MD_* k as changed in this lane; store() writes such a row when some lane of the wave
   // changed it (whole-row coalesced stores), so a steady step writes the rows the traffic accounting counts
   uint32_t dirty;
-  // within an episode every step but a terminal failure appends an entry, so the new entry's index is
-  // steps0 + 1; entry e lives in ring slot (lep + e) % FW_M_END_WINDOW and goal bit (lep + e) % 128 (lep = the
-  // episode's first `life`, the same on every lane for the same e: coalesced rows)
-  __device__ __forceinline__ void fetch_entry(const DevCfg<T>& c, const State<T>& s, int64_t i, uint32_t lep) {
+  // entry e lives in ring slot (lep + e) % FW_M_END_WINDOW (lep = the episode's first `life`, the same on every
+  // lane for the same e: coalesced rows)
+  __device__ __forceinline__ void fetch_entry(const State<T>& s, int64_t i, uint32_t lep) {
     const int ps = (int)((lep + b - 1u) % (uint32_t)FW_M_END_WINDOW);
     const int ns = (int)((lep + b) % (uint32_t)FW_M_END_WINDOW);
 #pragma unroll
@@ -602,22 +580,16 @@ struct Met {
       prev[k] = ld_(s.met, MR_RING + 3 * ps + k, s.ld, i);
       old[k] = ld_(s.met, MR_RING + 3 * ns + k, s.ld, i);
     }
-    const uint32_t pn = lep + b, po = pn - (uint32_t)(c.streak_req > 0 ? c.streak_req : 0);
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      gw_new[k] = ld_(s.metu, gb_row(k, pn), s.ld, i);
-      gw_old[k] = ld_(s.metu, gb_row(k, po), s.ld, i);
-    }
   }
-  __device__ __forceinline__ void load(const DevCfg<T>& c, const State<T>& s, int64_t i, uint32_t lep, int steps0) {
+  // b_guess: the new entry's index as the goal history assumes it (GoalHist)
+  __device__ __forceinline__ void load(const State<T>& s, int64_t i, uint32_t lep, uint32_t b_guess) {
 #pragma unroll
     for (int r = 0; r < MR_RING; r++) row[r] = ld_(s.met, r, s.ld, i);
 #pragma unroll
     for (int r = 0; r < M16_ROWS; r++) u[r] = ld_(s.metu16, r, s.ld, i);
-    cnt = ld_(s.metu, MU_CNT, s.ld, i);
-    b = (uint32_t)steps0 + 1u;
+    b = b_guess;
     dirty = 0u;
-    fetch_entry(c, s, i, lep);
+    fetch_entry(s, i, lep);
   }
   __device__ __forceinline__ void store(const State<T>& s, int64_t i) const {
     // MR_E0 (the episode's initial errors) never changes after metrics_init: not written back
@@ -628,24 +600,23 @@ struct Met {
     }
 #pragma unroll
     for (int r = 0; r < M16_ROWS; r++) {
-      const bool rare = r >= M16_GC;  // goal counts, settling, rise indices
-      if (!rare || __ballot((dirty >> (MD_U + r - M16_GC)) & 1u)) st_(s.metu16, r, s.ld, i, (uint16_t)u[r]);
+      // goal counts, settling, rise indices: all rows change only now and then
+      if (__ballot((dirty >> (MD_U + r - M16_GC)) & 1u)) st_(s.metu16, r, s.ld, i, (uint16_t)u[r]);
     }
-    st_(s.metu, MU_CNT, s.ld, i, cnt);
   }
 };
 
-// one successful step: errors w.r.t. the NEW targets (fixed_wing.py:575-579), goal statuses
-// `gb` w.r.t. the old ones (:534-537); gall = the updated "all" register.  Writes the new
-// error into the end-error ring and the new goal bits into the goal buffers.
+// one successful step appending history entry b: errors w.r.t. the NEW targets (fixed_wing.py:575-579), goal
+// statuses `gb` w.r.t. the old ones (:534-537); gcnt = the goal history's window counts with entry b included.
+// Writes the new error into the end-error ring.
 template <typename T>
 __device__ __forceinline__ void metrics_step(const DevCfg<T>& c, const State<T>& s, int64_t i, Met<T>& M,
-                                             const T* tgt, const T* vals, uint32_t gb, const uint32_t gall[4],
+                                             const T* tgt, const T* vals, uint32_t gb, uint32_t gcnt, uint32_t b,
                                              uint32_t lep) {
-  const uint32_t n0 = M.u[M16_N], b = n0;  // index of the new history entry
+  const uint32_t n0 = b;  // entries before this one
   if (b != M.b) {  // stepping on after a failed (done) step without reset: the entry's slots moved
     M.b = b;
-    M.fetch_entry(c, s, i, lep);
+    M.fetch_entry(s, i, lep);
   }
   const int slot = (int)((lep + b) % (uint32_t)FW_M_END_WINDOW);
 #pragma unroll
@@ -673,21 +644,10 @@ __device__ __forceinline__ void metrics_step(const DevCfg<T>& c, const State<T>&
     }
   }
   if (c.streak_req > 0) {
-    const uint32_t pn = lep + b, po = pn - (uint32_t)c.streak_req;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t bit = (gb >> k) & 1u;
-      bool set;
-      if (k < 3) {  // the window count: + the new status, - the one leaving the req-deep window
-        uint32_t ck = (M.cnt >> (8 * k)) & 0xFFu;
-        if (b >= (uint32_t)c.streak_req) ck -= (M.gw_old[k] >> (po & 31u)) & 1u;
-        ck += bit;
-        M.cnt = (M.cnt & ~(0xFFu << (8 * k))) | (ck << (8 * k));
-        st_(s.metu, gb_row(k, pn), s.ld, i, gb_set(M.gw_new[k], pn, bit));
-        set = settled_n(c, ck, n0 + 1u);
-      } else {
-        set = settled(c, gall, n0 + 1u);
-      }
+      const bool set = settled_n(c, (gcnt >> (8 * k)) & 0xFFu, n0 + 1u);
       M.u[M16_GC + k] += bit;
       M.dirty |= bit << (MD_U + k);
       if (M.u[M16_SET + k] == M_NONE && set) {
@@ -696,16 +656,14 @@ __device__ __forceinline__ void metrics_step(const DevCfg<T>& c, const State<T>&
       }
     }
   }
-  M.u[M16_N] = n0 + 1u;
 }
 
 // the record of a done episode (get_metric for every cfg metric), layout FW_M_* of fwsim.h
-// out: column of the SoA record [FW_NMETRIC][N] (element m at out[m * stride]).
+// n: the history entries; out: column of the SoA record [FW_NMETRIC][N] (element m at out[m * stride]).
 template <typename T>
-__device__ __forceinline__ void metrics_final(const DevCfg<T>& c, const Met<T>& M, int n_commands, T* out,
+__device__ __forceinline__ void metrics_final(const DevCfg<T>& c, const Met<T>& M, uint32_t n, int n_commands, T* out,
                                               int64_t stride) {
   const T nan = T(NAN);
-  const uint32_t n = M.u[M16_N];
   const int cnt = n < (uint32_t)FW_M_END_WINDOW ? (int)n : FW_M_END_WINDOW;
 #pragma unroll
   for (int k = 0; k < 3; k++) {
@@ -852,9 +810,26 @@ __device__ __forceinline__ void load_row(const T* p, int rows, int64_t ld, int64
   for (int r = 0; r < rows; r++) dst[r] = p[r * ld + i];
 }
 
+// the goal history of a fresh episode: entry 0 (the reset state) at lifetime position lep.  The other nibbles of
+// its word are entries of an earlier episode or ones this episode writes before reading: a plain store, no
+// read-modify-write.
+template <typename T>
+__device__ __forceinline__ void goal_init(const DevCfg<T>& c, const State<T>& s, int64_t i, const T* tgt,
+                                          const T* der, uint32_t lep) {
+  const int64_t ld = s.ld;
+  if (c.streak_req > 0) {
+    const T vals[3] = {der[0], der[1], der[3]};
+    const uint32_t gb = goal_status_bits(c, tgt, vals);
+    st_(s.goal, gring_row(lep), ld, i, gring_set(0u, lep, gb));
+    st_(s.goal, GB_CNT, ld, i, (gb & 1u) | ((gb >> 1) & 1u) << 8 | ((gb >> 2) & 1u) << 16 | ((gb >> 3) & 1u) << 24);
+  }
+  st_(s.goal, GB_N, ld, i, 1u);
+}
+
+// lep: the fresh episode's first `life`
 template <typename T>
 __device__ __forceinline__ void store_env_fresh(const DevCfg<T>& c, const State<T>& s, int64_t i, const T* y, const T* der,
-                                                const T* wind, const T* tgt) {
+                                                const T* wind, const T* tgt, uint32_t lep) {
   const int64_t ld = s.ld;
 #pragma unroll
   for (int k = 0; k < NY; k++) st_(s.y, k, ld, i, y[k]);
@@ -868,12 +843,7 @@ __device__ __forceinline__ void store_env_fresh(const DevCfg<T>& c, const State<
   if (c.has_env) {
 #pragma unroll
     for (int k = 0; k < 3; k++) st_(s.target, k, ld, i, tgt[k]);
-    const T vals[3] = {der[0], der[1], der[3]};
-    const uint32_t g0 = goal_all(c, tgt, vals) ? 1u : 0u;
-    st_(s.goal, 0, ld, i, g0);
-    st_(s.goal, 1, ld, i, 0u);
-    st_(s.goal, 2, ld, i, 0u);
-    st_(s.goal, 3, ld, i, 0u);
+    goal_init(c, s, i, tgt, der, lep);
     st_(s.ep_ret, 0, ld, i, T(0));
   }
   s.steps[i] = 0u;
@@ -892,7 +862,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(const DevCfg<T>* __restrict__ c
   const DevCfg<T>& c = *cfgp;
   T y[NY], der[8], wind[3], tgt[3] = {T(0), T(0), T(0)};
   reset_lane(c, s, i, init, tin, y, der, wind, tgt);
-  store_env_fresh(c, s, i, y, der, wind, tgt);
+  store_env_fresh(c, s, i, y, der, wind, tgt, s.life[i]);
   if (c.has_env && c.metrics) {
     const T vr[3] = {der[0], der[1], der[3]};
     metrics_init(c, s, i, tgt, vr, s.life[i]);
@@ -1059,7 +1029,13 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   const int steps_tgt = steps_tgt0 + 1;
   // ---- epilogue inputs: action / command histories (newest first), goal register, metric state ----
   T seqA[RING + 1][3], seqC[RING + 1][3];
-  uint32_t g[4];
+  // goal history (GB_*): entry count, counts, the ring words of the new entry and of the entry leaving the window
+  uint32_t gn = 1u, gcnt = 0u, gw_new = 0u, gw_old = 0u;
+  const bool goal_on = c.streak_req > 0;
+  const uint32_t req = goal_on ? (uint32_t)c.streak_req : 0u;
+  // every step but a terminal failure appends a history entry, so the new entry's index is steps0 + 1 unless the
+  // caller stepped on after a failure without reset: the loads below assume it (no load waits on GB_N)
+  const uint32_t b_guess = (uint32_t)steps0 + 1u;
   Met<T> M;
   T prev_cmd[3];
   T ep_ret0;
@@ -1082,10 +1058,27 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
         for (int q = 0; q < 3; q++) seqC[j][q] = s.cmd_ring[((int64_t)slot * 3 + q) * ld + i];
       }
     }
-    load_row(s.goal, 4, ld, i, g);
+    if (goal_on || c.metrics) gn = ld_(s.goal, GB_N, ld, i);
+    if (goal_on) {
+      gw_new = ld_(s.goal, gring_row(lep + b_guess), ld, i);
+      gw_old = ld_(s.goal, gring_row(lep + b_guess - req), ld, i);
+      gcnt = ld_(s.goal, GB_CNT, ld, i);
+    }
     if (c.metrics) {
-      M.load(c, s, i, lep, steps0);
-      load_row(s.cmd, 3, ld, i, prev_cmd);
+      M.load(s, i, lep, b_guess);
+      // the previous constrained command: recomputed from the previous raw action where the action ring
+      // already delivered it (scale_fwd(clip(.)) and constrain_commands are pure functions of the action),
+      // else the command row
+      if (c.act_need >= 1) {
+#pragma unroll
+        for (int q = 0; q < 3; q++)
+          prev_cmd[q] =
+              c.scale_actions ? scale_fwd(c, q, clipv(seqA[1][q], c.scale_low, c.scale_high)) : seqA[1][q];
+        T sp_unused[3];
+        (void)constrain_commands(c, prev_cmd, sp_unused);
+      } else {
+        load_row(s.cmd, 3, ld, i, prev_cmd);
+      }
     }
     ep_ret0 = ld_(s.ep_ret, 0, ld, i);
   };
@@ -1159,33 +1152,38 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   if (sterm == 0) {
     const T vals[3] = {der[0], der[1], der[3]};
     uint32_t gb = 0;
-    if (c.streak_req > 0) {
+    const uint32_t b = gn;  // the new history entry
+    if (goal_on) {
+      // history["goal"][*].append (fixed_wing.py:536-538): the entry's nibble, and per status the window count
+      // + the new status - the one leaving the req-deep window (the deque of get_metric, :1682-1700)
       gb = goal_status_bits(c, tgt, vals);
-      const uint32_t bit = (gb >> 3) & 1u;
-      g[3] = (g[3] << 1) | (g[2] >> 31);
-      g[2] = (g[2] << 1) | (g[1] >> 31);
-      g[1] = (g[1] << 1) | (g[0] >> 31);
-      g[0] = (g[0] << 1) | bit;
-      if (steps_tgt >= c.streak_req) {
-        int cnt = 0, rem = c.streak_req;
+      const uint32_t pn = lep + b, po = pn - req;
+      if (b != b_guess) {
+        gw_new = ld_(s.goal, gring_row(pn), ld, i);
+        gw_old = ld_(s.goal, gring_row(po), ld, i);
+      }
+      const uint32_t leave = b >= req ? gring_get(gw_old, po) : 0u;
 #pragma unroll
-        for (int w = 0; w < 4; w++) {
-          const int take = rem >= 32 ? 32 : (rem > 0 ? rem : 0);
-          const uint32_t m = take == 32 ? 0xFFFFFFFFu : ((1u << take) - 1u);
-          cnt += __builtin_popcount(g[w] & m);
-          rem -= take;
-        }
-        if ((double)cnt / (double)c.streak_req >= (double)c.streak_frac && c.on_success == 1) {
-          done = true;
-          term = FW_TERM_SUCCESS;
-        }
+      for (int k = 0; k < 4; k++) {
+        const uint32_t ck = ((gcnt >> (8 * k)) & 0xFFu) - ((leave >> k) & 1u) + ((gb >> k) & 1u);
+        gcnt = (gcnt & ~(0xFFu << (8 * k))) | (ck << (8 * k));
+      }
+      st_(s.goal, gring_row(pn), ld, i, gring_set(gw_new, pn, gb));
+      st_(s.goal, GB_CNT, ld, i, gcnt);
+      // np.mean(history["goal"]["all"][-streak_req:]) >= success_streak_fraction (:540-547)
+      if (steps_tgt >= c.streak_req &&
+          (double)(gcnt >> 24) / (double)c.streak_req >= (double)c.streak_frac && c.on_success == 1) {
+        done = true;
+        term = FW_TERM_SUCCESS;
       }
     }
+    if (goal_on || c.metrics) st_(s.goal, GB_N, ld, i, b + 1u);
     reward = reward_of(c, y, der, tgt, steps, seqA);
     next_target(c, steps_tgt, tgt);
 #ifndef FW_MET_SKIP_STEP
-    if (c.metrics) metrics_step(c, s, i, M, tgt, vals, gb, g, lep);
+    if (c.metrics) metrics_step(c, s, i, M, tgt, vals, gb, gcnt, b, lep);
 #endif
+    gn = b + 1u;
   } else {
     done = true;
     reward = c.step_fail_timesteps ? (T)(steps - c.steps_max) : c.step_fail_value;
@@ -1218,7 +1216,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
     M.store(s, i);
 #endif
 #ifndef FW_MET_SKIP_FINAL
-    if (done && s.met_out) metrics_final(c, M, steps, s.met_out + i, s.n);
+    if (done && s.met_out) metrics_final(c, M, gn, steps, s.met_out + i, s.n);
 #endif
   }
   FW_TSTAMP(3);
@@ -1230,7 +1228,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
       // the worker's env.reset() passes no turbulence_noise: Dryden.reset(None) (dryden.py:184-188)
       if (s.noise_env_len) s.noise_env_len[i] = 0;
       reset_lane(c, s, i, (const T*)nullptr, (const T*)nullptr, yr, dr, wr, tr);
-      store_env_fresh(c, s, i, yr, dr, wr, tr);
+      store_env_fresh(c, s, i, yr, dr, wr, tr, life0 + 1u);
 #ifndef FW_MET_SKIP_INIT
       if (c.metrics) {
         const T vr[3] = {dr[0], dr[1], dr[3]};
@@ -1254,8 +1252,6 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
 #pragma unroll
   for (int k = 0; k < 3; k++)  // (constant-class targets never change within an episode)
     if (__ballot(bits_differ(tgt[k], tgt_in[k]))) st_(s.target, k, ld, i, tgt[k]);
-#pragma unroll
-  for (int w = 0; w < 4; w++) st_(s.goal, w, ld, i, g[w]);
   st_(s.ep_ret, 0, ld, i, ep_ret);
   s.steps[i] = (uint32_t)(steps & 0xFFFF) | ((uint32_t)(steps_tgt & 0xFFFF) << 16);
   s.life[i] = life0 + 1u;
@@ -1636,7 +1632,7 @@ struct fw_handle {
   void* met_out = nullptr;  // [FW_NMETRIC][N] done-episode records (fw_set_metrics_output)
   // offsets (bytes) of the SoA blocks inside base
   size_t o_y, o_der, o_wind, o_target, o_cmd, o_epret, o_act, o_cmdring, o_steps, o_goal, o_episode, o_life;
-  size_t o_met = 0, o_metu = 0, o_metu16 = 0;
+  size_t o_met = 0, o_metu16 = 0;
   int obs_hist = 0;         // past raw observation rows kept per env ((length - 1) * step + 2, 0 = none)
   size_t o_obs_init = 0, o_obs_ring = 0;
   size_t o_prm = 0;         // per-aircraft parameter rows (env->n_rand > 0 at create; 0 = none)
@@ -2018,7 +2014,6 @@ State<T> state_of(const fw_handle* h) {
   s.key1 = (uint32_t)(h->seed >> 32);
   s.env_offset = (uint32_t)h->env_offset;
   s.met = h->metrics ? (T*)(b + h->o_met) : nullptr;
-  s.metu = h->metrics ? (uint32_t*)(b + h->o_metu) : nullptr;
   s.metu16 = h->metrics ? (uint16_t*)(b + h->o_metu16) : nullptr;
   s.met_out = (T*)h->met_out;
   s.obs_init = h->obs_hist ? (T*)(b + h->o_obs_init) : nullptr;
@@ -2156,12 +2151,11 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
   h->o_act = off; off += (size_t)h->act_window * 3 * row;
   h->o_cmdring = off; off += (size_t)h->cmd_window * 3 * row;
   h->o_steps = off; off += row32;
-  h->o_goal = off; off += 4 * row32;
+  h->o_goal = off; off += (size_t)GB_ROWS * row32;
   h->o_episode = off; off += row32;
   h->o_life = off; off += row32;
   if (h->metrics) {
     h->o_met = off; off += (size_t)MT_ROWS * row;
-    h->o_metu = off; off += (size_t)MU_ROWS * row32;
     h->o_metu16 = off; off += (size_t)M16_ROWS * align_up((size_t)h->ld * 2, 256);
   }
   if (sim->turbulence) {  // Dryden filter-bank state (used when the chunk is too short for the FIR)
@@ -2186,6 +2180,7 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
   h->base_bytes = off;
   e = hipMalloc(&h->base, off);
   if (e == hipSuccess) e = hipMemset(h->base, 0, off);
+  if (e == hipSuccess) e = hipMemsetD32((hipDeviceptr_t)((char*)h->base + h->o_life), (int)LIFE0, (size_t)h->ld);
   if (e == hipSuccess) e = hipMalloc(&h->dcfg, precision == FW_F64 ? sizeof(DevCfg<double>) : sizeof(DevCfg<float>));
   if (e != hipSuccess) {
     if (h->base) (void)hipFree(h->base);
@@ -2406,16 +2401,17 @@ int fw_collect_records(const fw_handle* h, int64_t* n_records, int64_t* max_reco
 }
 
 // FW_BLK_ACT_RING / FW_BLK_CMD_RING as the ABI presents them (action k of the current episode in slot
-// (k - 1) % W, fwsim.h) <-> the device layout (slot (L_ep + k - 1) % W with L_ep = life - steps_count, the
-// lifetime-indexed rings of State): a per-aircraft rotation of the W slots.
+// (k - 1) % W, fwsim.h) <-> the device layout (the action j steps back, k = steps_count + 1 - j, in slot
+// (life - j) % W: the expression k_env_step reads it with): a per-aircraft rotation of the W slots.
 __global__ void k_ring_xlate(const char* __restrict__ src, char* __restrict__ dst, int W, int64_t n, int esz,
                              int64_t row_dev, int64_t row_abi, const uint32_t* __restrict__ life,
                              const uint32_t* __restrict__ steps, int to_abi) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const uint32_t lep = life[i] - (steps[i] & 0xFFFFu);
-  for (int q = 0; q < W; q++) {
-    const int p = (int)((lep + (uint32_t)q) % (uint32_t)W);
+  const int st = (int)(steps[i] & 0xFFFFu);
+  for (int j = 1; j <= W; j++) {
+    const int p = (int)((life[i] - (uint32_t)j) % (uint32_t)W);
+    const int q = ((st - j) % W + W) % W;  // (k - 1) % W for k = st + 1 - j (k <= 0: an earlier episode's slot)
     for (int a = 0; a < 3; a++) {
       const int64_t rl = (int64_t)q * 3 + a, rp = (int64_t)p * 3 + a;
       const char* from = to_abi ? src + rp * row_dev + i * esz : src + rl * row_abi + i * esz;
@@ -2438,6 +2434,48 @@ static int ring_copy(fw_handle* h, int32_t block, size_t off, size_t esz, const 
   return check_launch();
 }
 
+// FW_BLK_GOAL as the ABI presents it (the 128-bit register of the "all" statuses, bit j of row j / 32 = entry
+// N - 1 - j of the episode's history, 0 past its start, fwsim.h) <-> the device's goal history (GB_*: nibble ring
+// by lifetime position, window counts, entry count N).  Setting takes N = steps_count + 1 from FW_BLK_STEPS (the
+// history of an episode without a failed step: a checkpoint sets FW_BLK_STEPS first), rewrites the "all" bit of
+// the 128 ring positions and recounts the "all" window; the per-target statuses and counts (metrics) stay.
+__global__ void k_goal_xlate(uint32_t* __restrict__ goal, int64_t ld, uint32_t* __restrict__ reg, int64_t n,
+                             const uint32_t* __restrict__ life, const uint32_t* __restrict__ steps, int req,
+                             int to_abi) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t N = to_abi ? goal[GB_N * ld + i] : (steps[i] & 0xFFFFu) + 1u;
+  const uint32_t newest = life[i] - (steps[i] & 0xFFFFu) + N - 1u;  // lifetime position of entry N - 1
+  if (!to_abi) goal[GB_N * ld + i] = N;
+  if (to_abi) {
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t j = 0; j < 128u && j < N; j++) {
+      const uint32_t pos = newest - j;
+      w[j >> 5] |= ((gring_get(goal[gring_row(pos) * ld + i], pos) >> 3) & 1u) << (j & 31u);
+    }
+    for (int r = 0; r < 4; r++) reg[r * n + i] = w[r];
+    return;
+  }
+  uint32_t cnt = 0u;
+  for (uint32_t j = 0; j < 128u; j++) {
+    const uint32_t pos = newest - j, bit = (reg[(j >> 5) * n + i] >> (j & 31u)) & 1u;
+    uint32_t* wp = goal + gring_row(pos) * ld + i;
+    *wp = gring_set(*wp, pos, (gring_get(*wp, pos) & 7u) | (bit << 3));
+    if ((int)j < req && j < N) cnt += bit;
+  }
+  uint32_t* cp = goal + GB_CNT * ld + i;
+  *cp = (*cp & 0x00FFFFFFu) | (cnt << 24);
+}
+
+static int goal_copy(fw_handle* h, const void* src, void* dst, int to_abi, hipStream_t st) {
+  char* b = (char*)h->base;
+  hipLaunchKernelGGL(k_goal_xlate, dim3((unsigned)((h->n + 255) / 256)), dim3(256), 0, st, (uint32_t*)(b + h->o_goal),
+                     (int64_t)h->ld, to_abi ? (uint32_t*)dst : (uint32_t*)const_cast<void*>(src), h->n,
+                     (const uint32_t*)(b + h->o_life), (const uint32_t*)(b + h->o_steps),
+                     h->has_env ? std::max(h->env.streak_req, 0) : 0, to_abi);
+  return check_launch();
+}
+
 static int block_info(const fw_handle* h, int32_t block, size_t* off, int* rows, size_t* esz) {
   const size_t T_ = h->precision == FW_F64 ? 8 : 4;
   switch (block) {
@@ -2456,7 +2494,9 @@ static int block_info(const fw_handle* h, int32_t block, size_t* off, int* rows,
     case FW_BLK_CMD_RING:
       if (!h->has_env || !h->cmd_window) return set_err(FW_E_INVALID, "handle keeps no command ring");
       *off = h->o_cmdring; *rows = 3 * h->cmd_window; *esz = T_; return FW_OK;
-    case FW_BLK_GOAL: *off = h->o_goal; *rows = 4; *esz = 4; return FW_OK;
+    case FW_BLK_GOAL:
+      if (!h->has_env) return set_err(FW_E_INVALID, "handle has no env (no goal history)");
+      *off = h->o_goal; *rows = 4; *esz = 4; return FW_OK;
     default: return set_err(FW_E_INVALID, "unknown state block");
   }
 }
@@ -2481,6 +2521,7 @@ int fw_get_state(fw_handle* h, int32_t block, void* dst_dev, void* stream) {
   FW_HIP(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
   if (block == FW_BLK_ACT_RING || block == FW_BLK_CMD_RING) return ring_copy(h, block, off, esz, nullptr, dst_dev, 1, st);
+  if (block == FW_BLK_GOAL) return goal_copy(h, nullptr, dst_dev, 1, st);
   const size_t row = align_up((size_t)h->ld * esz, 256);
   FW_HIP(hipMemcpy2DAsync(dst_dev, h->n * esz, (char*)h->base + off, row, h->n * esz, rows, hipMemcpyDeviceToDevice,
                           st));
@@ -2496,6 +2537,7 @@ int fw_set_state(fw_handle* h, int32_t block, const void* src_dev, void* stream)
   FW_HIP(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
   if (block == FW_BLK_ACT_RING || block == FW_BLK_CMD_RING) return ring_copy(h, block, off, esz, src_dev, nullptr, 0, st);
+  if (block == FW_BLK_GOAL) return goal_copy(h, src_dev, nullptr, 0, st);
   const size_t row = align_up((size_t)h->ld * esz, 256);
   FW_HIP(hipMemcpy2DAsync((char*)h->base + off, row, src_dev, h->n * esz, h->n * esz, rows, hipMemcpyDeviceToDevice,
                           st));
