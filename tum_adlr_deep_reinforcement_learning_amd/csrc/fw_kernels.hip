@@ -70,6 +70,11 @@ constexpr int BLOCK = FW_BLOCK;
 #define FW_QUAD_MIN_WAVES 1  // ... of their quad (Q = 4) instances
 #endif
 #define FW_WAVES(Q) ((Q) == 4 ? FW_QUAD_MIN_WAVES : FW_MIN_WAVES)
+#ifndef FW_HALF_WAVE
+// A/B only (tools/r05_halfwave.sh; with FW_MIN_WAVES=2): one-lane k_env_step waves step 32 aircraft (lanes 0..31),
+// twice the waves, so a second wave can share each SIMD.  No collect epilogue, no tail handoff to the idle lanes.
+#define FW_HALF_WAVE 0
+#endif
 #ifndef FW_PREF_Q4_F64
 // 1: the fp64 quad instances prefetch the epilogue's loads like the fp32 ones.  In fp64 the prefetched
 // rows spill (339 VGPRs): 8192 aircraft 0.137 -> 0.099 ms per step without it (profiles/r03_ab_pref64.log)
@@ -1504,7 +1509,12 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_env_step(const DevCfg<T>
                                                     int32_t* __restrict__ term_out, T* __restrict__ tobs_out,
                                                     T* __restrict__ episode_out, int32_t* __restrict__ stats,
                                                     int auto_reset) {
+#if FW_HALF_WAVE
+  const int64_t tid = Q == 1 ? (threadIdx.x < 32 ? (int64_t)blockIdx.x * 32 + threadIdx.x : (int64_t)s.n)
+                             : (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+#else
   const int64_t tid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+#endif
   const int64_t i = tid / Q;  // Q = 4: lanes 4i..4i+3 integrate aircraft i (fw_quad.hpp)
   const bool collect = s.col_rec || s.col_ret || s.col_ctrl;
   if (i >= s.n && !collect) return;
@@ -1958,18 +1968,20 @@ int lanes_of(const fw_handle* h) {
 
 // launch KERNEL<T, C> with C chosen by the handle's structural specialisation (G / P: the gym / pyfly
 // X8 view types of this kernel)
-#define FW_LAUNCH_SPEC_AS(KERNEL, G, P, T, h, st, ...)                                                          \
+#define FW_LAUNCH_SPEC_GRID(KERNEL, G, P, T, h, st, grid, ...)                                                  \
   do {                                                                                                           \
-    const dim3 g_(grid_of(h)), b_(BLOCK);                                                                        \
+    const dim3 gg_(grid), b_(BLOCK);                                                                             \
     if ((h)->rand_active)                                                                                        \
-      hipLaunchKernelGGL((KERNEL<T, DevCfg<T>, true>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);  \
+      hipLaunchKernelGGL((KERNEL<T, DevCfg<T>, true>), gg_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);  \
     else if ((h)->spec == 1)                                                                                     \
-      hipLaunchKernelGGL((KERNEL<T, G<T>>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);             \
+      hipLaunchKernelGGL((KERNEL<T, G<T>>), gg_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);             \
     else if ((h)->spec == 2)                                                                                     \
-      hipLaunchKernelGGL((KERNEL<T, P<T>>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);             \
+      hipLaunchKernelGGL((KERNEL<T, P<T>>), gg_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);             \
     else                                                                                                         \
-      hipLaunchKernelGGL((KERNEL<T, DevCfg<T>>), g_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);        \
+      hipLaunchKernelGGL((KERNEL<T, DevCfg<T>>), gg_, b_, 0, st, (const DevCfg<T>*)(h)->dcfg, __VA_ARGS__);        \
   } while (0)
+#define FW_LAUNCH_SPEC_AS(KERNEL, G, P, T, h, st, ...) \
+  FW_LAUNCH_SPEC_GRID(KERNEL, G, P, T, h, st, grid_of(h), __VA_ARGS__)
 #define FW_LAUNCH_SPEC(KERNEL, T, h, st, ...) FW_LAUNCH_SPEC_AS(KERNEL, GymX8Cfg, PyflyX8Cfg, T, h, st, __VA_ARGS__)
 
 // ... and Q = lanes per aircraft (1, or 4 for the quad integrator)
@@ -1977,7 +1989,8 @@ int lanes_of(const fw_handle* h) {
   do {                                                                                                             \
     const dim3 b_(BLOCK);                                                                                          \
     const int q_ = lanes_of(h);                                                                                    \
-    const dim3 g_((unsigned)(((h)->n * q_ + BLOCK - 1) / BLOCK));                                                  \
+    const dim3 g_((unsigned)(((h)->n * q_ + (FW_HALF_WAVE && q_ == 1 ? 32 : BLOCK) - 1) /                          \
+                             (FW_HALF_WAVE && q_ == 1 ? 32 : BLOCK)));                                            \
     const DevCfg<T>* d_ = (const DevCfg<T>*)(h)->dcfg;                                                             \
     if (q_ == 4) {                                                                                                 \
       if ((h)->rand_active) hipLaunchKernelGGL((KERNEL<T, DevCfg<T>, true, 4>), g_, b_, 0, st, d_, __VA_ARGS__);   \
@@ -1985,7 +1998,7 @@ int lanes_of(const fw_handle* h) {
       else if ((h)->spec == 2) hipLaunchKernelGGL((KERNEL<T, PyflyX8Cfg<T>, false, 4>), g_, b_, 0, st, d_, __VA_ARGS__); \
       else hipLaunchKernelGGL((KERNEL<T, DevCfg<T>, false, 4>), g_, b_, 0, st, d_, __VA_ARGS__);                  \
     } else {                                                                                                       \
-      FW_LAUNCH_SPEC(KERNEL, T, h, st, __VA_ARGS__);                                                               \
+      FW_LAUNCH_SPEC_GRID(KERNEL, GymX8Cfg, PyflyX8Cfg, T, h, st, g_, __VA_ARGS__);                                \
     }                                                                                                              \
   } while (0)
 

@@ -421,6 +421,9 @@ struct QRun {
   int rejected, nfev, nacc;
 };
 
+#ifndef FW_QUAD_DIAG_FOLD
+#define FW_QUAD_DIAG_FOLD 3  // timing diagnostics only (below): 3 = all pairs, the shipped integrator
+#endif
 #ifndef FW_QUAD_UNROLL
 #define FW_QUAD_UNROLL 1  // 0 = the stage machine below (one RHS site per loop iteration), A/B switch
 #endif
@@ -442,6 +445,10 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
   using V = V2<T>;
   using namespace dp5;
   constexpr int NQ = 3;
+  // pairs of the trial-step folds (Dormand-Prince stages, error norm, acceptance): NQ.  Diagnostic builds only
+  // (FW_QUAD_DIAG_FOLD=2, tools/r05_fold8.sh; wrong results): the fold load of an 8-lane group (3 elements a lane)
+  constexpr int NF = FW_QUAD_DIAG_FOLD;
+  static_assert(NF >= 1 && NF <= NQ, "FW_QUAD_DIAG_FOLD: 1..3 pairs");
   const T rtol = c.rtol, atol = c.atol;
   const double t_bound = c.t_bound;
   const T inv_sqrt_n = T(0.22941573387056177);  // 1 / sqrt(19)
@@ -481,7 +488,9 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
   };
   auto seed = [&]() {  // stage-1 input and accumulators of a trial step
 #pragma unroll
-    for (int p = 0; p < NQ; p++) {
+    for (int p = NF; p < NQ; p++) ys[p] = Y[p];  // (diagnostic builds: the pairs the folds skip stay at Y)
+#pragma unroll
+    for (int p = 0; p < NF; p++) {
       const V f = F[p];
       ys[p] = Y[p] + (f * T(A10)) * ht;
       P2v[p] = f * T(A20);
@@ -561,7 +570,7 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
     tight = any_lane(active && room <= 6);
     if (!eval(false, 1)) break;  // K1
 #pragma unroll
-    for (int p = 0; p < NQ; p++) {
+    for (int p = 0; p < NF; p++) {
       ys[p] = Y[p] + (P2v[p] + K[p] * T(A21)) * ht;
       P3[p] += K[p] * T(A31);
       P4[p] += K[p] * T(A41);
@@ -569,7 +578,7 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
     }
     if (!eval(false, 2)) break;  // K2
 #pragma unroll
-    for (int p = 0; p < NQ; p++) {
+    for (int p = 0; p < NF; p++) {
       P3[p] += K[p] * T(A32);
       P4[p] += K[p] * T(A42);
       P5[p] += K[p] * T(A52);
@@ -579,7 +588,7 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
     }
     if (!eval(false, 3)) break;  // K3
 #pragma unroll
-    for (int p = 0; p < NQ; p++) {
+    for (int p = 0; p < NF; p++) {
       P4[p] += K[p] * T(A43);
       P5[p] += K[p] * T(A53);
       YB[p] += K[p] * T(B3);
@@ -588,7 +597,7 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
     }
     if (!eval(false, 4)) break;  // K4
 #pragma unroll
-    for (int p = 0; p < NQ; p++) {
+    for (int p = 0; p < NF; p++) {
       P5[p] += K[p] * T(A54);
       YB[p] += K[p] * T(B4);
       ER[p] += K[p] * T(E4);
@@ -596,7 +605,7 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
     }
     if (!eval(false, 5)) break;  // K5; ys <- y_new
 #pragma unroll
-    for (int p = 0; p < NQ; p++) {
+    for (int p = 0; p < NF; p++) {
       YB[p] += K[p] * T(B5);
       ER[p] += K[p] * T(E5);
       ys[p] = Y[p] + ht * YB[p];
@@ -605,7 +614,7 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
     if (active) nfev += 6;
     T es = T(0);
 #pragma unroll
-    for (int p = 0; p < NQ; p++) {
+    for (int p = 0; p < NF; p++) {
       const V e = (ER[p] + K[p] * T(E6)) * ht;
       const V y0 = Y[p], y1 = ys[p];
       V sc;
@@ -622,7 +631,7 @@ __device__ __forceinline__ int rk45_quad_core(const C& c, const A& a, const QCtx
         h_abs *= factor;
         t = t_new;
 #pragma unroll
-        for (int p = 0; p < NQ; p++) {
+        for (int p = 0; p < NF; p++) {
           Y[p] = ys[p];
           F[p] = K[p];
         }
