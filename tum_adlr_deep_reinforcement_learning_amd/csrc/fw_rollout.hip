@@ -725,6 +725,12 @@ struct PolArgs {
 };
 
 constexpr int PM_WAVES = 4;  // waves per block; two blocks per CU (two waves per SIMD)
+#ifndef FW_POL_STAGGER
+#define FW_POL_STAGGER 0  // s_sleep units (64 cycles) the second half of the grid waits (A/B, below)
+#endif
+#ifndef FW_POL_TILES
+#define FW_POL_TILES 1  // 16-env tiles per wave iteration of k_policy_mfma (A/B: tools/r05_pol.sh)
+#endif
 #ifndef FW_POL_DIAG
 // timing diagnostics only (tools/r04_poldiag.sh builds library variants; their results are wrong): 1 = no tanh,
 // 2 = no hidden-layer MFMA, 3 = no LDS weight fill, 4 = no row / output stores, 5 = no observation normalisation
@@ -810,7 +816,8 @@ __device__ __forceinline__ void pol_fill_lds(const fw_mlp_policy& P, float* W) {
 
 __device__ __forceinline__ f32x4 lds4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
-template <int S>  // k-steps of 4 observation features (d <= 4 S)
+// S: k-steps of 4 observation features (d <= 4 S); AM: actions held per lane (act_dim <= AM, 4 or POL_MAXA)
+template <int S, int AM = POL_MAXA>
 __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
   using L = PolLds<S>;
   extern __shared__ float Wl[];
@@ -818,9 +825,8 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
   const int c16 = lane & 15, g = lane >> 4;
   const int d = G.P.d, A = G.P.act_dim;
   const int64_t n = G.n;
-  // ---- the block's A-operand image in LDS (two blocks per CU, two waves per SIMD: one wave's MFMAs overlap
+  // ---- the block's A-operand image in LDS (filled below; two blocks per CU, two waves per SIMD: one wave's MFMAs overlap
   // the other's tanh / loads; with the weights in registers a wave took 430 VGPRs and ran alone on its SIMD)
-  if (FW_POL_DIAG != 3) pol_fill_lds<S>(G.P, Wl);
   const float* W0 = Wl + L::L0 + lane * S;
   const float* W1 = Wl + L::L1 + lane * 4;
   const float* WH = Wl + L::HD + lane * 4;
@@ -830,14 +836,35 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
   const float* noise = G.noise;
   if (noise) noise += (G.ctrl ? row : (G.noise_row ? (int64_t)G.noise_row[0] : 0)) * n * A;
   const bool nobs = G.rms && G.norm_obs;
+  // The prologue's loads are issued together from clamped, valid addresses under wave-uniform conditions, then
+  // selected: a load per feature / action under its own lane condition compiled to a branch with a wait each,
+  // eight dependent round trips before the first tile (fp64 statistics) plus the action constants.
   double mean[S], den[S];
+  const bool nrew = G.rms && G.norm_rew;
+  double rvar = 0.0;
+  if (nobs || nrew) {
+    double mr[S], vr[S];
 #pragma unroll
-  for (int s = 0; s < S; s++) {
-    const int f = 4 * s + g;
-    mean[s] = (nobs && f < d) ? G.rms[f] : 0.0;
-    den[s] = (nobs && f < d) ? sqrt(G.rms[d + f] + G.eps) : 1.0;
+    for (int s = 0; s < S; s++) {
+      const int f = 4 * s + g, fc = f < d ? f : d - 1;
+      mr[s] = G.rms[fc];
+      vr[s] = G.rms[d + fc];
+    }
+    rvar = G.rms[2 * d + 2];
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const bool on = nobs && 4 * s + g < d;
+      mean[s] = on ? mr[s] : 0.0;
+      den[s] = on ? sqrt(vr[s] + G.eps) : 1.0;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      mean[s] = 0.0;
+      den[s] = 1.0;
+    }
   }
-  const double rden = (G.rms && G.norm_rew) ? sqrt(G.rms[2 * d + 2] + G.eps) : 1.0;
+  const double rden = nrew ? sqrt(rvar + G.eps) : 1.0;
   float* obs_rows = G.obs_rows ? G.obs_rows + row * n * d : nullptr;
   float* act = G.act + row * n * A;
   float* val = G.val + row * n;
@@ -845,20 +872,35 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
   const float half_log_2pi = 0.91893853320467274f;
   // per-action constants, loaded once (uniform: scalar registers), not per tile inside the lane-divergent
   // action stage (where each load waited for every outstanding load, the next tile's prefetch included)
-  float lsA[POL_MAXA], sdA[POL_MAXA], hiA[POL_MAXA], loA[POL_MAXA];
+  float lsA[AM], sdA[AM], hiA[AM], loA[AM];
+  {
+    float l_[AM], h_[AM], o_[AM];
 #pragma unroll
-  for (int a = 0; a < POL_MAXA; a++) {
-    lsA[a] = a < A ? G.P.log_std[a] : 0.0f;
-    sdA[a] = expf(lsA[a]);
-    hiA[a] = (a < A && G.clipped) ? G.high[a] : 0.0f;
-    loA[a] = (a < A && G.clipped) ? G.low[a] : 0.0f;
+    for (int a = 0; a < AM; a++) l_[a] = G.P.log_std[a < A ? a : A - 1];
+    if (G.clipped) {
+#pragma unroll
+      for (int a = 0; a < AM; a++) {
+        h_[a] = G.high[a < A ? a : A - 1];
+        o_[a] = G.low[a < A ? a : A - 1];
+      }
+    } else {
+#pragma unroll
+      for (int a = 0; a < AM; a++) h_[a] = o_[a] = 0.0f;
+    }
+#pragma unroll
+    for (int a = 0; a < AM; a++) {
+      lsA[a] = a < A ? l_[a] : 0.0f;
+      sdA[a] = expf(lsA[a]);
+      hiA[a] = a < A ? h_[a] : 0.0f;
+      loA[a] = a < A ? o_[a] : 0.0f;
+    }
   }
 
   const int64_t tiles = (n + 15) / 16;
   const int64_t wid = (int64_t)blockIdx.x * PM_WAVES + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * PM_WAVES;
-  // A tile's inputs are loaded one tile ahead (their HBM latency hides under the previous tile's MFMAs):
-  // the raw observation features of this lane, and -- for the row stores -- the previous step's reward and
-  // done flag (lanes g == 1) and this step's noise draws (lanes g == 0).  Restrict-qualified locals: the
+  // A tile's inputs are loaded one iteration ahead (their HBM latency hides under the previous iteration's
+  // MFMAs): the raw observation features of this lane, and -- for the row stores -- the previous step's reward
+  // and done flag (lanes g == 1) and this step's noise draws (lanes g == 0).  Restrict-qualified locals: the
   // output stores cannot alias the inputs, so the loads are not serialised behind them.
   const float* __restrict__ obs_in = G.obs;
   const float* __restrict__ rew_in = G.reward;
@@ -869,10 +911,10 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
     float o[S];
     float r;
     uint32_t dn;
-    float z[POL_MAXA];
+    float z[AM];
   };
   // branch-free, and not selected on load: every lane loads from a clamped, valid address straight into the
-  // register it is consumed from one tile later; the validity masks apply at the use (a select right after
+  // register it is consumed from one iteration later; the validity masks apply at the use (a select right after
   // the load, or a load inside an exec-masked block, makes the compiler wait for it there)
   auto fetch = [&](int64_t t, In& in) {
     const int64_t e = t * 16 + c16;
@@ -887,127 +929,207 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
       in.dn = done_in[ec];
     }
 #pragma unroll
-    for (int a = 0; a < POL_MAXA; a++)
+    for (int a = 0; a < AM; a++)
       if (noise_in && a < A) in.z[a] = noise_in[ec * A + a];
   };
-  In nxt{};
-  fetch(wid, nxt);
-  for (int64_t tile = wid; tile < tiles; tile += nw) {
-    const int64_t env = tile * 16 + c16;
-    const bool valid = env < n;
-    const In cur = nxt;
-    fetch(tile + nw, nxt);
+  // PT tiles per iteration, interleaved stage by stage: each A operand read from LDS serves PT tiles, and one
+  // tile's tanh overlaps the other's MFMAs within the wave (the per-tile arithmetic, and so every bit of the
+  // outputs, is the same for any PT)
+  constexpr int PT = FW_POL_TILES;
+  In nxt[PT];
+#pragma unroll
+  for (int p = 0; p < PT; p++) nxt[p] = In{};
+#pragma unroll
+  for (int p = 0; p < PT; p++) fetch(wid * PT + p, nxt[p]);
+  // the block's weight image after the first tiles' loads are issued (their latency hides under the fill)
+  if (FW_POL_DIAG != 3) pol_fill_lds<S>(G.P, Wl);
+#if FW_POL_STAGGER
+  // A/B (tools/r05_pol.sh): the CU's second block starts FW_POL_STAGGER x 64 cycles late, so its waves' tanh
+  // phases meet their SIMD partners' MFMA phases instead of running in lockstep with them
+  if (blockIdx.x >= gridDim.x / 2)
+#pragma unroll
+    for (int k = 0; k < FW_POL_STAGGER / 32; k++) __builtin_amdgcn_s_sleep(32);
+#endif
+  for (int64_t base = wid * PT; base < tiles; base += nw * PT) {
+    In cur[PT];
+#pragma unroll
+    for (int p = 0; p < PT; p++) {
+      cur[p] = nxt[p];
+      fetch(base + nw * PT + p, nxt[p]);
+    }
+    int64_t env[PT];
+    bool valid[PT];
     // ---- observation (normalised) = B operands of layer 0; the rollout's observation row
-    float x[S];
+    float x[PT][S];
 #pragma unroll
-    for (int s = 0; s < S; s++) {
-      const int f = 4 * s + g;
-      float o = (valid && f < d) ? cur.o[s] : 0.0f;
-      if (FW_POL_DIAG != 5 && nobs && valid && f < d) o = norm_obs_val(o, mean[s], den[s], G.clip_obs);
-      x[s] = o;
-      if (FW_POL_DIAG != 4 && obs_rows && valid && f < d) obs_rows[env * d + f] = o;
+    for (int p = 0; p < PT; p++) {
+      env[p] = (base + p) * 16 + c16;
+      valid[p] = base + p < tiles && env[p] < n;
+#pragma unroll
+      for (int s = 0; s < S; s++) {
+        const int f = 4 * s + g;
+        float o = (valid[p] && f < d) ? cur[p].o[s] : 0.0f;
+        if (FW_POL_DIAG != 5 && nobs && valid[p] && f < d) o = norm_obs_val(o, mean[s], den[s], G.clip_obs);
+        x[p][s] = o;
+        if (FW_POL_DIAG != 4 && obs_rows && valid[p] && f < d) obs_rows[env[p] * d + f] = o;
+      }
+      // ---- the previous step's reward row (normalised) and the episode starts of this row
+      if (rows_prev && g == 1 && valid[p]) {
+        double r = (double)cur[p].r;
+        if (G.rms && G.norm_rew) r = fmin(fmax(r / rden, -G.clip_rew), G.clip_rew);
+        if (FW_POL_DIAG != 4) G.rew_rows[(row - 1) * n + env[p]] = (float)r;
+        G.start_rows[row * n + env[p]] = (uint8_t)cur[p].dn;
+      }
     }
-    // ---- the previous step's reward row (normalised) and the episode starts of this row
-    if (rows_prev && g == 1 && valid) {
-      double r = (double)cur.r;
-      if (G.rms && G.norm_rew) r = fmin(fmax(r / rden, -G.clip_rew), G.clip_rew);
-      if (FW_POL_DIAG != 4) G.rew_rows[(row - 1) * n + env] = (float)r;
-      G.start_rows[row * n + env] = (uint8_t)cur.dn;
-    }
-    asm volatile("" ::: "memory");  // the A operands are re-read from LDS every tile (not hoisted into VGPRs)
-    // ---- layer 0 (8 independent accumulators, starting at the scaled bias)
-    f32x4 cp[4], cv[4];
+    asm volatile("" ::: "memory");  // the A operands are re-read from LDS every iteration (not hoisted into VGPRs)
+    // ---- layer 0 (8 independent accumulators per tile, starting at the scaled bias)
+    f32x4 cp[PT][4], cv[PT][4];
 #pragma unroll
     for (int O = 0; O < 4; O++) {
-      cp[O] = lds4(WB + (0 * 4 + O) * 16);
-      cv[O] = lds4(WB + (1 * 4 + O) * 16);
+      const f32x4 bp = lds4(WB + (0 * 4 + O) * 16), bv = lds4(WB + (1 * 4 + O) * 16);
+#pragma unroll
+      for (int p = 0; p < PT; p++) {
+        cp[p][O] = bp;
+        cv[p][O] = bv;
+      }
     }
+    // every fragment of a k-group first, then the MFMAs round-robin over the eight accumulators (a dependent
+    // MFMA every 8 issues, past its 40-cycle latency; the per-accumulator order -- s4, then k -- is unchanged)
 #pragma unroll
-    for (int O = 0; O < 4; O++) {
+    for (int s4 = 0; s4 < S; s4 += 4) {
+      f32x4 ap[4], av[4];
 #pragma unroll
-      for (int s4 = 0; s4 < S; s4 += 4) {
-        const f32x4 ap = lds4(W0 + (0 * 4 + O) * 64 * S + s4), av = lds4(W0 + (1 * 4 + O) * 64 * S + s4);
+      for (int O = 0; O < 4; O++) {
+        ap[O] = lds4(W0 + (0 * 4 + O) * 64 * S + s4);
+        av[O] = lds4(W0 + (1 * 4 + O) * 64 * S + s4);
+      }
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-          cp[O] = mfma4(ap[k], x[s4 + k], cp[O]);
-          cv[O] = mfma4(av[k], x[s4 + k], cv[O]);
+      for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int O = 0; O < 4; O++)
+#pragma unroll
+          for (int p = 0; p < PT; p++) {
+            cp[p][O] = mfma4(ap[O][k], x[p][s4 + k], cp[p][O]);
+            cv[p][O] = mfma4(av[O][k], x[p][s4 + k], cv[p][O]);
+          }
+    }
+    f32x4 hpv[PT][4], hvv[PT][4];  // tanh(layer 0): the B operands of layer 1, k-step (T, v) = register v of tile T
+#pragma unroll
+    for (int p = 0; p < PT; p++)
+#pragma unroll
+      for (int T = 0; T < 4; T++)
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+          hpv[p][T][v] = FW_POL_DIAG == 1 ? cp[p][T][v] : ftanh2(cp[p][T][v]);
+          hvv[p][T][v] = FW_POL_DIAG == 1 ? cv[p][T][v] : ftanh2(cv[p][T][v]);
         }
-      }
-    }
-    f32x4 hpv[4], hvv[4];  // tanh(layer 0): the B operands of layer 1, k-step (T, v) = register v of tile T
-#pragma unroll
-    for (int T = 0; T < 4; T++)
-#pragma unroll
-      for (int v = 0; v < 4; v++) {
-        hpv[T][v] = FW_POL_DIAG == 1 ? cp[T][v] : ftanh2(cp[T][v]);
-        hvv[T][v] = FW_POL_DIAG == 1 ? cv[T][v] : ftanh2(cv[T][v]);
-      }
     // ---- layer 1
 #pragma unroll
     for (int O = 0; O < 4; O++) {
-      cp[O] = lds4(WB + (2 * 4 + O) * 16);
-      cv[O] = lds4(WB + (3 * 4 + O) * 16);
-    }
+      const f32x4 bp = lds4(WB + (2 * 4 + O) * 16), bv = lds4(WB + (3 * 4 + O) * 16);
 #pragma unroll
-    for (int T = 0; T < 4; T++)
+      for (int p = 0; p < PT; p++) {
+        cp[p][O] = bp;
+        cv[p][O] = bv;
+      }
+    }
+    // the k-step group T + 1's eight fragments are read while group T's MFMAs issue (registers, double
+    // buffered); MFMAs round-robin over the eight accumulators; per accumulator the order (T, then v) is unchanged
+    {
+      f32x4 ap[2][4], av[2][4];
 #pragma unroll
       for (int O = 0; O < 4; O++) {
+        ap[0][O] = lds4(W1 + ((0 * 4 + O) * 4 + 0) * 256);
+        av[0][O] = lds4(W1 + ((1 * 4 + O) * 4 + 0) * 256);
+      }
+#pragma unroll
+      for (int T = 0; T < 4; T++) {
+        const int cb = T & 1, nb = cb ^ 1;
+        if (T < 3) {
+#pragma unroll
+          for (int O = 0; O < 4; O++) {
+            ap[nb][O] = lds4(W1 + ((0 * 4 + O) * 4 + T + 1) * 256);
+            av[nb][O] = lds4(W1 + ((1 * 4 + O) * 4 + T + 1) * 256);
+          }
+        }
         if (FW_POL_DIAG == 2) {
-          cp[O] += hpv[T];
-          cv[O] += hvv[T];
+#pragma unroll
+          for (int O = 0; O < 4; O++)
+#pragma unroll
+            for (int p = 0; p < PT; p++) {
+              cp[p][O] += hpv[p][T];
+              cv[p][O] += hvv[p][T];
+            }
           continue;
         }
-        const f32x4 ap = lds4(W1 + ((0 * 4 + O) * 4 + T) * 256), av = lds4(W1 + ((1 * 4 + O) * 4 + T) * 256);
+#pragma unroll
+        for (int v = 0; v < 4; v++)
+#pragma unroll
+          for (int O = 0; O < 4; O++)
+#pragma unroll
+            for (int p = 0; p < PT; p++) {
+              cp[p][O] = mfma4(ap[cb][O][v], hpv[p][T][v], cp[p][O]);
+              cv[p][O] = mfma4(av[cb][O][v], hvv[p][T][v], cv[p][O]);
+            }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < PT; p++)
+#pragma unroll
+      for (int T = 0; T < 4; T++)
 #pragma unroll
         for (int v = 0; v < 4; v++) {
-          cp[O] = mfma4(ap[v], hpv[T][v], cp[O]);
-          cv[O] = mfma4(av[v], hvv[T][v], cv[O]);
+          hpv[p][T][v] = FW_POL_DIAG == 1 ? cp[p][T][v] : ftanh2(cp[p][T][v]);
+          hvv[p][T][v] = FW_POL_DIAG == 1 ? cv[p][T][v] : ftanh2(cv[p][T][v]);
         }
-      }
-#pragma unroll
-    for (int T = 0; T < 4; T++)
-#pragma unroll
-      for (int v = 0; v < 4; v++) {
-        hpv[T][v] = FW_POL_DIAG == 1 ? cp[T][v] : ftanh2(cp[T][v]);
-        hvv[T][v] = FW_POL_DIAG == 1 ? cv[T][v] : ftanh2(cv[T][v]);
-      }
     // ---- heads: actor rows 0..A-1 and the value row 15 of one tile (two accumulators, disjoint rows)
-    f32x4 ha = {0.0f, 0.0f, 0.0f, 0.0f}, hc = {0.0f, 0.0f, 0.0f, 0.0f};
+    f32x4 ha[PT], hc[PT];
+#pragma unroll
+    for (int p = 0; p < PT; p++) {
+      ha[p] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      hc[p] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
 #pragma unroll
     for (int T = 0; T < 4; T++) {
       const f32x4 ap = lds4(WH + (0 * 4 + T) * 256), av = lds4(WH + (1 * 4 + T) * 256);
 #pragma unroll
-      for (int v = 0; v < 4; v++) {
-        ha = mfma4(ap[v], hpv[T][v], ha);
-        hc = mfma4(av[v], hvv[T][v], hc);
-      }
+      for (int v = 0; v < 4; v++)
+#pragma unroll
+        for (int p = 0; p < PT; p++) {
+          ha[p] = mfma4(ap[v], hpv[p][T][v], ha[p]);
+          hc[p] = mfma4(av[v], hvv[p][T][v], hc[p]);
+        }
     }
     const f32x4 bh = lds4(Wl + L::BH + 4 * g);
-    f32x4 out;
 #pragma unroll
-    for (int v = 0; v < 4; v++) out[v] = (ha[v] + hc[v]) + bh[v];  // one of ha / hc is 0 in each row
-    // rows 4..7 (A > 4) from the lanes 16 up
-    f32x4 hi;
+    for (int p = 0; p < PT; p++) {
+      f32x4 out;
 #pragma unroll
-    for (int v = 0; v < 4; v++) hi[v] = __shfl(out[v], (lane + 16) & 63);
-    if (FW_POL_DIAG != 4 && g == 3 && valid) val[env] = out[3];
-    if (g == 0 && valid) {
-      float lp = 0.0f;
+      for (int v = 0; v < 4; v++) out[v] = (ha[p][v] + hc[p][v]) + bh[v];  // one of ha / hc is 0 in each row
+      // rows 4..7 (A > 4) from the lanes 16 up
+      f32x4 hi = out;
+      if constexpr (AM > 4)
 #pragma unroll
-      for (int a = 0; a < POL_MAXA; a++) {
-        if (a < A) {
-          const float m = a < 4 ? out[a & 3] : hi[a & 3];
-          const float ls = lsA[a];
-          const float sd = sdA[a];
-          // the module's arithmetic (rollout.py MlpActorCritic.forward): separate mul / add, as torch's kernels
-          const float ac = noise ? m + sd * cur.z[a] : m;
-          const float dv = ac - m;
-          lp = lp + (((-(dv * dv)) / ((2.0f * sd) * sd) - ls) - half_log_2pi);
-          if (FW_POL_DIAG != 4) act[env * A + a] = ac;
-          if (FW_POL_DIAG != 4 && G.clipped) G.clipped[env * A + a] = fmaxf(fminf(ac, hiA[a]), loA[a]);
+        for (int v = 0; v < 4; v++) hi[v] = __shfl(out[v], (lane + 16) & 63);
+      if (FW_POL_DIAG != 4 && g == 3 && valid[p]) val[env[p]] = out[3];
+      if (g == 0 && valid[p]) {
+        float lp = 0.0f;
+#pragma unroll
+        for (int a = 0; a < AM; a++) {
+          if (a < A) {
+            const float m = a < 4 ? out[a & 3] : hi[a & 3];
+            const float ls = lsA[a];
+            const float sd = sdA[a];
+            // the module's arithmetic (rollout.py MlpActorCritic.forward): separate mul / add, as torch's kernels
+            const float ac = noise ? m + sd * cur[p].z[a] : m;
+            const float dv = ac - m;
+            lp = lp + (((-(dv * dv)) / ((2.0f * sd) * sd) - ls) - half_log_2pi);
+            if (FW_POL_DIAG != 4) act[env[p] * A + a] = ac;
+            if (FW_POL_DIAG != 4 && G.clipped) G.clipped[env[p] * A + a] = fmaxf(fminf(ac, hiA[a]), loA[a]);
+          }
         }
+        if (FW_POL_DIAG != 4) logp[env[p]] = lp;
       }
-      if (FW_POL_DIAG != 4) logp[env] = lp;
     }
   }
 }
@@ -1043,12 +1165,15 @@ int launch_mfma(const PolArgs& G, hipStream_t s) {
   if (int rc = cu_count(&cus)) return rc;
   const int64_t tiles = (G.n + 15) / 16;
   static const int per_cu = std::getenv("FW_POL_BLOCKS_PER_CU") ? std::atoi(std::getenv("FW_POL_BLOCKS_PER_CU")) : 2;
+  const int64_t groups = (tiles + FW_POL_TILES - 1) / FW_POL_TILES;
   const unsigned grid = (unsigned)std::max<int64_t>(
-      1, std::min<int64_t>((tiles + PM_WAVES - 1) / PM_WAVES, (int64_t)cus * std::max(per_cu, 1)));
-  if (G.P.d <= 16)
-    hipLaunchKernelGGL(k_policy_mfma<4>, dim3(grid), dim3(64 * PM_WAVES), PolLds<4>::FLOATS * sizeof(float), s, G);
+      1, std::min<int64_t>((groups + PM_WAVES - 1) / PM_WAVES, (int64_t)cus * std::max(per_cu, 1)));
+  if (G.P.d <= 16 && G.P.act_dim <= 4)
+    hipLaunchKernelGGL((k_policy_mfma<4, 4>), dim3(grid), dim3(64 * PM_WAVES), PolLds<4>::FLOATS * sizeof(float), s, G);
+  else if (G.P.d <= 16)
+    hipLaunchKernelGGL((k_policy_mfma<4, POL_MAXA>), dim3(grid), dim3(64 * PM_WAVES), PolLds<4>::FLOATS * sizeof(float), s, G);
   else
-    hipLaunchKernelGGL(k_policy_mfma<8>, dim3(grid), dim3(64 * PM_WAVES), PolLds<8>::FLOATS * sizeof(float), s, G);
+    hipLaunchKernelGGL((k_policy_mfma<8, POL_MAXA>), dim3(grid), dim3(64 * PM_WAVES), PolLds<8>::FLOATS * sizeof(float), s, G);
   FW_HIP(hipGetLastError());
   return FW_OK;
 }
