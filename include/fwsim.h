@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FWSIM_ABI_VERSION 9
+#define FWSIM_ABI_VERSION 10
 
 /* ---- error codes ---------------------------------------------------------- */
 #define FW_OK 0
@@ -214,7 +214,9 @@ typedef struct fw_env_config {
   double step_fail_value;
   double term_weight[3];              /* per function class (linear, quadratic, exponential) */
   int32_t term_present[3];
-  int32_t pad_;
+  int32_t reward_potential;           /* reward.form "potential" (fixed_wing.py:1080-1108): each term's shaping
+                                       * enters as its change since the env's previous successful step (the
+                                       * first step of an episode: the value alone) */
   fw_rew_factor rew[FW_MAX_REW];
   /* streaming episode metrics (fixed_wing.py:1644-1736), reported per done env through
    * fw_set_metrics_output; 0 = not tracked (no extra state traffic) */

@@ -671,6 +671,10 @@ typedef struct orc_env {
   int32_t has_params;
   double params[FW_NPARAM];
   double params0[FW_NPARAM];
+  /* reward.form "potential": self.prev_shaping per function class (fixed_wing.py:296, 470, 1108);
+   * has_prev = 0 is the reference's None (set by reset) */
+  double prev_shaping[3];
+  int32_t has_prev[3];
 } orc_env;
 
 static void push_hist(double h[FW_MAX_WINDOW][3], int32_t* n, const double* v) {
@@ -789,8 +793,8 @@ void orc_env_observe(const fw_sim_config* c, const fw_env_config* e, const orc_e
   }
 }
 
-/* get_reward fixed_wing.py:941-1111 (form "absolute") */
-static double get_reward(const fw_env_config* e, const orc_env* s, const double* action) {
+/* get_reward fixed_wing.py:941-1111 (forms "absolute" and "potential") */
+static double get_reward(const fw_env_config* e, orc_env* s, const double* action) {
   double term_val[3] = {0, 0, 0}, term_shape[3] = {0, 0, 0};
   for (int f = 0; f < e->n_rew; f++) {
     const fw_rew_factor* F = &e->rew[f];
@@ -831,8 +835,18 @@ static double get_reward(const fw_env_config* e, const orc_env* s, const double*
   for (int k = 0; k < 3; k++) {
     if (!e->term_present[k]) continue;
     double v;
-    if (k == FW_FUN_EXPONENTIAL) v = -1 + exp(term_val[k] + term_shape[k]);
-    else v = term_val[k] + term_shape[k];
+    if (e->reward_potential) {  /* fixed_wing.py:1080-1104 */
+      if (k == FW_FUN_EXPONENTIAL)
+        v = s->has_prev[k] ? -1 + exp(term_val[k] + (term_shape[k] - s->prev_shaping[k])) : -1 + exp(term_val[k]);
+      else
+        v = s->has_prev[k] ? term_val[k] + (term_shape[k] - s->prev_shaping[k]) : term_val[k];
+    } else if (k == FW_FUN_EXPONENTIAL) {
+      v = -1 + exp(term_val[k] + term_shape[k]);
+    } else {
+      v = term_val[k] + term_shape[k];
+    }
+    s->prev_shaping[k] = term_shape[k];  /* :1108, every term of every call */
+    s->has_prev[k] = 1;
     reward += e->term_weight[k] * v;
   }
   return reward;

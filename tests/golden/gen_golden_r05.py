@@ -14,6 +14,9 @@ Fixtures:
   pyfly_short_turb.npz  PyFly trajectories with turbulence_sim_length 8 / 20 / 40 over several chunks
                      (injected noise; PID and random commands)
   env_short_turb.npz FixedWingAircraft episodes with steps_max 40 (turbulence chunk = steps_max = 40)
+  env_potential.npz  FixedWingAircraft episodes with reward.form "potential" (fixed_wing.py:1080-1108: the
+                     shaping terms enter as the change since the previous step), random and PID actions,
+                     turbulence off and light
 
 Usage:  python tests/golden/gen_golden_r05.py
 """
@@ -82,11 +85,32 @@ def gen_env_short():
     np.savez_compressed(os.path.join(OUT, "env_short_turb.npz"), **out)
 
 
+def gen_env_potential():
+    out = {}
+    rng = np.random.RandomState(507)
+    for name, turb, pol, ckw in [("rand_off", False, "rand", None), ("pid_off", False, "pid", {"action": {"scale_space": False}}),
+                                 ("rand_light", True, "rand", None)]:
+        kw = {"reward": {"form": "potential"}}
+        if ckw:
+            kw.update(ckw)
+        env = G.make_env(turb, 300, kw)
+        assert env.cfg["reward"]["form"] == "potential"
+        ep = G.env_episode(env, rng, turb, 300, omega_deg=20.0, policy=pol)
+        for k, v in ep.items():
+            out[name + "__" + k] = v
+        out[name + "__turb"] = np.array(turb)
+        out[name + "__scale_space"] = np.array(ckw is None)
+        print("env potential %s: %d steps, last term=%r" % (name, len(ep["rew"]), ep["term"][-1]))
+    np.savez_compressed(os.path.join(OUT, "env_potential.npz"), **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["dryden", "pyfly", "env"]
+    which = sys.argv[1:] or ["dryden", "pyfly", "env", "potential"]
     if "dryden" in which:
         gen_dryden_short()
     if "pyfly" in which:
         gen_pyfly_short()
     if "env" in which:
         gen_env_short()
+    if "potential" in which:
+        gen_env_potential()

@@ -416,3 +416,34 @@ def test_goal_history_block_transfer():
         assert torch.equal(a.get_block(C.FW_BLK_GOAL), b.get_block(C.FW_BLK_GOAL)), s
         succ += int((ta == C.FW_TERM_SUCCESS).sum())
     assert succ > 0
+
+
+@pytest.mark.parametrize("precision", ["float64", "float32"])
+@pytest.mark.parametrize("name", ["rand_off", "pid_off", "rand_light"])
+def test_env_potential_reward_episode(name, precision):
+    """reward.form "potential" on the device (State::shp, reward_of) against the reference's own episodes
+    (env_potential.npz): done flags identical; fp64 rewards within 1e-6 + 1e-6 / step (the env-level gate of
+    the other episode fixtures), fp32 within 1e-3 (1 + |r|) -- the shaping difference of two fp32 errors."""
+    import _fixtures as F
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
+    d = F.load("env_potential.npz")
+    g = lambda k: d[name + "__" + k]  # noqa: E731
+    ckw = {"steps_max": 300, "reward": {"form": "potential"}}
+    if not bool(g("scale_space")):
+        ckw["action"] = {"scale_space": False}
+    turb = bool(g("turb"))
+    spec = C.EnvSpec(config_kw=ckw, sim_config_kw={"turbulence": turb, "turbulence_intensity": "light"})
+    eng = Engine(spec.sim, spec, 1, device=DEV, precision=precision)
+    if turb:
+        eng.set_noise(g("noise")[None])
+    eng.reset(init=F.env_init(g("init"))[:, None], target=g("target0")[:, None])
+    acts = torch.tensor(g("act"), dtype=eng.dtype, device=DEV)
+    for s in range(len(acts)):
+        _, rew, done, _ = eng.env_step(acts[s:s + 1], auto_reset=False)
+        assert bool(done[0]) == bool(g("done")[s]), s
+        r, ref = float(rew[0]), float(g("rew")[s])
+        tol = (1e-6 + 1e-6 * s) if precision == "float64" else 1e-3 * (1 + abs(ref))
+        assert abs(r - ref) <= tol, (s, r, ref)
+        if bool(done[0]):
+            break
+    eng.close()

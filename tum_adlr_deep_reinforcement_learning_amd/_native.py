@@ -22,7 +22,7 @@ SOURCES = UNITS + [os.path.join(CSRC, "fw_device.hpp"), os.path.join(CSRC, "fw_q
 ARCH = os.environ.get("FWSIM_ARCH", "gfx950")
 
 _lib = None
-ABI_VERSION = 9  # include/fwsim.h FWSIM_ABI_VERSION
+ABI_VERSION = 10  # include/fwsim.h FWSIM_ABI_VERSION
 
 
 class FwError(RuntimeError):

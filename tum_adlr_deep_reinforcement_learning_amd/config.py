@@ -147,7 +147,7 @@ class FwEnvConfig(ctypes.Structure):
                 ("n_rew", ctypes.c_int32), ("step_fail_timesteps", ctypes.c_int32),
                 ("step_fail_value", ctypes.c_double),
                 ("term_weight", ctypes.c_double * 3), ("term_present", ctypes.c_int32 * 3),
-                ("pad_", ctypes.c_int32),
+                ("reward_potential", ctypes.c_int32),
                 ("rew", FwRewFactor * FW_MAX_REW),
                 ("metrics", ctypes.c_int32), ("pad2_", ctypes.c_int32),
                 ("rise_low", ctypes.c_double), ("rise_high", ctypes.c_double),
@@ -570,8 +570,8 @@ class EnvSpec:
             self.obs_noise = (float(noise.get("mean", 0)), float(noise.get("var", 0)))
         if cfg.get("integration_window", 0):
             raise NotImplementedError("integration_window")
-        if cfg["reward"].get("form", "absolute") != "absolute":
-            raise NotImplementedError("reward.form other than 'absolute'")
+        if cfg["reward"].get("form", "absolute") not in ("absolute", "potential"):
+            raise NotImplementedError("reward.form %r" % cfg["reward"].get("form"))
         if cfg["reward"].get("randomize_scaling", False):
             raise NotImplementedError("reward.randomize_scaling")
         if cfg["target"].get("resample_every", 0):
@@ -824,6 +824,7 @@ class EnvSpec:
         fails = r.get("step_fail", 0)
         e.step_fail_timesteps = int(fails == "timesteps")
         e.step_fail_value = 0.0 if fails == "timesteps" else float(fails)
+        e.reward_potential = int(r.get("form", "absolute") == "potential")  # fixed_wing.py:566, 1080-1108
         for term in r["terms"]:
             fc = term["function_class"]
             if fc not in FW_FUN:

@@ -141,6 +141,7 @@ struct DevCfg {
   T term_weight[3];
   int term_present[3];
   int metrics;                         // streaming episode metrics tracked (fw_env_config.metrics)
+  int reward_potential;                // reward.form "potential" (fw_env_config.reward_potential)
   T rise_low, rise_high;
   int obs_len, obs_step, obs_hist;     // observation rows, their spacing, past rows kept (0: no history)
   int obs_noise;                       // observation.noise drawn

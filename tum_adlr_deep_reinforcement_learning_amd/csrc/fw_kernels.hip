@@ -113,6 +113,8 @@ struct State {
                       // (below).  Starting at LIFE0 >= 2^16 + any window keeps life - steps_count - window > 0
                       // whatever FW_BLK_STEPS a caller sets, so no slot expression wraps below 0.
   T* dry;             // [12][ld] Dryden filter-bank state of the current step (short chunks; null: FIR or off)
+  T* shp;             // [3][ld] reward.form "potential": the previous step's shaping per function class (NaN =
+                      // the reference's None, after a reset), or null
   const T* noise;     // injected N(0,1) turbulence noise [4][noise_len][ld] or null
   int64_t noise_len;
   int32_t* noise_env_len;  // [ld] per-env injected length (0: Philox; zeroed by the auto-reset) or null: all
@@ -460,8 +462,10 @@ __device__ __forceinline__ void observe_env(const C& c, const State<T>& s, int64
 
 // get_reward (fixed_wing.py:941-1111), form "absolute"
 template <typename T>
+// shp: with reward.form "potential", the previous step's shaping per function class (NaN = None) on input,
+// this step's on output (fixed_wing.py:1080-1108); null for "absolute"
 __device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* der, const T* tgt, int steps,
-                                       const T (*seqA)[3]) {
+                                       const T (*seqA)[3], T* shp = nullptr) {
   T tv[3] = {T(0), T(0), T(0)}, ts[3] = {T(0), T(0), T(0)};
   for (int f = 0; f < c.n_rew; f++) {
     const fw_rew_factor F = c.rew[f];
@@ -508,7 +512,15 @@ __device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* 
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     if (!c.term_present[k]) continue;
-    const T v = (k == FW_FUN_EXPONENTIAL) ? T(-1) + exp(tv[k] + ts[k]) : tv[k] + ts[k];
+    T v;
+    if (shp) {  // potential: the shaping's change since the previous step, or nothing after a reset
+      const T prev = shp[k];
+      const T a = isnan(prev) ? tv[k] : tv[k] + (ts[k] - prev);
+      v = (k == FW_FUN_EXPONENTIAL) ? T(-1) + exp(a) : a;
+      shp[k] = ts[k];
+    } else {
+      v = (k == FW_FUN_EXPONENTIAL) ? T(-1) + exp(tv[k] + ts[k]) : tv[k] + ts[k];
+    }
     r += c.term_weight[k] * v;
   }
   return r;
@@ -850,6 +862,9 @@ __device__ __forceinline__ void store_env_fresh(const DevCfg<T>& c, const State<
     for (int k = 0; k < 3; k++) st_(s.target, k, ld, i, tgt[k]);
     goal_init(c, s, i, tgt, der, lep);
     st_(s.ep_ret, 0, ld, i, T(0));
+    if (s.shp)  // self.prev_shaping[*] = None (fixed_wing.py:469-470)
+#pragma unroll
+      for (int k = 0; k < 3; k++) st_(s.shp, k, ld, i, T(NAN));
   }
   s.steps[i] = 0u;
 }
@@ -1044,6 +1059,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   Met<T> M;
   T prev_cmd[3];
   T ep_ret0;
+  T shp[3] = {T(0), T(0), T(0)};  // reward.form "potential": the previous step's shaping (State::shp)
   auto load_epilogue = [&]() {
     life0 = s.life[i];
     lep = life0 - (uint32_t)steps0;
@@ -1086,6 +1102,9 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
       }
     }
     ep_ret0 = ld_(s.ep_ret, 0, ld, i);
+    if (s.shp)
+#pragma unroll
+      for (int k = 0; k < 3; k++) shp[k] = ld_(s.shp, k, ld, i);
   };
   if constexpr (PREF) load_epilogue();
 
@@ -1183,7 +1202,13 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
       }
     }
     if (goal_on || c.metrics) st_(s.goal, GB_N, ld, i, b + 1u);
-    reward = reward_of(c, y, der, tgt, steps, seqA);
+    if (s.shp) {
+      reward = reward_of(c, y, der, tgt, steps, seqA, shp);
+#pragma unroll
+      for (int k = 0; k < 3; k++) st_(s.shp, k, ld, i, shp[k]);
+    } else {
+      reward = reward_of(c, y, der, tgt, steps, seqA);
+    }
     next_target(c, steps_tgt, tgt);
 #ifndef FW_MET_SKIP_STEP
     if (c.metrics) metrics_step(c, s, i, M, tgt, vals, gb, gcnt, b, lep);
@@ -1647,6 +1672,7 @@ struct fw_handle {
   size_t o_obs_init = 0, o_obs_ring = 0;
   size_t o_prm = 0;         // per-aircraft parameter rows (env->n_rand > 0 at create; 0 = none)
   size_t o_dry = 0;         // Dryden filter-bank state rows (turbulence on at create; 0 = none)
+  size_t o_shp = 0;         // potential-form shaping rows (env->reward_potential at create; 0 = none)
   int rand_active = 0;      // the current config randomises parameters (kernels read the rows)
   int lanes_opt = FW_LANES_AUTO;  // fw_set_lanes: 0 = automatic, 1, 4
   int quad_ok = 1;          // the config allows the quad integrator (no wrapped ODE-state variable)
@@ -1826,6 +1852,7 @@ void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
     d.streak_frac = (T)e.streak_frac;
     d.step_fail_value = (T)e.step_fail_value;
     d.metrics = h->metrics && e.metrics;
+    d.reward_potential = e.reward_potential ? 1 : 0;
     d.rise_low = (T)e.rise_low;
     d.rise_high = (T)e.rise_high;
     d.obs_len = e.obs_length > 1 ? e.obs_length : 1;
@@ -2033,6 +2060,7 @@ State<T> state_of(const fw_handle* h) {
   s.obs_ring = h->obs_hist ? (T*)(b + h->o_obs_ring) : nullptr;
   s.prm = h->o_prm ? (T*)(b + h->o_prm) : nullptr;
   s.dry = (h->o_dry && h->sim.turbulence && h->sim.dryden_state) ? (T*)(b + h->o_dry) : nullptr;
+  s.shp = (h->o_shp && h->has_env && h->env.reward_potential) ? (T*)(b + h->o_shp) : nullptr;
   s.col_ret = h->col.ret;
   s.col_gamma = h->col.gamma;
   s.col_rec = h->col.records;
@@ -2174,6 +2202,9 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
   if (sim->turbulence) {  // Dryden filter-bank state (used when the chunk is too short for the FIR)
     h->o_dry = off; off += (size_t)12 * row;
   }
+  if (env && env->reward_potential) {  // the previous step's reward shaping (reward.form "potential")
+    h->o_shp = off; off += (size_t)3 * row;
+  }
   if (env && env->n_rand > 0) {  // per-aircraft parameters (simulator parameter randomisation)
     h->o_prm = off; off += (size_t)FW_NPARAM * row;
   }
@@ -2287,6 +2318,8 @@ int fw_update_config(fw_handle* h, const fw_sim_config* sim, const fw_env_config
       return set_err(FW_E_UNSUPPORTED, "episode metrics must be enabled when the handle is created");
     if (env->n_rand > 0 && !h->o_prm)
       return set_err(FW_E_UNSUPPORTED, "parameter randomisation must be enabled when the handle is created");
+    if (env->reward_potential && !h->o_shp)
+      return set_err(FW_E_UNSUPPORTED, "reward.form \"potential\" must be set when the handle is created");
     h->env = *env;
   }
   if (sim->turbulence && sim->dryden_state && !h->o_dry)
