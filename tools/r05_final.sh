@@ -24,3 +24,7 @@ BENCH_ARGS="--steps 20 --warmup 5 --no-cpu-baseline --long-window 0 --no-open-lo
   bash tools/traffic.sh || exit $?
 cp profiles/pmc_env_step.json "$OUT/pmc_env_step.json"
 bash tools/collect_prof.sh "$(basename $OUT)_collect" || exit $?
+# review item 5: SQ counters of the fp64 vs fp32 one-lane env step over the same tail protocol (40 launches)
+for prec in float32 float64; do
+  TAIL_PREC=$prec TAIL_STEPS=40 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --output-format csv -d "$OUT/pmc_$prec" -- python3 tools/tail.py > "$OUT/pmc_$prec.log" 2>&1 || exit $?
+done
