@@ -724,7 +724,18 @@ struct PolArgs {
   int64_t n;
 };
 
-constexpr int PM_WAVES = 4;  // waves per block; two blocks per CU (two waves per SIMD)
+#ifndef FW_POL_VHEADS
+// 1: the 4-action / 8-wave instance computes the heads (<= 4 actor rows + the critic row) on the VALU -- 80
+// multiply-adds per lane and a butterfly over the four lane groups -- instead of 32 MFMAs of which 12 of 16
+// output rows are padding (A/B: tools/r05_pol.sh)
+#define FW_POL_VHEADS 0
+#endif
+#ifndef FW_POL_WAVES
+// waves per block of the k_policy_mfma instance of SB3's default shapes (d <= 16, act_dim <= 4); two blocks per
+// CU share the CU's LDS (one weight image each).  8: four resident waves per SIMD at <= 128 VGPRs (one 16-env
+// tile per wave at 65536 envs); 4: two per SIMD (the wider instances, whose registers do not fit 128)
+#define FW_POL_WAVES 8
+#endif
 #ifndef FW_POL_STAGGER
 #define FW_POL_STAGGER 0  // s_sleep units (64 cycles) the second half of the grid waits (A/B, below)
 #endif
@@ -757,68 +768,85 @@ __device__ __forceinline__ float norm_obs_val(float o, double mean, double den, 
 template <int S>
 struct PolLds {
   static constexpr int L1 = 0, L0 = L1 + 2 * 4 * 4 * 64 * 4, HD = L0 + 2 * 4 * 64 * S, B = HD + 2 * 4 * 64 * 4,
-                       BH = B + 2 * 2 * 4 * 16, FLOATS = BH + 16;
+                       BH = B + 2 * 2 * 4 * 16, NRM = BH + 16, HV = NRM + 2 * 2 * 4 * S, FLOATS = HV + 4 * 5 * 16;
+  // HV: the heads for the VALU form (FW_POL_VHEADS): [g][row][16] with rows 0..3 = actor rows (0 past act_dim),
+  // row 4 = the critic; entry 4 T + v of lane group g = hidden unit 16 T + 4 g + v (the layer-1 B-operand slot)
+  // NRM: the VecNormalize mean and sqrt(var + eps) of features 0 .. 4 S - 1 as doubles (8-wave blocks read
+  // them from here instead of holding them in VGPRs)
+  static_assert(NRM % 2 == 0, "NRM holds doubles");
 };
 
 // The image is filled region by region with unrolled, independent loads (a load-then-store loop with a region
 // switch in its body issued one global load per iteration and waited for each: ~15 us of a 34-us launch).
-template <int S>
+template <int S, int PM_WAVES>
 __device__ __forceinline__ void pol_fill_lds(const fw_mlp_policy& P, float* W) {
   using L = PolLds<S>;
-  static_assert(64 * PM_WAVES == 256, "fill strides assume 256 threads");
-  const int d = P.d, A = P.act_dim, H = POL_MAXH, t = threadIdx.x;
+  constexpr int NT = 64 * PM_WAVES;  // threads of the block; every region below is a multiple of 256 entries
+  const int d = P.d, A = P.act_dim, H = POL_MAXH, t0 = threadIdx.x;
   const float K2 = 2.8853900817779268f;  // 2 log2(e): tanh(x) = 1 - 2 / (exp2(K2 x) + 1)
-  {  // L1: 2048 float4 fragments, 8 per thread; fragment q = ((net * 4 + O) * 4 + T) * 64 + l
-    f32x4 v[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const int q = t + 256 * k, l = q & 63, T = (q >> 6) & 3, O = (q >> 8) & 3, net = q >> 10;
-      const float* w = net ? P.vf_w1 : P.pi_w1;
-      v[k] = *reinterpret_cast<const f32x4*>(w + (16 * O + (l & 15)) * H + 16 * T + 4 * (l >> 4));
+  for (int base = 0; base < 256; base += NT) {  // (NT = 256: one pass; NT = 512: the upper half idles)
+    const int t = t0 + base;
+    if (NT > 256 && t >= 256) break;
+    {  // L1: 2048 float4 fragments, 8 per 256-thread stripe; fragment q = ((net * 4 + O) * 4 + T) * 64 + l
+      f32x4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int q = t + 256 * k, l = q & 63, T = (q >> 6) & 3, O = (q >> 8) & 3, net = q >> 10;
+        const float* w = net ? P.vf_w1 : P.pi_w1;
+        v[k] = *reinterpret_cast<const f32x4*>(w + (16 * O + (l & 15)) * H + 16 * T + 4 * (l >> 4));
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) *reinterpret_cast<f32x4*>(W + L::L1 + 4 * (t + 256 * k)) = K2 * v[k];
     }
+    {  // L0: 512 S floats, 2 S per stripe; element q = ((net * 4 + O) * 64 + l) * S + s
+      float v[2 * S];
 #pragma unroll
-    for (int k = 0; k < 8; k++) *reinterpret_cast<f32x4*>(W + L::L1 + 4 * (t + 256 * k)) = K2 * v[k];
-  }
-  {  // L0: 512 S floats, 2 S per thread; element q = ((net * 4 + O) * 64 + l) * S + s
-    float v[2 * S];
+      for (int k = 0; k < 2 * S; k++) {
+        const int q = t + 256 * k, sidx = q % S, l = (q / S) & 63, O = (q / (S * 64)) & 3, net = q / (S * 256);
+        const int f = 4 * sidx + (l >> 4);
+        const float* w = net ? P.vf_w0 : P.pi_w0;
+        v[k] = w[(16 * O + (l & 15)) * d + (f < d ? f : d - 1)];
+        v[k] = f < d ? K2 * v[k] : 0.0f;
+      }
 #pragma unroll
-    for (int k = 0; k < 2 * S; k++) {
-      const int q = t + 256 * k, sidx = q % S, l = (q / S) & 63, O = (q / (S * 64)) & 3, net = q / (S * 256);
-      const int f = 4 * sidx + (l >> 4);
-      const float* w = net ? P.vf_w0 : P.pi_w0;
-      v[k] = w[(16 * O + (l & 15)) * d + (f < d ? f : d - 1)];
-      v[k] = f < d ? K2 * v[k] : 0.0f;
+      for (int k = 0; k < 2 * S; k++) W[L::L0 + t + 256 * k] = v[k];
     }
+    {  // HD: 512 float4 fragments, 2 per stripe; fragment q = (net * 4 + T) * 64 + l (row r = l & 15)
+      f32x4 v[2];
 #pragma unroll
-    for (int k = 0; k < 2 * S; k++) W[L::L0 + t + 256 * k] = v[k];
-  }
-  {  // HD: 512 float4 fragments, 2 per thread; fragment q = (net * 4 + T) * 64 + l (row r = l & 15)
-    f32x4 v[2];
+      for (int k = 0; k < 2; k++) {
+        const int q = t + 256 * k, l = q & 63, T = (q >> 6) & 3, net = q >> 8, r = l & 15;
+        const int kk = 16 * T + 4 * (l >> 4);
+        const float* src = net ? P.val_w + kk : P.act_w + (r < A ? r : 0) * H + kk;
+        v[k] = *reinterpret_cast<const f32x4*>(src);
+        if (net ? r != 15 : r >= A) v[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      }
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
-      const int q = t + 256 * k, l = q & 63, T = (q >> 6) & 3, net = q >> 8, r = l & 15;
-      const int kk = 16 * T + 4 * (l >> 4);
-      const float* src = net ? P.val_w + kk : P.act_w + (r < A ? r : 0) * H + kk;
-      v[k] = *reinterpret_cast<const f32x4*>(src);
-      if (net ? r != 15 : r >= A) v[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      for (int k = 0; k < 2; k++) *reinterpret_cast<f32x4*>(W + L::HD + 4 * (t + 256 * k)) = v[k];
     }
-#pragma unroll
-    for (int k = 0; k < 2; k++) *reinterpret_cast<f32x4*>(W + L::HD + 4 * (t + 256 * k)) = v[k];
+    {  // B: 256 floats, one per stripe entry; q = ((layer * 2 + net) * 4 + O) * 16 + u
+      const int u = t & 15, O = (t >> 4) & 3, net = (t >> 6) & 1, layer = t >> 7;
+      const float* b = layer ? (net ? P.vf_b1 : P.pi_b1) : (net ? P.vf_b0 : P.pi_b0);
+      W[L::B + t] = K2 * b[16 * O + u];
+    }
   }
-  {  // B: 256 floats, one per thread; q = ((layer * 2 + net) * 4 + O) * 16 + u
-    const int u = t & 15, O = (t >> 4) & 3, net = (t >> 6) & 1, layer = t >> 7;
-    const float* b = layer ? (net ? P.vf_b1 : P.pi_b1) : (net ? P.vf_b0 : P.pi_b0);
-    W[L::B + t] = K2 * b[16 * O + u];
-  }
+  const int t = t0;
   if (t < 16) W[L::BH + t] = t < A ? P.act_b[t] : (t == 15 ? P.val_b[0] : 0.0f);
+  for (int q = t; q < 4 * 5 * 16; q += NT) {  // HV
+    const int gq = q / 80, r = (q / 16) % 5, kk = q % 16, u = 16 * (kk >> 2) + 4 * gq + (kk & 3);
+    W[L::HV + q] = r < 4 ? (r < A ? P.act_w[r * H + u] : 0.0f) : P.val_w[u];
+  }
   __syncthreads();
 }
 
 __device__ __forceinline__ f32x4 lds4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
-// S: k-steps of 4 observation features (d <= 4 S); AM: actions held per lane (act_dim <= AM, 4 or POL_MAXA)
-template <int S, int AM = POL_MAXA>
-__global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
+// S: k-steps of 4 observation features (d <= 4 S); AM: actions held per lane (act_dim <= AM, 4 or POL_MAXA);
+// PM_WAVES: waves per block (4 or 8; two blocks per CU)
+template <int S, int AM, int PM_WAVES>
+__global__ __launch_bounds__(64 * PM_WAVES, PM_WAVES / 2) void k_policy_mfma(PolArgs G) {  // (min waves per SIMD)
+  constexpr bool FW_POL_DBUF_ = PM_WAVES <= 4;  // layer-1 fragments double-buffered in VGPRs (32 extra)
   using L = PolLds<S>;
   extern __shared__ float Wl[];
   const int lane = threadIdx.x & 63;
@@ -839,7 +867,8 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
   // The prologue's loads are issued together from clamped, valid addresses under wave-uniform conditions, then
   // selected: a load per feature / action under its own lane condition compiled to a branch with a wait each,
   // eight dependent round trips before the first tile (fp64 statistics) plus the action constants.
-  double mean[S], den[S];
+  constexpr bool NRM_LDS = PM_WAVES > 4;  // (register budget of four waves per SIMD)
+  double mean[NRM_LDS ? 1 : S], den[NRM_LDS ? 1 : S];
   const bool nrew = G.rms && G.norm_rew;
   double rvar = 0.0;
   if (nobs || nrew) {
@@ -851,17 +880,29 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
       vr[s] = G.rms[d + fc];
     }
     rvar = G.rms[2 * d + 2];
+    if constexpr (!NRM_LDS) {
 #pragma unroll
-    for (int s = 0; s < S; s++) {
-      const bool on = nobs && 4 * s + g < d;
-      mean[s] = on ? mr[s] : 0.0;
-      den[s] = on ? sqrt(vr[s] + G.eps) : 1.0;
+      for (int s = 0; s < S; s++) {
+        const bool on = nobs && 4 * s + g < d;
+        mean[s] = on ? mr[s] : 0.0;
+        den[s] = on ? sqrt(vr[s] + G.eps) : 1.0;
+      }
+    } else if (threadIdx.x < 64 && c16 == 0) {  // lanes 0, 16, 32, 48 of wave 0: features 4 s + g
+      double* nl = reinterpret_cast<double*>(Wl + L::NRM);
+#pragma unroll
+      for (int s = 0; s < S; s++) {
+        const bool on = nobs && 4 * s + g < d;
+        nl[4 * s + g] = on ? mr[s] : 0.0;
+        nl[4 * S + 4 * s + g] = on ? sqrt(vr[s] + G.eps) : 1.0;
+      }
     }
   } else {
+    if constexpr (!NRM_LDS) {
 #pragma unroll
-    for (int s = 0; s < S; s++) {
-      mean[s] = 0.0;
-      den[s] = 1.0;
+      for (int s = 0; s < S; s++) {
+        mean[s] = 0.0;
+        den[s] = 1.0;
+      }
     }
   }
   const double rden = nrew ? sqrt(rvar + G.eps) : 1.0;
@@ -942,7 +983,7 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
 #pragma unroll
   for (int p = 0; p < PT; p++) fetch(wid * PT + p, nxt[p]);
   // the block's weight image after the first tiles' loads are issued (their latency hides under the fill)
-  if (FW_POL_DIAG != 3) pol_fill_lds<S>(G.P, Wl);
+  if (FW_POL_DIAG != 3) pol_fill_lds<S, PM_WAVES>(G.P, Wl);
 #if FW_POL_STAGGER
   // A/B (tools/r05_pol.sh): the CU's second block starts FW_POL_STAGGER x 64 cycles late, so its waves' tanh
   // phases meet their SIMD partners' MFMA phases instead of running in lockstep with them
@@ -969,7 +1010,14 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
       for (int s = 0; s < S; s++) {
         const int f = 4 * s + g;
         float o = (valid[p] && f < d) ? cur[p].o[s] : 0.0f;
-        if (FW_POL_DIAG != 5 && nobs && valid[p] && f < d) o = norm_obs_val(o, mean[s], den[s], G.clip_obs);
+        if (FW_POL_DIAG != 5 && nobs && valid[p] && f < d) {
+          if constexpr (NRM_LDS) {
+            const double* nl = reinterpret_cast<const double*>(Wl + L::NRM);
+            o = norm_obs_val(o, nl[f], nl[4 * S + f], G.clip_obs);
+          } else {
+            o = norm_obs_val(o, mean[s], den[s], G.clip_obs);
+          }
+        }
         x[p][s] = o;
         if (FW_POL_DIAG != 4 && obs_rows && valid[p] && f < d) obs_rows[env[p] * d + f] = o;
       }
@@ -1033,19 +1081,30 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
         cv[p][O] = bv;
       }
     }
-    // the k-step group T + 1's eight fragments are read while group T's MFMAs issue (registers, double
-    // buffered); MFMAs round-robin over the eight accumulators; per accumulator the order (T, then v) is unchanged
+    // the k-step group T + 1's eight fragments are read while group T's MFMAs issue (FW_POL_DBUF: registers,
+    // double buffered); MFMAs round-robin over the eight accumulators; per accumulator the order (T, then v)
+    // is unchanged
+    if constexpr (PM_WAVES <= 4) {
     {
-      f32x4 ap[2][4], av[2][4];
+      constexpr int NB = FW_POL_DBUF_ ? 2 : 1;
+      f32x4 ap[NB][4], av[NB][4];
+      if constexpr (NB == 2) {
 #pragma unroll
-      for (int O = 0; O < 4; O++) {
-        ap[0][O] = lds4(W1 + ((0 * 4 + O) * 4 + 0) * 256);
-        av[0][O] = lds4(W1 + ((1 * 4 + O) * 4 + 0) * 256);
+        for (int O = 0; O < 4; O++) {
+          ap[0][O] = lds4(W1 + ((0 * 4 + O) * 4 + 0) * 256);
+          av[0][O] = lds4(W1 + ((1 * 4 + O) * 4 + 0) * 256);
+        }
       }
 #pragma unroll
       for (int T = 0; T < 4; T++) {
-        const int cb = T & 1, nb = cb ^ 1;
-        if (T < 3) {
+        const int cb = NB == 2 ? (T & 1) : 0, nb = NB == 2 ? (cb ^ 1) : 0;
+        if (NB == 1) {
+#pragma unroll
+          for (int O = 0; O < 4; O++) {
+            ap[0][O] = lds4(W1 + ((0 * 4 + O) * 4 + T) * 256);
+            av[0][O] = lds4(W1 + ((1 * 4 + O) * 4 + T) * 256);
+          }
+        } else if (T < 3) {
 #pragma unroll
           for (int O = 0; O < 4; O++) {
             ap[nb][O] = lds4(W1 + ((0 * 4 + O) * 4 + T + 1) * 256);
@@ -1073,6 +1132,21 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
             }
       }
     }
+    } else {  // (8-wave blocks: two fragments at a time, the round-4 order; the same per-accumulator order)
+#pragma unroll
+      for (int T = 0; T < 4; T++)
+#pragma unroll
+        for (int O = 0; O < 4; O++) {
+          const f32x4 ap = lds4(W1 + ((0 * 4 + O) * 4 + T) * 256), av = lds4(W1 + ((1 * 4 + O) * 4 + T) * 256);
+#pragma unroll
+          for (int v = 0; v < 4; v++)
+#pragma unroll
+            for (int p = 0; p < PT; p++) {
+              cp[p][O] = mfma4(ap[v], hpv[p][T][v], cp[p][O]);
+              cv[p][O] = mfma4(av[v], hvv[p][T][v], cv[p][O]);
+            }
+        }
+    }
 #pragma unroll
     for (int p = 0; p < PT; p++)
 #pragma unroll
@@ -1082,6 +1156,7 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
           hpv[p][T][v] = FW_POL_DIAG == 1 ? cp[p][T][v] : ftanh2(cp[p][T][v]);
           hvv[p][T][v] = FW_POL_DIAG == 1 ? cv[p][T][v] : ftanh2(cv[p][T][v]);
         }
+    constexpr bool VH = FW_POL_VHEADS && AM <= 4 && PM_WAVES > 4;
     // ---- heads: actor rows 0..A-1 and the value row 15 of one tile (two accumulators, disjoint rows)
     f32x4 ha[PT], hc[PT];
 #pragma unroll
@@ -1089,16 +1164,41 @@ __global__ __launch_bounds__(64 * PM_WAVES, 2) void k_policy_mfma(PolArgs G) {
       ha[p] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
       hc[p] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     }
+    if constexpr (VH) {
+      // VALU form: lane group g's partial dot products over its 16 hidden units (order T, v), then the sum over
+      // the four groups as a butterfly (the same bits on every lane)
+      const float* hvw = Wl + L::HV + g * 80;
 #pragma unroll
-    for (int T = 0; T < 4; T++) {
-      const f32x4 ap = lds4(WH + (0 * 4 + T) * 256), av = lds4(WH + (1 * 4 + T) * 256);
-#pragma unroll
-      for (int v = 0; v < 4; v++)
+      for (int r = 0; r < 5; r++) {
+        const f32x4 w0 = lds4(hvw + 16 * r), w1 = lds4(hvw + 16 * r + 4), w2 = lds4(hvw + 16 * r + 8),
+                    w3 = lds4(hvw + 16 * r + 12);
+        const f32x4 wr[4] = {w0, w1, w2, w3};
 #pragma unroll
         for (int p = 0; p < PT; p++) {
-          ha[p] = mfma4(ap[v], hpv[p][T][v], ha[p]);
-          hc[p] = mfma4(av[v], hvv[p][T][v], hc[p]);
+          float acc = 0.0f;
+#pragma unroll
+          for (int T = 0; T < 4; T++)
+#pragma unroll
+            for (int v = 0; v < 4; v++) acc = fmaf(wr[T][v], r < 4 ? hpv[p][T][v] : hvv[p][T][v], acc);
+          acc += __shfl_xor(acc, 16);
+          acc += __shfl_xor(acc, 32);
+          // the MFMA form's C layout: lane group 0 holds actor rows 0..3, group 3 row 15 (the critic)
+          if (r < 4) ha[p][r] = g == 0 ? acc : 0.0f;
+          else hc[p][3] = g == 3 ? acc : 0.0f;
         }
+      }
+    } else {
+#pragma unroll
+      for (int T = 0; T < 4; T++) {
+        const f32x4 ap = lds4(WH + (0 * 4 + T) * 256), av = lds4(WH + (1 * 4 + T) * 256);
+#pragma unroll
+        for (int v = 0; v < 4; v++)
+#pragma unroll
+          for (int p = 0; p < PT; p++) {
+            ha[p] = mfma4(ap[v], hpv[p][T][v], ha[p]);
+            hc[p] = mfma4(av[v], hvv[p][T][v], hc[p]);
+          }
+      }
     }
     const f32x4 bh = lds4(Wl + L::BH + 4 * g);
 #pragma unroll
@@ -1165,15 +1265,18 @@ int launch_mfma(const PolArgs& G, hipStream_t s) {
   if (int rc = cu_count(&cus)) return rc;
   const int64_t tiles = (G.n + 15) / 16;
   static const int per_cu = std::getenv("FW_POL_BLOCKS_PER_CU") ? std::atoi(std::getenv("FW_POL_BLOCKS_PER_CU")) : 2;
+  const bool small = G.P.d <= 16 && G.P.act_dim <= 4;  // SB3's default shapes for this env
+  const int waves = small ? FW_POL_WAVES : 4;
   const int64_t groups = (tiles + FW_POL_TILES - 1) / FW_POL_TILES;
   const unsigned grid = (unsigned)std::max<int64_t>(
-      1, std::min<int64_t>((groups + PM_WAVES - 1) / PM_WAVES, (int64_t)cus * std::max(per_cu, 1)));
-  if (G.P.d <= 16 && G.P.act_dim <= 4)
-    hipLaunchKernelGGL((k_policy_mfma<4, 4>), dim3(grid), dim3(64 * PM_WAVES), PolLds<4>::FLOATS * sizeof(float), s, G);
+      1, std::min<int64_t>((groups + waves - 1) / waves, (int64_t)cus * std::max(per_cu, 1)));
+  if (small)
+    hipLaunchKernelGGL((k_policy_mfma<4, 4, FW_POL_WAVES>), dim3(grid), dim3(64 * FW_POL_WAVES),
+                       PolLds<4>::FLOATS * sizeof(float), s, G);
   else if (G.P.d <= 16)
-    hipLaunchKernelGGL((k_policy_mfma<4, POL_MAXA>), dim3(grid), dim3(64 * PM_WAVES), PolLds<4>::FLOATS * sizeof(float), s, G);
+    hipLaunchKernelGGL((k_policy_mfma<4, POL_MAXA, 4>), dim3(grid), dim3(256), PolLds<4>::FLOATS * sizeof(float), s, G);
   else
-    hipLaunchKernelGGL((k_policy_mfma<8, POL_MAXA>), dim3(grid), dim3(64 * PM_WAVES), PolLds<8>::FLOATS * sizeof(float), s, G);
+    hipLaunchKernelGGL((k_policy_mfma<8, POL_MAXA, 4>), dim3(grid), dim3(256), PolLds<8>::FLOATS * sizeof(float), s, G);
   FW_HIP(hipGetLastError());
   return FW_OK;
 }
