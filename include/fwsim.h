@@ -221,7 +221,9 @@ typedef struct fw_env_config {
   /* streaming episode metrics (fixed_wing.py:1644-1736), reported per done env through
    * fw_set_metrics_output; 0 = not tracked (no extra state traffic) */
   int32_t metrics;
-  int32_t pad2_;
+  int32_t resample_every;             /* target.resample_every (fixed_wing.py:570-574): > 0 draws new targets
+                                       * (sample_target, :654-746, from the handle's Philox streams) once the
+                                       * current ones have been held that many steps; 0 = never */
   double rise_low, rise_high;         /* rise_time metric "low" / "high" (defaults 0.1, 0.9) */
   /* observation.length / step / noise (get_observation, fixed_wing.py:1113-1262).  The
    * observation of one env is obs_length rows of n_obs entries (row r = lag 1 + r * obs_step),

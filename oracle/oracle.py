@@ -136,6 +136,10 @@ class OracleEnv:
     """One FixedWingAircraft (fixed_wing.py:483-628) on the CPU oracle."""
 
     def __init__(self, sim_cfg, env_cfg, n_obs):
+        if getattr(env_cfg, "resample_every", 0):
+            # the device draws resampled targets from its Philox streams, the reference from np_random: no
+            # common sequence to restate (tests/test_gpu_r05.py checks the device's draws structurally)
+            raise NotImplementedError("oracle: target.resample_every")
         self.L = lib()
         self.sim_cfg, self.env_cfg, self.n_obs = sim_cfg, env_cfg, n_obs
         self.buf = ctypes.create_string_buffer(self.L.orc_env_state_size())

@@ -447,3 +447,54 @@ def test_env_potential_reward_episode(name, precision):
         if bool(done[0]):
             break
     eng.close()
+
+
+def test_target_resample_every():
+    """target.resample_every (fixed_wing.py:570-574, sample_target :654-746): after every `resample_every` steps
+    with the same targets the env draws new ones -- U(low, high) narrowed to the post-step value -+ delta --
+    and the target step count restarts (FW_BLK_STEPS >> 16).  The constant-class roll / pitch targets change
+    exactly at those steps and stay inside their intervals; a second engine with the same seed draws the same
+    targets (the reference draws from np_random: distribution-level parity only, parity unpinned)."""
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
+    R = 25
+    spec = C.EnvSpec(config_kw={"steps_max": 400, "target": {"resample_every": R}},
+                     sim_config_kw={"turbulence": False})
+    assert spec.struct().resample_every == R
+    n = 256
+    a, b = (Engine(spec.sim, spec, n, device=DEV, precision="float64") for _ in range(2))
+    for e in (a, b):
+        e.seed(21)
+        e.reset()
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(5)
+    e = spec.struct()
+    lo, hi, dl = (np.array(list(v))[:2] for v in (e.target_low, e.target_high, e.target_delta))
+    alive = np.ones(n, bool)
+    tprev = a.get_block(C.FW_BLK_TARGET).cpu().numpy()
+    changes = 0
+    for s in range(1, 3 * R + 1):
+        act = torch.rand(n, 3, generator=gen, device=DEV, dtype=torch.float64) * 0.2 - 0.1  # gentle: few failures
+        _, _, da, _ = a.env_step(act, auto_reset=False)
+        b.env_step(act, auto_reset=False)
+        alive &= ~da.cpu().numpy().astype(bool)
+        t = a.get_block(C.FW_BLK_TARGET).cpu().numpy()
+        der = a.get_block(C.FW_BLK_DERIVED).cpu().numpy()
+        st = (a.get_block(C.FW_BLK_STEPS)[0].cpu().numpy().astype(np.int64) >> 16) & 0xFFFF
+        assert torch.equal(a.get_block(C.FW_BLK_TARGET), b.get_block(C.FW_BLK_TARGET)), s
+        idx = np.nonzero(alive)[0]
+        moved = np.any(t[:2, idx] != tprev[:2, idx], axis=0)
+        if s % R == 0:
+            assert moved.all(), s
+            assert (st[idx] == 0).all(), s
+            vals = der[:2, idx]  # roll, pitch after the step
+            l2 = np.maximum(lo[:, None], vals - dl[:, None])
+            h2 = np.maximum(np.minimum(hi[:, None], vals + dl[:, None]), l2)
+            assert np.all(t[:2, idx] >= l2 - 1e-12) and np.all(t[:2, idx] <= h2 + 1e-12), s
+            changes += 1
+        else:
+            assert not moved.any(), s
+            assert (st[idx] == s % R).all(), s
+        tprev = t
+    assert changes == 3 and alive.sum() > n // 2
+    a.close()
+    b.close()

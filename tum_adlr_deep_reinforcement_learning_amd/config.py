@@ -149,7 +149,7 @@ class FwEnvConfig(ctypes.Structure):
                 ("term_weight", ctypes.c_double * 3), ("term_present", ctypes.c_int32 * 3),
                 ("reward_potential", ctypes.c_int32),
                 ("rew", FwRewFactor * FW_MAX_REW),
-                ("metrics", ctypes.c_int32), ("pad2_", ctypes.c_int32),
+                ("metrics", ctypes.c_int32), ("resample_every", ctypes.c_int32),
                 ("rise_low", ctypes.c_double), ("rise_high", ctypes.c_double),
                 ("obs_length", ctypes.c_int32), ("obs_step", ctypes.c_int32),
                 ("obs_noise", ctypes.c_int32), ("pad3_", ctypes.c_int32),
@@ -574,8 +574,6 @@ class EnvSpec:
             raise NotImplementedError("reward.form %r" % cfg["reward"].get("form"))
         if cfg["reward"].get("randomize_scaling", False):
             raise NotImplementedError("reward.randomize_scaling")
-        if cfg["target"].get("resample_every", 0):
-            raise NotImplementedError("target.resample_every")
         if cfg["target"].get("on_success", "none") not in ("none", "done"):
             raise NotImplementedError("target.on_success=%r" % cfg["target"].get("on_success"))
         sim_keys = set(cfg.get("simulator", {}).keys()) - {"states", "model"}
@@ -825,6 +823,7 @@ class EnvSpec:
         e.step_fail_timesteps = int(fails == "timesteps")
         e.step_fail_value = 0.0 if fails == "timesteps" else float(fails)
         e.reward_potential = int(r.get("form", "absolute") == "potential")  # fixed_wing.py:566, 1080-1108
+        e.resample_every = int(cfg["target"].get("resample_every", 0) or 0)  # fixed_wing.py:570-574
         for term in r["terms"]:
             fc = term["function_class"]
             if fc not in FW_FUN:

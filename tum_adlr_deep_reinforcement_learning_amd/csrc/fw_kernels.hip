@@ -822,6 +822,24 @@ __device__ __forceinline__ void reset_lane(const DevCfg<T>& c, const State<T>& s
   }
 }
 
+// sample_target (fixed_wing.py:654-746) during an episode (target.resample_every): U(low, high) narrowed to
+// vals -+ delta, as at the reset, from Philox stream 6 keyed by (env, episode, env step)
+template <typename T>
+__device__ __forceinline__ void resample_targets(const DevCfg<T>& c, const State<T>& s, int64_t i, int steps,
+                                                 const T* vals, T* tgt) {
+  uint32_t r[4];
+  philox(s.key0, s.key1, s.env_offset + (uint32_t)i, s.episode[i], 6u, (uint32_t)steps, r);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    T lo = c.target_low[k], hi = c.target_high[k];
+    if (c.has_delta[k]) {
+      lo = fmax(lo, vals[k] - c.target_delta[k]);
+      hi = fmax(fmin(hi, vals[k] + c.target_delta[k]), lo);
+    }
+    tgt[k] = lo + (hi - lo) * u01<T>(r[k]);  // numpy uniform
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ void load_row(const T* p, int rows, int64_t ld, int64_t i, T* dst) {
   for (int r = 0; r < rows; r++) dst[r] = p[r * ld + i];
@@ -1046,7 +1064,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   for (int q = 0; q < 3; q++) cmd[q] = c.scale_actions ? scale_fwd(c, q, clipv(a[q], c.scale_low, c.scale_high)) : a[q];
 
   const int steps = steps0 + 1;
-  const int steps_tgt = steps_tgt0 + 1;
+  int steps_tgt = steps_tgt0 + 1;
   // ---- epilogue inputs: action / command histories (newest first), goal register, metric state ----
   T seqA[RING + 1][3], seqC[RING + 1][3];
   // goal history (GB_*): entry count, counts, the ring words of the new entry and of the entry leaving the window
@@ -1208,6 +1226,12 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
       for (int k = 0; k < 3; k++) st_(s.shp, k, ld, i, shp[k]);
     } else {
       reward = reward_of(c, y, der, tgt, steps, seqA);
+    }
+    if (c.resample_every > 0 && steps_tgt >= c.resample_every) {
+      // target.resample_every (fixed_wing.py:570-574): sample_target (:654-746) from the state after the step,
+      // then _get_next_target with the target step count restarted; Philox stream 6, block = the env step
+      resample_targets(c, s, i, steps, vals, tgt);
+      steps_tgt = 0;
     }
     next_target(c, steps_tgt, tgt);
 #ifndef FW_MET_SKIP_STEP
@@ -1853,6 +1877,7 @@ void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
     d.step_fail_value = (T)e.step_fail_value;
     d.metrics = h->metrics && e.metrics;
     d.reward_potential = e.reward_potential ? 1 : 0;
+    d.resample_every = e.resample_every > 0 ? e.resample_every : 0;
     d.rise_low = (T)e.rise_low;
     d.rise_high = (T)e.rise_high;
     d.obs_len = e.obs_length > 1 ? e.obs_length : 1;
