@@ -171,8 +171,11 @@ typedef struct fw_obs_entry {
 
 typedef struct fw_rew_factor {
   int32_t kind, var, window, fun;
-  int32_t shaping, pad_;
+  int32_t shaping;
+  int32_t randomize;                 /* reward.randomize_scaling with "scaling": [low, high] (fixed_wing.py:473-479):
+                                      * each reset draws the factor's scaling from U(scaling, scaling_hi) */
   double scaling, max, sign;         /* max = +inf if absent */
+  double scaling_hi;
 } fw_rew_factor;
 
 /* target classes (fixed_wing.py:1363-1471) */

@@ -140,6 +140,8 @@ class OracleEnv:
             # the device draws resampled targets from its Philox streams, the reference from np_random: no
             # common sequence to restate (tests/test_gpu_r05.py checks the device's draws structurally)
             raise NotImplementedError("oracle: target.resample_every")
+        if any(env_cfg.rew[k].randomize for k in range(env_cfg.n_rew)):
+            raise NotImplementedError("oracle: reward.randomize_scaling (the device's Philox draws)")
         self.L = lib()
         self.sim_cfg, self.env_cfg, self.n_obs = sim_cfg, env_cfg, n_obs
         self.buf = ctypes.create_string_buffer(self.L.orc_env_state_size())

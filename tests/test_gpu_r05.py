@@ -498,3 +498,64 @@ def test_target_resample_every():
     assert changes == 3 and alive.sum() > n // 2
     a.close()
     b.close()
+
+
+def test_reward_randomize_scaling(tmp_path):
+    """reward.randomize_scaling (fixed_wing.py:473-479): a factor with "scaling": [low, high] gets a new
+    U(low, high) scaling at every reset (Philox stream 7 on the device; the reference draws from np_random, so
+    parity is distribution-level: unpinned).  With the roll error as the only reward term the scaling each env
+    used is |error| / -reward: constant within an episode, inside [low, high], spread over the envs, redrawn by
+    a reset, and the same bits on a second engine with the same seed."""
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
+    import json
+    from tum_adlr_deep_reinforcement_learning_amd import defaults
+    lo, hi = 0.5, 2.0
+    cfg = defaults.default_env_config()
+    cfg["steps_max"] = 400
+    cfg["reward"].update({"form": "absolute", "randomize_scaling": True,
+                          "terms": [{"function_class": "linear", "weight": 1.0}],
+                          "factors": [{"name": "roll", "class": "state", "type": "error", "function_class": "linear",
+                                       "scaling": [lo, hi], "shaping": False, "sign": -1}]})
+    path = tmp_path / "fixed_wing_config.json"
+    path.write_text(json.dumps(cfg))
+    spec = C.EnvSpec(config_path=str(path), sim_config_kw={"turbulence": False})
+    assert spec.struct().rew[0].randomize == 1
+    n = 128
+    a, b = (Engine(spec.sim, spec, n, device=DEV, precision="float64") for _ in range(2))
+    for e in (a, b):
+        e.seed(8)
+        e.reset()
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(2)
+
+    def scalings(steps):
+        seen = np.full((steps, n), np.nan)
+        alive = np.ones(n, bool)
+        for s in range(steps):
+            act = torch.rand(n, 3, generator=gen, device=DEV, dtype=torch.float64) * 0.2 - 0.1
+            _, ra, da, _ = a.env_step(act, auto_reset=False)
+            ra = ra.clone()
+            _, rb, _, _ = b.env_step(act, auto_reset=False)
+            assert torch.equal(ra, rb), s
+            alive &= ~da.cpu().numpy().astype(bool)
+            t = a.get_block(C.FW_BLK_TARGET)[0].cpu().numpy()
+            roll = a.get_block(C.FW_BLK_DERIVED)[0].cpu().numpy()
+            err = np.abs((roll - t + np.pi) % (2 * np.pi) - np.pi)
+            r = ra.cpu().numpy()
+            ok = alive & (err > 1e-3)
+            seen[s, ok] = err[ok] / -r[ok]
+        return seen
+
+    s1 = scalings(20)
+    per_env = np.nanmedian(s1, axis=0)
+    dev = np.nanmax(np.abs(s1 - per_env) / per_env, axis=0)
+    assert np.nanmax(dev) < 1e-9
+    got = per_env[~np.isnan(per_env)]
+    assert len(got) > n // 2 and got.min() >= lo and got.max() <= hi and got.std() > 0.2
+    for e in (a, b):
+        e.reset()
+    s2 = np.nanmedian(scalings(5), axis=0)
+    both = ~np.isnan(per_env) & ~np.isnan(s2)
+    assert both.sum() > n // 2 and np.mean(np.abs(s2[both] - per_env[both]) > 1e-6) > 0.9  # redrawn
+    a.close()
+    b.close()

@@ -123,8 +123,9 @@ class FwObsEntry(ctypes.Structure):
 
 class FwRewFactor(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("var", ctypes.c_int32), ("window", ctypes.c_int32),
-                ("fun", ctypes.c_int32), ("shaping", ctypes.c_int32), ("pad_", ctypes.c_int32),
-                ("scaling", ctypes.c_double), ("max", ctypes.c_double), ("sign", ctypes.c_double)]
+                ("fun", ctypes.c_int32), ("shaping", ctypes.c_int32), ("randomize", ctypes.c_int32),
+                ("scaling", ctypes.c_double), ("max", ctypes.c_double), ("sign", ctypes.c_double),
+                ("scaling_hi", ctypes.c_double)]
 
 
 class FwRandParam(ctypes.Structure):
@@ -572,8 +573,6 @@ class EnvSpec:
             raise NotImplementedError("integration_window")
         if cfg["reward"].get("form", "absolute") not in ("absolute", "potential"):
             raise NotImplementedError("reward.form %r" % cfg["reward"].get("form"))
-        if cfg["reward"].get("randomize_scaling", False):
-            raise NotImplementedError("reward.randomize_scaling")
         if cfg["target"].get("on_success", "none") not in ("none", "done"):
             raise NotImplementedError("target.on_success=%r" % cfg["target"].get("on_success"))
         sim_keys = set(cfg.get("simulator", {}).keys()) - {"states", "model"}
@@ -866,7 +865,14 @@ class EnvSpec:
             if not e.term_present[F.fun]:
                 raise KeyError(fc)
             F.shaping = int(bool(f.get("shaping", False)))
-            F.scaling = float(f["scaling"])
+            sc = f["scaling"]
+            if isinstance(sc, (list, tuple)):
+                # reward.randomize_scaling (fixed_wing.py:473-479): U(low, high) per episode on the device
+                if not r.get("randomize_scaling", False):
+                    raise TypeError("reward factor %r: list scaling without randomize_scaling" % f["name"])
+                F.randomize, F.scaling, F.scaling_hi = 1, float(sc[0]), float(sc[1])
+            else:
+                F.scaling = F.scaling_hi = float(sc)
             F.max = float(f["max"]) if f.get("max") is not None else INF
             F.sign = float(f.get("sign", -1))
         return e

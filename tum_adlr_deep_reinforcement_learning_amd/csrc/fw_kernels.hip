@@ -115,6 +115,7 @@ struct State {
   T* dry;             // [12][ld] Dryden filter-bank state of the current step (short chunks; null: FIR or off)
   T* shp;             // [3][ld] reward.form "potential": the previous step's shaping per function class (NaN =
                       // the reference's None, after a reset), or null
+  T* rsc;             // [FW_MAX_REW][ld] reward.randomize_scaling: this episode's scaling per factor, or null
   const T* noise;     // injected N(0,1) turbulence noise [4][noise_len][ld] or null
   int64_t noise_len;
   int32_t* noise_env_len;  // [ld] per-env injected length (0: Philox; zeroed by the auto-reset) or null: all
@@ -464,11 +465,14 @@ __device__ __forceinline__ void observe_env(const C& c, const State<T>& s, int64
 template <typename T>
 // shp: with reward.form "potential", the previous step's shaping per function class (NaN = None) on input,
 // this step's on output (fixed_wing.py:1080-1108); null for "absolute"
+// rsc: with reward.randomize_scaling, this aircraft's column of State::rsc (row stride ld), else null
 __device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* der, const T* tgt, int steps,
-                                       const T (*seqA)[3], T* shp = nullptr) {
+                                       const T (*seqA)[3], T* shp = nullptr, const T* rsc = nullptr,
+                                       int64_t ld = 0) {
   T tv[3] = {T(0), T(0), T(0)}, ts[3] = {T(0), T(0), T(0)};
   for (int f = 0; f < c.n_rew; f++) {
     const fw_rew_factor F = c.rew[f];
+    const T scl = (rsc && F.randomize) ? rsc[f * ld] : (T)F.scaling;
     T val = T(0);
     if (F.kind == FW_REW_ACTION_VALUE) {
       val = fabs(seqA[0][0]) + fabs(seqA[0][1]) + fabs(seqA[0][2]);
@@ -498,11 +502,11 @@ __device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* 
       val = target_error(c, F.var, tgt[F.var], state_value(tvv[F.var], y, der));
     }
     if (F.fun == FW_FUN_LINEAR) {
-      val = fabs(val) / (T)F.scaling;
+      val = fabs(val) / scl;
       val = val < T(0) ? T(0) : val;
       val = val > (T)F.max ? (T)F.max : val;
     } else {
-      val = val * val / (T)F.scaling;
+      val = val * val / scl;
     }
     const T sg = sgn((T)F.sign);
     if (F.shaping) ts[F.fun] += val * sg;
@@ -883,6 +887,14 @@ __device__ __forceinline__ void store_env_fresh(const DevCfg<T>& c, const State<
     if (s.shp)  // self.prev_shaping[*] = None (fixed_wing.py:469-470)
 #pragma unroll
       for (int k = 0; k < 3; k++) st_(s.shp, k, ld, i, T(NAN));
+    if (s.rsc)  // reward.randomize_scaling (fixed_wing.py:473-479): Philox stream 7, one block per factor
+      for (int r = 0; r < c.n_rew; r++)
+        if (c.rew[r].randomize) {
+          uint32_t rnd[4];
+          philox(s.key0, s.key1, s.env_offset + (uint32_t)i, s.episode[i], 7u, (uint32_t)r, rnd);
+          const T lo = (T)c.rew[r].scaling, hi = (T)c.rew[r].scaling_hi;
+          st_(s.rsc, r, ld, i, lo + (hi - lo) * u01<T>(rnd[0]));  // np_random.uniform(low, high)
+        }
   }
   s.steps[i] = 0u;
 }
@@ -1220,10 +1232,11 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
       }
     }
     if (goal_on || c.metrics) st_(s.goal, GB_N, ld, i, b + 1u);
-    if (s.shp) {
-      reward = reward_of(c, y, der, tgt, steps, seqA, shp);
+    if (s.shp || s.rsc) {
+      reward = reward_of(c, y, der, tgt, steps, seqA, s.shp ? shp : nullptr, s.rsc ? s.rsc + i : nullptr, ld);
+      if (s.shp)
 #pragma unroll
-      for (int k = 0; k < 3; k++) st_(s.shp, k, ld, i, shp[k]);
+        for (int k = 0; k < 3; k++) st_(s.shp, k, ld, i, shp[k]);
     } else {
       reward = reward_of(c, y, der, tgt, steps, seqA);
     }
@@ -1697,6 +1710,7 @@ struct fw_handle {
   size_t o_prm = 0;         // per-aircraft parameter rows (env->n_rand > 0 at create; 0 = none)
   size_t o_dry = 0;         // Dryden filter-bank state rows (turbulence on at create; 0 = none)
   size_t o_shp = 0;         // potential-form shaping rows (env->reward_potential at create; 0 = none)
+  size_t o_rsc = 0;         // per-episode reward scalings (a randomised factor at create; 0 = none)
   int rand_active = 0;      // the current config randomises parameters (kernels read the rows)
   int lanes_opt = FW_LANES_AUTO;  // fw_set_lanes: 0 = automatic, 1, 4
   int quad_ok = 1;          // the config allows the quad integrator (no wrapped ODE-state variable)
@@ -2086,6 +2100,7 @@ State<T> state_of(const fw_handle* h) {
   s.prm = h->o_prm ? (T*)(b + h->o_prm) : nullptr;
   s.dry = (h->o_dry && h->sim.turbulence && h->sim.dryden_state) ? (T*)(b + h->o_dry) : nullptr;
   s.shp = (h->o_shp && h->has_env && h->env.reward_potential) ? (T*)(b + h->o_shp) : nullptr;
+  s.rsc = h->o_rsc ? (T*)(b + h->o_rsc) : nullptr;
   s.col_ret = h->col.ret;
   s.col_gamma = h->col.gamma;
   s.col_rec = h->col.records;
@@ -2230,6 +2245,11 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
   if (env && env->reward_potential) {  // the previous step's reward shaping (reward.form "potential")
     h->o_shp = off; off += (size_t)3 * row;
   }
+  if (env) {  // per-episode reward scalings (reward.randomize_scaling)
+    bool any = false;
+    for (int r = 0; r < env->n_rew; r++) any = any || env->rew[r].randomize;
+    if (any) { h->o_rsc = off; off += (size_t)FW_MAX_REW * row; }
+  }
   if (env && env->n_rand > 0) {  // per-aircraft parameters (simulator parameter randomisation)
     h->o_prm = off; off += (size_t)FW_NPARAM * row;
   }
@@ -2343,6 +2363,9 @@ int fw_update_config(fw_handle* h, const fw_sim_config* sim, const fw_env_config
       return set_err(FW_E_UNSUPPORTED, "episode metrics must be enabled when the handle is created");
     if (env->n_rand > 0 && !h->o_prm)
       return set_err(FW_E_UNSUPPORTED, "parameter randomisation must be enabled when the handle is created");
+    for (int r = 0; r < env->n_rew; r++)
+      if (env->rew[r].randomize && !h->o_rsc)
+        return set_err(FW_E_UNSUPPORTED, "reward.randomize_scaling must be set when the handle is created");
     if (env->reward_potential && !h->o_shp)
       return set_err(FW_E_UNSUPPORTED, "reward.form \"potential\" must be set when the handle is created");
     h->env = *env;
