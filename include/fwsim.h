@@ -143,6 +143,7 @@ typedef struct fw_sim_config {
 /* ---- gym env configuration (fixed_wing_config.json) ------------------------ */
 #define FW_MAX_OBS 32
 #define FW_MAX_REW 8
+#define FW_MAX_IWIN 256
 #define FW_MAX_WINDOW 16
 #define FW_MAX_OBS_LEN 16     /* observation.length (history rows) */
 #define FW_MAX_OBS_HIST 64    /* past observation rows kept per env: (length - 1) * step + 2 */
@@ -152,6 +153,9 @@ typedef struct fw_sim_config {
 #define FW_OBS_TARGET_ABS 1     /* var = target index 0..2 (roll, pitch, Va) */
 #define FW_OBS_TARGET_REL 2
 #define FW_OBS_ACTION_WINDOW 3  /* var = action index 0..2 */
+#define FW_OBS_TARGET_INT 4     /* var = target index: "integrator" -- the sum of the error history over
+                                 * integration_window entries, the newest excluded, padded with the episode's
+                                 * first error (fixed_wing.py:1160-1182); observation length 1 only */
 
 typedef struct fw_obs_entry {
   int32_t kind, var, window, norm;
@@ -164,6 +168,8 @@ typedef struct fw_obs_entry {
 #define FW_REW_ACTION_DELTA 2
 #define FW_REW_ACTION_BOUND 3
 #define FW_REW_ACTION_VALUE 4
+#define FW_REW_STATE_INT_ERROR 5 /* var = target index: the sum of the last integration_window errors, padded
+                                  * with the first (fixed_wing.py:1001-1012) */
 
 #define FW_FUN_LINEAR 0
 #define FW_FUN_QUADRATIC 1
@@ -237,7 +243,7 @@ typedef struct fw_env_config {
   int32_t obs_length;                 /* >= 1 (0 is read as 1) */
   int32_t obs_step;                   /* >= 1 (0 is read as 1) */
   int32_t obs_noise;                  /* 1: add observation noise */
-  int32_t pad3_;
+  int32_t integration_window;         /* cfg "integration_window" (<= FW_MAX_IWIN; 0 = none) */
   double obs_noise_mean, obs_noise_std;
   /* simulator parameter randomisation: n_rand entries of rand[] (0 = every aircraft flies the sim
    * config's parameters).  Only parameters _forces reads at run time change the dynamics; the

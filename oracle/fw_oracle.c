@@ -675,6 +675,9 @@ typedef struct orc_env {
    * has_prev = 0 is the reference's None (set by reset) */
   double prev_shaping[3];
   int32_t has_prev[3];
+  /* history["error"] (fixed_wing.py:462-466, 575-579): entry 0 at the reset, one per successful step */
+  double err_hist[2048][3];
+  int32_t n_err;
 } orc_env;
 
 static void push_hist(double h[FW_MAX_WINDOW][3], int32_t* n, const double* v) {
@@ -737,6 +740,18 @@ static double get_error(const fw_env_config* e, const orc_env* s, int k) {
   return s->target[k] - val;
 }
 
+/* np.sum(history["error"][k][a:b]) with Python slice bounds already resolved to [a, b) */
+static double err_sum(const orc_env* s, int k, int a, int b) {
+  double v = 0;
+  for (int i = a; i < b; i++) v += s->err_hist[i][k];
+  return v;
+}
+/* Python's list[start:stop] bounds for negative indices on a list of n entries */
+static int py_idx(int i, int n) {
+  if (i < 0) i += n;
+  return i < 0 ? 0 : (i > n ? n : i);
+}
+
 /* _get_goal_status fixed_wing.py:1346-1361 ("all" entry) */
 static int goal_all(const fw_env_config* e, const orc_env* s) {
   int all = 1;
@@ -769,6 +784,10 @@ void orc_env_observe(const fw_sim_config* c, const fw_env_config* e, const orc_e
       val = s->target[E->var];
     } else if (E->kind == FW_OBS_TARGET_REL) {
       val = get_error(e, s, E->var);
+    } else if (E->kind == FW_OBS_TARGET_INT) {  /* fixed_wing.py:1160-1182, i = 1 */
+      const int W = e->integration_window, n = s->n_err;
+      val = err_sum(s, E->var, py_idx(-W - 1, n), py_idx(-1, n));
+      if (s->steps - 1 < W) val += (double)(W - (s->steps - 1)) * s->err_hist[0][E->var];
     } else { /* action window */
       int ai = E->var;
       if (s->steps - 1 < 0) {
@@ -817,6 +836,10 @@ static double get_reward(const fw_env_config* e, orc_env* s, const double* actio
       }
     } else if (F->kind == FW_REW_STATE_VALUE) {
       val = state_value(s, F->var);
+    } else if (F->kind == FW_REW_STATE_INT_ERROR) {  /* fixed_wing.py:1001-1012 */
+      const int W = e->integration_window, n = s->n_err;
+      val = err_sum(s, F->var, W == 0 ? 0 : py_idx(-W, n), n);  /* [-W:] ([-0:] is the whole list) */
+      if (s->steps < W) val += (double)(W - s->steps) * s->err_hist[0][F->var];
     } else { /* state error */
       val = get_error(e, s, F->var);
     }
@@ -889,6 +912,12 @@ static void next_target(const fw_sim_config* c, const fw_env_config* e, const or
  * init: FW_NINIT values (no NaN allowed here), target[3]. */
 int orc_env_reset(const fw_sim_config* c, const fw_env_config* e, orc_env* s, const double* init,
                   const double* target, double* obs) {
+  /* FixedWingAircraft.reset computes the observation BEFORE it replaces self.history (fixed_wing.py:452-459):
+   * an "integrator" entry then reads the previous episode's error history (None at the first reset) */
+  double prev_int[3] = {0, 0, 0};
+  const int prev_n = s->n_err, W = e->integration_window;
+  for (int k = 0; k < 3 && prev_n > 0; k++)
+    prev_int[k] = err_sum(s, k, py_idx(-W - 1, prev_n), py_idx(-1, prev_n)) + (double)(W + 1) * s->err_hist[0][k];
   memset(s, 0, sizeof(*s));
   double eul[3] = {init[FW_I_ROLL], init[FW_I_PITCH], init[FW_I_YAW]};
   int t;
@@ -917,7 +946,18 @@ int orc_env_reset(const fw_sim_config* c, const fw_env_config* e, orc_env* s, co
   s->steps_tgt = 0;
   s->goal_all[0] = (uint8_t)goal_all(e, s);
   s->n_goal = 1;
-  if (obs) orc_env_observe(c, e, s, obs);
+  for (int k = 0; k < 3; k++) s->err_hist[0][k] = get_error(e, s, k);
+  s->n_err = 1;
+  if (obs) {
+    orc_env_observe(c, e, s, obs);
+    for (int o = 0; o < e->n_obs; o++) {
+      const fw_obs_entry* E = &e->obs[o];
+      if (E->kind != FW_OBS_TARGET_INT) continue;
+      double v = prev_n > 0 ? prev_int[E->var] : get_error(e, s, E->var) * (double)W;  /* history None (:1163-1167) */
+      if (E->norm) v = (v - E->mean) / E->var_;
+      obs[o] = v;
+    }
+  }
   return 0;
 }
 
@@ -977,6 +1017,10 @@ int orc_env_step(const fw_sim_config* c, const fw_env_config* e, orc_env* s, con
     double nt[3];
     next_target(c, e, s, nt);
     for (int k = 0; k < 3; k++) s->target[k] = nt[k];
+    if (s->n_err < 2048) {  /* history["error"][k].append(self._get_error(k)) (:575-579) */
+      for (int k = 0; k < 3; k++) s->err_hist[s->n_err][k] = get_error(e, s, k);
+      s->n_err++;
+    }
   } else {
     done = 1;
     if (e->step_fail_timesteps) *reward = (double)(s->steps - e->steps_max);

@@ -17,6 +17,9 @@ Fixtures:
   env_potential.npz  FixedWingAircraft episodes with reward.form "potential" (fixed_wing.py:1080-1108: the
                      shaping terms enter as the change since the previous step), random and PID actions,
                      turbulence off and light
+  env_intwin.npz     FixedWingAircraft episodes with integration_window 10: "integrator" target observations
+                     (roll, pitch) and "int_error" reward factors (roll, Va), fixed_wing.py:1001-1012, 1160-1182,
+                     including episodes that end in a constraint violation (the failure-step observation)
 
 Usage:  python tests/golden/gen_golden_r05.py
 """
@@ -104,8 +107,66 @@ def gen_env_potential():
     np.savez_compressed(os.path.join(OUT, "env_potential.npz"), **out)
 
 
+INTWIN_KW = {"integration_window": 10,
+             "observation": {"states": {6: {"value": "integrator"}, 7: {"value": "integrator"}}},
+             "reward": {"factors": {0: {"type": "int_error"}, 2: {"type": "int_error"}}}}
+
+
+def gen_env_intwin():
+    import copy
+    out = {}
+    rng = np.random.RandomState(508)
+    for name, pol, ckw, omega, scale in [("rand", "rand", None, 20.0, 1.2), ("pid", "pid", {"action": {"scale_space": False}}, 20.0, 1.2),
+                                         ("rand_hot", "rand", None, 200.0, 3.0), ("rand_hot2", "rand", None, 250.0, 3.0)]:
+        kw = copy.deepcopy(INTWIN_KW)
+        if ckw:
+            kw.update(ckw)
+        env = G.make_env(False, 300, kw)
+        assert env.integration_window == 10
+        ep = G.env_episode(env, rng, False, 300, act_scale=scale, omega_deg=omega, policy=pol)
+        for k, v in ep.items():
+            out[name + "__" + k] = v
+        out[name + "__scale_space"] = np.array(ckw is None)
+        print("env intwin %s: %d steps, last term=%r" % (name, len(ep["rew"]), ep["term"][-1]))
+    for name, steps_before in [("fail_early", 0), ("fail_late", 12)]:
+        ep = _fail_episode(G.make_env(False, 300, copy.deepcopy(INTWIN_KW)), rng, steps_before)
+        for k, v in ep.items():
+            out[name + "__" + k] = v
+        out[name + "__scale_space"] = np.array(True)
+        print("env intwin %s: %d steps, last term=%r" % (name, len(ep["rew"]), ep["term"][-1]))
+    np.savez_compressed(os.path.join(OUT, "env_intwin.npz"), **out)
+
+
+def _fail_episode(env, rng, calm):
+    """An episode that ends in the Va <= 70 constraint (fixed_wing_config.json): start at 66-69 m/s nose down,
+    `calm` gentle steps, then full throttle -- the failed step's observation is the one to pin."""
+    st = G.random_state(rng, omega_deg=10.0, dots=False)
+    st["velocity_u"], st["velocity_v"], st["velocity_w"] = rng.uniform(66, 69), 0.0, 0.0
+    st["pitch"] = -0.5
+    st["wind"] = [0.0, 0.0, 0.0]
+    target = {"roll": 0.1, "pitch": -0.2, "Va": 25.0}
+    obs0 = env.reset(state=dict(st), target=dict(target))
+    init = np.array([st[k] for k in G.ENV_STATE_KEYS] + [0.0, 0.0, 0.0] + list(st["wind"]))
+    obs, rew, done, term, acts, tgt = [obs0], [], [], [], [], [np.array([env.target["roll"], env.target["pitch"],
+                                                                          env.target["Va"]])]
+    for s in range(300):
+        a = rng.uniform(-0.1, 0.1, 3) if s < calm else np.array([-1.0, 0.0, 1.0])
+        o, r, d, info = env.step(a)
+        acts.append(np.asarray(a, dtype=np.float64))
+        obs.append(o)
+        rew.append(r)
+        done.append(d)
+        term.append(info.get("termination", ""))
+        tgt.append(np.array([env.target["roll"], env.target["pitch"], env.target["Va"]]))
+        if d:
+            break
+    return dict(init=init, target0=np.array([target["roll"], target["pitch"], target["Va"]]), noise=np.zeros((4, 1)),
+                obs=np.array(obs), act=np.array(acts), rew=np.array(rew), done=np.array(done), term=np.array(term),
+                target=np.array(tgt))
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["dryden", "pyfly", "env", "potential"]
+    which = sys.argv[1:] or ["dryden", "pyfly", "env", "potential", "intwin"]
     if "dryden" in which:
         gen_dryden_short()
     if "pyfly" in which:
@@ -114,3 +175,5 @@ if __name__ == "__main__":
         gen_env_short()
     if "potential" in which:
         gen_env_potential()
+    if "intwin" in which:
+        gen_env_intwin()

@@ -559,3 +559,80 @@ def test_reward_randomize_scaling(tmp_path):
     assert both.sum() > n // 2 and np.mean(np.abs(s2[both] - per_env[both]) > 1e-6) > 0.9  # redrawn
     a.close()
     b.close()
+
+
+def _intwin_spec(steps_max=300, scale_space=True):
+    import copy
+    from test_golden_r05 import INTWIN_KW
+    ckw = copy.deepcopy(INTWIN_KW)
+    ckw["steps_max"] = steps_max
+    if not scale_space:
+        ckw["action"] = {"scale_space": False}
+    return C.EnvSpec(config_kw=ckw, sim_config_kw={"turbulence": False})
+
+
+@pytest.mark.parametrize("precision", ["float64", "float32"])
+@pytest.mark.parametrize("name", ["rand", "pid", "rand_hot", "fail_late"])
+def test_env_integration_window_episode(name, precision):
+    """integration_window 10: "integrator" observations and "int_error" rewards on the device (State::iws /
+    iwr) against the reference's own episodes (env_intwin.npz): fp64 observations and rewards within
+    1e-6 + 1e-6 / step, fp32 within 2e-3 (1 + |ref|)."""
+    import _fixtures as F
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
+    d = F.load("env_intwin.npz")
+    g = lambda k: d[name + "__" + k]  # noqa: E731
+    spec = _intwin_spec(300, bool(g("scale_space")))
+    eng = Engine(spec.sim, spec, 1, device=DEV, precision=precision)
+    obs0 = eng.reset(init=F.env_init(g("init"))[:, None], target=g("target0")[:, None])
+    f64 = precision == "float64"
+    np.testing.assert_allclose(obs0[0].double().cpu().numpy(), g("obs")[0], rtol=1e-12 if f64 else 1e-5, atol=1e-6)
+    acts = torch.tensor(g("act"), dtype=eng.dtype, device=DEV)
+    for s in range(len(acts)):
+        obs, rew, done, _ = eng.env_step(acts[s:s + 1], auto_reset=False)
+        assert bool(done[0]) == bool(g("done")[s]), s
+        r, ref = float(rew[0]), float(g("rew")[s])
+        o = obs[0].double().cpu().numpy()
+        if f64:
+            tol = 1e-6 + 1e-6 * s
+            assert abs(r - ref) <= tol, (s, r, ref)
+            np.testing.assert_allclose(o, g("obs")[s + 1], rtol=1e-5, atol=tol)
+        else:
+            assert abs(r - ref) <= 2e-3 * (1 + abs(ref)), (s, r, ref)
+            np.testing.assert_allclose(o, g("obs")[s + 1], rtol=2e-3, atol=2e-3)
+        if bool(done[0]):
+            break
+    eng.close()
+
+
+def test_integration_window_reset_reads_previous_history():
+    """FixedWingAircraft.reset observes before it replaces self.history (fixed_wing.py:452-459): an
+    "integrator" entry of a reset observation is the PREVIOUS episode's window sum padded as at steps_count 0
+    (the current error x W at the first reset).  Device (fp64) against the oracle: an explicit second reset
+    after 17 steps, and the auto-reset at steps_max (only the integrator entries: the new episode's other
+    entries come from the device's own draws)."""
+    import _fixtures as F
+    from oracle import oracle as O
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
+    d = F.load("env_intwin.npz")
+    spec = _intwin_spec(17)
+    ints = [o for o in range(spec.n_obs) if spec.struct().obs[o].kind == C.FW_OBS_TARGET_INT]
+    eng = Engine(spec.sim, spec, 1, device=DEV, precision="float64")
+    ora = O.OracleEnv(spec.sim.struct(), spec.struct(), spec.n_obs)
+    iA, tA = F.env_init(d["rand__init"]), d["rand__target0"]
+    iB, tB = F.env_init(d["pid__init"]), d["pid__target0"]
+    np.testing.assert_allclose(eng.reset(init=iA[:, None], target=tA[:, None])[0].cpu().numpy(), ora.reset(iA, tA),
+                               rtol=1e-12, atol=1e-12)
+    acts = d["rand__act"][:17]
+    for s in range(16):
+        eng.env_step(torch.tensor(acts[s:s + 1], device=DEV), auto_reset=False)
+        ora.step(acts[s])
+    o_dev = eng.reset(init=iB[:, None], target=tB[:, None])[0].cpu().numpy()
+    o_ora = ora.reset(iB, tB)
+    np.testing.assert_allclose(o_dev, o_ora, rtol=1e-9, atol=1e-9)
+    for s in range(17):  # the 17th step ends the episode (steps_max) and auto-resets
+        obs, _, done, _ = eng.env_step(torch.tensor(acts[s:s + 1], device=DEV), auto_reset=True)
+        ora.step(acts[s])
+    assert bool(done[0])
+    o_ora = ora.reset(iA, tA)
+    np.testing.assert_allclose(obs[0].cpu().numpy()[ints], o_ora[ints], rtol=1e-9, atol=1e-9)
+    eng.close()

@@ -52,11 +52,12 @@ FW_NPARAM = len(PARAM_NAMES)
 
 FW_TERM_NONE, FW_TERM_STEPS, FW_TERM_SUCCESS = 0, 100, 101
 
-FW_OBS_STATE, FW_OBS_TARGET_ABS, FW_OBS_TARGET_REL, FW_OBS_ACTION_WINDOW = range(4)
-FW_REW_STATE_ERROR, FW_REW_STATE_VALUE, FW_REW_ACTION_DELTA, FW_REW_ACTION_BOUND, FW_REW_ACTION_VALUE = range(5)
+FW_OBS_STATE, FW_OBS_TARGET_ABS, FW_OBS_TARGET_REL, FW_OBS_ACTION_WINDOW, FW_OBS_TARGET_INT = range(5)
+(FW_REW_STATE_ERROR, FW_REW_STATE_VALUE, FW_REW_ACTION_DELTA, FW_REW_ACTION_BOUND, FW_REW_ACTION_VALUE,
+ FW_REW_STATE_INT_ERROR) = range(6)
 FW_FUN = {"linear": 0, "quadratic": 1, "exponential": 2}
 FW_TGT = {"constant": 0, "compensate": 1}
-FW_MAX_OBS, FW_MAX_REW, FW_MAX_WINDOW = 32, 8, 16
+FW_MAX_OBS, FW_MAX_REW, FW_MAX_WINDOW, FW_MAX_IWIN = 32, 8, 16, 256
 FW_MAX_OBS_LEN, FW_MAX_OBS_HIST = 16, 64
 
 (FW_I_ROLL, FW_I_PITCH, FW_I_YAW, FW_I_P, FW_I_Q, FW_I_R, FW_I_PN, FW_I_PE, FW_I_PD, FW_I_U, FW_I_V, FW_I_W,
@@ -153,7 +154,7 @@ class FwEnvConfig(ctypes.Structure):
                 ("metrics", ctypes.c_int32), ("resample_every", ctypes.c_int32),
                 ("rise_low", ctypes.c_double), ("rise_high", ctypes.c_double),
                 ("obs_length", ctypes.c_int32), ("obs_step", ctypes.c_int32),
-                ("obs_noise", ctypes.c_int32), ("pad3_", ctypes.c_int32),
+                ("obs_noise", ctypes.c_int32), ("integration_window", ctypes.c_int32),
                 ("obs_noise_mean", ctypes.c_double), ("obs_noise_std", ctypes.c_double),
                 ("n_rand", ctypes.c_int32), ("pad4_", ctypes.c_int32),
                 ("rand", FwRandParam * FW_NPARAM)]
@@ -569,8 +570,6 @@ class EnvSpec:
         self.obs_noise = None
         if noise is not None and (noise.get("var", 0) != 0 or noise.get("mean", 0) != 0):
             self.obs_noise = (float(noise.get("mean", 0)), float(noise.get("var", 0)))
-        if cfg.get("integration_window", 0):
-            raise NotImplementedError("integration_window")
         if cfg["reward"].get("form", "absolute") not in ("absolute", "potential"):
             raise NotImplementedError("reward.form %r" % cfg["reward"].get("form"))
         if cfg["target"].get("on_success", "none") not in ("none", "done"):
@@ -759,6 +758,10 @@ class EnvSpec:
                     E.kind = FW_OBS_TARGET_ABS
                 elif val == "relative":
                     E.kind = FW_OBS_TARGET_REL
+                elif val == "integrator":  # fixed_wing.py:1160-1182
+                    if self.obs_length > 1:
+                        raise NotImplementedError("integrator target observation with observation.length > 1")
+                    E.kind = FW_OBS_TARGET_INT
                 else:
                     raise NotImplementedError("target observation value %r" % val)
                 E.var = TARGET_INDEX[o["name"]]
@@ -823,6 +826,9 @@ class EnvSpec:
         e.step_fail_value = 0.0 if fails == "timesteps" else float(fails)
         e.reward_potential = int(r.get("form", "absolute") == "potential")  # fixed_wing.py:566, 1080-1108
         e.resample_every = int(cfg["target"].get("resample_every", 0) or 0)  # fixed_wing.py:570-574
+        e.integration_window = int(cfg.get("integration_window", 0) or 0)   # fixed_wing.py:83
+        if e.integration_window > FW_MAX_IWIN:
+            raise NotImplementedError("integration_window > %d" % FW_MAX_IWIN)
         for term in r["terms"]:
             fc = term["function_class"]
             if fc not in FW_FUN:
@@ -854,6 +860,8 @@ class EnvSpec:
                     F.kind, F.var = FW_REW_STATE_ERROR, TARGET_INDEX[f["name"]]
                 elif typ == "value":
                     F.kind, F.var = FW_REW_STATE_VALUE, STATE_VAR_IDS[f["name"]]
+                elif typ == "int_error":  # fixed_wing.py:1001-1012
+                    F.kind, F.var = FW_REW_STATE_INT_ERROR, TARGET_INDEX[f["name"]]
                 else:
                     raise NotImplementedError("state reward type %r" % typ)
             else:
@@ -875,6 +883,13 @@ class EnvSpec:
                 F.scaling = F.scaling_hi = float(sc)
             F.max = float(f["max"]) if f.get("max") is not None else INF
             F.sign = float(f.get("sign", -1))
+        uses_iw = any(e.obs[o].kind == FW_OBS_TARGET_INT for o in range(e.n_obs)) or \
+            any(e.rew[k].kind == FW_REW_STATE_INT_ERROR for k in range(e.n_rew))
+        if uses_iw and e.integration_window <= 0:
+            # the reference sums the whole history then ([-0:]); no config does that
+            raise NotImplementedError("integrator / int_error with integration_window 0")
+        if uses_iw and e.obs_noise and any(e.obs[o].kind == FW_OBS_TARGET_INT for o in range(e.n_obs)):
+            raise NotImplementedError("integrator observation with observation noise")
         return e
 
     def target_sampling(self):

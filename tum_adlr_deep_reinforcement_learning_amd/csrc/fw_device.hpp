@@ -143,6 +143,7 @@ struct DevCfg {
   int metrics;                         // streaming episode metrics tracked (fw_env_config.metrics)
   int reward_potential;                // reward.form "potential" (fw_env_config.reward_potential)
   int resample_every;                  // target.resample_every (fw_env_config.resample_every; 0 = never)
+  int iwin;                            // integration_window (fw_env_config.integration_window; 0 = none)
   T rise_low, rise_high;
   int obs_len, obs_step, obs_hist;     // observation rows, their spacing, past rows kept (0: no history)
   int obs_noise;                       // observation.noise drawn

@@ -116,6 +116,12 @@ struct State {
   T* shp;             // [3][ld] reward.form "potential": the previous step's shaping per function class (NaN =
                       // the reference's None, after a reset), or null
   T* rsc;             // [FW_MAX_REW][ld] reward.randomize_scaling: this episode's scaling per factor, or null
+  // integration_window W (fixed_wing.py:1001-1012, 1160-1182): the error history's sums.  iwr: ring of the last W
+  // errors per target, entry e in slot (L_ep + e) % W; iws rows IW_Q + k: sum of the last W of the n entries
+  // so far, IW_QP + k: the same before the newest entry (what an "integrator" observation reads), IW_E0 + k:
+  // entry 0 (the padding).  Null without an integration window.
+  T* iwr;             // [W][3][ld]
+  T* iws;             // [9][ld]
   const T* noise;     // injected N(0,1) turbulence noise [4][noise_len][ld] or null
   int64_t noise_len;
   int32_t* noise_env_len;  // [ld] per-env injected length (0: Philox; zeroed by the auto-reset) or null: all
@@ -346,6 +352,8 @@ __device__ __forceinline__ T obs_raw(const DevCfg<T>& c, const fw_obs_entry& E, 
     } else if (E.kind == FW_OBS_TARGET_REL) {
       const int tv[3] = {FW_V_ROLL, FW_V_PITCH, FW_V_VA};
       val = target_error(c, E.var, tgt[E.var], state_value(tv[E.var], y, der));
+    } else if (E.kind == FW_OBS_TARGET_INT) {
+      val = T(0);  // (written afterwards from the window sums: iw_obs)
     } else {  // action window
       const int ai = E.var;
       if (steps - 1 < 0) {
@@ -376,6 +384,39 @@ __device__ __forceinline__ T obs_raw(const DevCfg<T>& c, const fw_obs_entry& E, 
 template <typename T>
 __device__ __forceinline__ T obs_norm(const fw_obs_entry& E, T val) {
   return E.norm ? (val - (T)E.mean) / (T)E.var_ : val;
+}
+
+// integration_window (State::iws): rows of the window sums
+constexpr int IW_Q = 0, IW_QP = 3, IW_E0 = 6;
+// the sum plus the padding of an integrator value: s + (W - x) e0 when x < W (fixed_wing.py:1009-1012, 1177-1181)
+template <typename T>
+__device__ __forceinline__ T iw_value(const DevCfg<T>& c, T sum, int x, T e0) {
+  return x < c.iwin ? sum + T(c.iwin - x) * e0 : sum;
+}
+// the "integrator" entries of one length-1 observation row (v3: the raw values per target)
+template <typename T>
+__device__ __forceinline__ void iw_obs(const DevCfg<T>& c, const T* v3, T* out) {
+  if (!out) return;
+  for (int o = 0; o < c.n_obs; o++) {
+    const fw_obs_entry E = c.obs[o];
+    if (E.kind == FW_OBS_TARGET_INT) out[o] = obs_norm(E, v3[E.var]);
+  }
+}
+// a fresh episode's error history: entry 0 in its ring slot, the sums of one entry
+template <typename T>
+__device__ __forceinline__ void iw_init(const DevCfg<T>& c, const State<T>& s, int64_t i, const T* tgt, const T* der,
+                                        uint32_t lep) {
+  const int64_t ld = s.ld;
+  const int slot = (int)(lep % (uint32_t)c.iwin);
+  const T vals[3] = {der[0], der[1], der[3]};
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const T e0 = target_error(c, k, tgt[k], vals[k]);
+    st_(s.iwr, slot * 3 + k, ld, i, e0);
+    st_(s.iws, IW_Q + k, ld, i, e0);
+    st_(s.iws, IW_QP + k, ld, i, T(0));
+    st_(s.iws, IW_E0 + k, ld, i, e0);
+  }
 }
 
 // length-1 observation without noise (the default task): one row straight from the state
@@ -466,9 +507,10 @@ template <typename T>
 // shp: with reward.form "potential", the previous step's shaping per function class (NaN = None) on input,
 // this step's on output (fixed_wing.py:1080-1108); null for "absolute"
 // rsc: with reward.randomize_scaling, this aircraft's column of State::rsc (row stride ld), else null
+// iwq: with an integration window, the sums of the last W errors (3) then entry 0 (3), else null
 __device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* der, const T* tgt, int steps,
                                        const T (*seqA)[3], T* shp = nullptr, const T* rsc = nullptr,
-                                       int64_t ld = 0) {
+                                       int64_t ld = 0, const T* iwq = nullptr) {
   T tv[3] = {T(0), T(0), T(0)}, ts[3] = {T(0), T(0), T(0)};
   for (int f = 0; f < c.n_rew; f++) {
     const fw_rew_factor F = c.rew[f];
@@ -497,6 +539,8 @@ __device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* 
       }
     } else if (F.kind == FW_REW_STATE_VALUE) {
       val = state_value(F.var, y, der);
+    } else if (F.kind == FW_REW_STATE_INT_ERROR) {  // fixed_wing.py:1001-1012
+      val = iwq ? iw_value(c, iwq[F.var], steps, iwq[3 + F.var]) : T(0);
     } else {
       const int tvv[3] = {FW_V_ROLL, FW_V_PITCH, FW_V_VA};
       val = target_error(c, F.var, tgt[F.var], state_value(tvv[F.var], y, der));
@@ -911,8 +955,24 @@ __global__ __launch_bounds__(BLOCK) void k_reset(const DevCfg<T>* __restrict__ c
   if (mask && !mask[i]) return;
   const DevCfg<T>& c = *cfgp;
   T y[NY], der[8], wind[3], tgt[3] = {T(0), T(0), T(0)};
+  // integrator observations at the reset read the previous episode's history (None before the first reset:
+  // the current error x W), fixed_wing.py:452-459, 1163-1167
+  T rv[3] = {T(0), T(0), T(0)};
+  const bool iw_first = s.iws ? ld_(s.goal, GB_N, s.ld, i) == 0u : true;
+  if (s.iws && !iw_first)
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+      rv[k] = iw_value(c, ld_(s.iws, IW_QP + k, s.ld, i), -1, ld_(s.iws, IW_E0 + k, s.ld, i));
   reset_lane(c, s, i, init, tin, y, der, wind, tgt);
   store_env_fresh(c, s, i, y, der, wind, tgt, s.life[i]);
+  if (s.iws) {
+    iw_init(c, s, i, tgt, der, s.life[i]);
+    if (iw_first) {
+      const T vals[3] = {der[0], der[1], der[3]};
+#pragma unroll
+      for (int k = 0; k < 3; k++) rv[k] = target_error(c, k, tgt[k], vals[k]) * T(c.iwin);
+    }
+  }
   if (c.has_env && c.metrics) {
     const T vr[3] = {der[0], der[1], der[3]};
     metrics_init(c, s, i, tgt, vr, s.life[i]);
@@ -925,6 +985,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset(const DevCfg<T>* __restrict__ c
       for (int a = 0; a < 3; a++) seq[j][a] = T(0);
     observe_env(c, s, i, s.episode[i], OBS_RESET, y, der, tgt, 0, seq, seq,
                 obs ? obs + i * (int64_t)c.n_obs * c.obs_len : nullptr, s.life[i]);
+    if (s.iws) iw_obs(c, rv, obs ? obs + i * (int64_t)c.n_obs * c.obs_len : nullptr);
   }
 }
 
@@ -961,6 +1022,12 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const DevCfg<T>* __restrict__
   }
   observe_env(c, s, i, s.episode[i], OBS_PEEK, y, der, tgt, steps, seqA, seqC, obs + i * (int64_t)c.n_obs * c.obs_len,
               life - (uint32_t)steps);
+  if (s.iws) {  // get_observation with the current history: the sum before the newest entry + padding
+    T v[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) v[k] = iw_value(c, ld_(s.iws, IW_QP + k, ld, i), steps - 1, ld_(s.iws, IW_E0 + k, ld, i));
+    iw_obs(c, v, obs + i * (int64_t)c.n_obs * c.obs_len);
+  }
 }
 
 // Re-reads the pre-step ODE state after the RK loop (sim_step_masked's reload hook): the
@@ -1090,6 +1157,8 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   T prev_cmd[3];
   T ep_ret0;
   T shp[3] = {T(0), T(0), T(0)};  // reward.form "potential": the previous step's shaping (State::shp)
+  // integration window (State::iws): the window sums before this step, entry 0, the entry leaving the window
+  T iwq[6] = {T(0), T(0), T(0), T(0), T(0), T(0)}, iqp[3] = {T(0), T(0), T(0)}, iold[3] = {T(0), T(0), T(0)};
   auto load_epilogue = [&]() {
     life0 = s.life[i];
     lep = life0 - (uint32_t)steps0;
@@ -1109,7 +1178,17 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
         for (int q = 0; q < 3; q++) seqC[j][q] = s.cmd_ring[((int64_t)slot * 3 + q) * ld + i];
       }
     }
-    if (goal_on || c.metrics) gn = ld_(s.goal, GB_N, ld, i);
+    if (goal_on || c.metrics || s.iws) gn = ld_(s.goal, GB_N, ld, i);
+    if (s.iws) {
+      const int os = (int)((lep + b_guess) % (uint32_t)c.iwin);  // entry b - W shares the new entry's slot
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        iwq[k] = ld_(s.iws, IW_Q + k, ld, i);
+        iwq[3 + k] = ld_(s.iws, IW_E0 + k, ld, i);
+        iqp[k] = ld_(s.iws, IW_QP + k, ld, i);
+        iold[k] = ld_(s.iwr, os * 3 + k, ld, i);
+      }
+    }
     if (goal_on) {
       gw_new = ld_(s.goal, gring_row(lep + b_guess), ld, i);
       gw_old = ld_(s.goal, gring_row(lep + b_guess - req), ld, i);
@@ -1231,9 +1310,10 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
         term = FW_TERM_SUCCESS;
       }
     }
-    if (goal_on || c.metrics) st_(s.goal, GB_N, ld, i, b + 1u);
-    if (s.shp || s.rsc) {
-      reward = reward_of(c, y, der, tgt, steps, seqA, s.shp ? shp : nullptr, s.rsc ? s.rsc + i : nullptr, ld);
+    if (goal_on || c.metrics || s.iws) st_(s.goal, GB_N, ld, i, b + 1u);
+    if (s.shp || s.rsc || s.iws) {
+      reward = reward_of(c, y, der, tgt, steps, seqA, s.shp ? shp : nullptr, s.rsc ? s.rsc + i : nullptr, ld,
+                         s.iws ? iwq : nullptr);
       if (s.shp)
 #pragma unroll
         for (int k = 0; k < 3; k++) st_(s.shp, k, ld, i, shp[k]);
@@ -1247,6 +1327,21 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
       steps_tgt = 0;
     }
     next_target(c, steps_tgt, tgt);
+    if (s.iws) {  // history["error"][k].append(self._get_error(k)) (fixed_wing.py:575-579): the window sums move on
+      const int ns = (int)((lep + b) % (uint32_t)c.iwin);
+      if (b != b_guess)
+#pragma unroll
+        for (int k = 0; k < 3; k++) iold[k] = ld_(s.iwr, ns * 3 + k, ld, i);
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const T err = target_error(c, k, tgt[k], vals[k]);
+        iqp[k] = iwq[k];
+        iwq[k] = b >= (uint32_t)c.iwin ? (iwq[k] + err) - iold[k] : iwq[k] + err;
+        st_(s.iwr, ns * 3 + k, ld, i, err);
+        st_(s.iws, IW_Q + k, ld, i, iwq[k]);
+        st_(s.iws, IW_QP + k, ld, i, iqp[k]);
+      }
+    }
 #ifndef FW_MET_SKIP_STEP
     if (c.metrics) metrics_step(c, s, i, M, tgt, vals, gb, gcnt, b, lep);
 #endif
@@ -1262,7 +1357,15 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   const int64_t ow = (int64_t)c.n_obs * c.obs_len;  // values per observation (rows x entries)
   const int omode = sterm ? OBS_FAIL : OBS_STEP;
   T* orow = obs_out + i * ow;
-  if (done && tobs_out) observe_env(c, s, i, episode, omode, y, der, tgt, steps, seqA, seqC, tobs_out + i * ow, lep);
+  // the "integrator" observation entries: the sum before the newest entry + padding (i = 1, fixed_wing.py:1168-1181)
+  T iwv[3] = {T(0), T(0), T(0)};
+  if (s.iws)
+#pragma unroll
+    for (int k = 0; k < 3; k++) iwv[k] = iw_value(c, iqp[k], steps - 1, iwq[3 + k]);
+  if (done && tobs_out) {
+    observe_env(c, s, i, episode, omode, y, der, tgt, steps, seqA, seqC, tobs_out + i * ow, lep);
+    if (s.iws) iw_obs(c, iwv, tobs_out + i * ow);
+  }
 
   rew_out[i] = reward;
   done_out[i] = done ? 1 : 0;
@@ -1304,6 +1407,15 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
 #endif
       T seq0[RING + 1][3];
       observe_env(c, s, i, s.episode[i], OBS_RESET, yr, dr, tr, 0, seq0, seq0, orow, life0 + 1u);  // (reset_lane's +1)
+      if (s.iws) {
+        // FixedWingAircraft.reset observes BEFORE it replaces the history (fixed_wing.py:452-459): the finished
+        // episode's sums, padded as at steps_count 0; then the new episode's entry 0
+        T rv[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) rv[k] = iw_value(c, iqp[k], -1, iwq[3 + k]);
+        iw_obs(c, rv, orow);
+        iw_init(c, s, i, tr, dr, life0 + 1u);
+      }
       s.life[i] = life0 + 1u;
       FW_TSTAMP(5);
       return;
@@ -1311,6 +1423,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   }
 #ifndef FW_SKIP_OBS
   observe_env(c, s, i, episode, omode, y, der, tgt, steps, seqA, seqC, orow, lep);
+  if (s.iws) iw_obs(c, iwv, orow);
 #endif
 #pragma unroll
   for (int r = 0; r < NY; r++) st_(s.y, r, ld, i, y[r]);
@@ -1711,6 +1824,8 @@ struct fw_handle {
   size_t o_dry = 0;         // Dryden filter-bank state rows (turbulence on at create; 0 = none)
   size_t o_shp = 0;         // potential-form shaping rows (env->reward_potential at create; 0 = none)
   size_t o_rsc = 0;         // per-episode reward scalings (a randomised factor at create; 0 = none)
+  size_t o_iwr = 0, o_iws = 0;  // integration-window ring and sums (env->integration_window > 0 at create)
+  int iwin = 0;
   int rand_active = 0;      // the current config randomises parameters (kernels read the rows)
   int lanes_opt = FW_LANES_AUTO;  // fw_set_lanes: 0 = automatic, 1, 4
   int quad_ok = 1;          // the config allows the quad integrator (no wrapped ODE-state variable)
@@ -1892,6 +2007,7 @@ void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
     d.metrics = h->metrics && e.metrics;
     d.reward_potential = e.reward_potential ? 1 : 0;
     d.resample_every = e.resample_every > 0 ? e.resample_every : 0;
+    d.iwin = e.integration_window > 0 ? e.integration_window : 0;
     d.rise_low = (T)e.rise_low;
     d.rise_high = (T)e.rise_high;
     d.obs_len = e.obs_length > 1 ? e.obs_length : 1;
@@ -2101,6 +2217,8 @@ State<T> state_of(const fw_handle* h) {
   s.dry = (h->o_dry && h->sim.turbulence && h->sim.dryden_state) ? (T*)(b + h->o_dry) : nullptr;
   s.shp = (h->o_shp && h->has_env && h->env.reward_potential) ? (T*)(b + h->o_shp) : nullptr;
   s.rsc = h->o_rsc ? (T*)(b + h->o_rsc) : nullptr;
+  s.iwr = h->o_iwr ? (T*)(b + h->o_iwr) : nullptr;
+  s.iws = h->o_iws ? (T*)(b + h->o_iws) : nullptr;
   s.col_ret = h->col.ret;
   s.col_gamma = h->col.gamma;
   s.col_rec = h->col.records;
@@ -2245,6 +2363,11 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
   if (env && env->reward_potential) {  // the previous step's reward shaping (reward.form "potential")
     h->o_shp = off; off += (size_t)3 * row;
   }
+  if (env && env->integration_window > 0) {  // the error history's window sums (integration_window)
+    h->iwin = env->integration_window;
+    h->o_iwr = off; off += (size_t)3 * h->iwin * row;
+    h->o_iws = off; off += (size_t)9 * row;
+  }
   if (env) {  // per-episode reward scalings (reward.randomize_scaling)
     bool any = false;
     for (int r = 0; r < env->n_rew; r++) any = any || env->rew[r].randomize;
@@ -2366,6 +2489,8 @@ int fw_update_config(fw_handle* h, const fw_sim_config* sim, const fw_env_config
     for (int r = 0; r < env->n_rew; r++)
       if (env->rew[r].randomize && !h->o_rsc)
         return set_err(FW_E_UNSUPPORTED, "reward.randomize_scaling must be set when the handle is created");
+    if (env->integration_window != h->iwin)
+      return set_err(FW_E_UNSUPPORTED, "integration_window must be the one the handle was created with");
     if (env->reward_potential && !h->o_shp)
       return set_err(FW_E_UNSUPPORTED, "reward.form \"potential\" must be set when the handle is created");
     h->env = *env;
