@@ -608,7 +608,7 @@ def test_integration_window_reset_reads_previous_history():
     """FixedWingAircraft.reset observes before it replaces self.history (fixed_wing.py:452-459): an
     "integrator" entry of a reset observation is the PREVIOUS episode's window sum padded as at steps_count 0
     (the current error x W at the first reset).  Device (fp64) against the oracle: an explicit second reset
-    after 17 steps, and the auto-reset at steps_max (only the integrator entries: the new episode's other
+    after 16 steps, and the auto-reset at steps_max (only the integrator entries: the new episode's other
     entries come from the device's own draws)."""
     import _fixtures as F
     from oracle import oracle as O

@@ -388,6 +388,11 @@ __device__ __forceinline__ T obs_norm(const fw_obs_entry& E, T val) {
 
 // integration_window (State::iws): rows of the window sums
 constexpr int IW_Q = 0, IW_QP = 3, IW_E0 = 6;
+// a[k] for a runtime k by selects: a register array indexed at run time would be placed in scratch
+template <typename T>
+__device__ __forceinline__ T pick3(const T* a, int k) {
+  return k == 0 ? a[0] : (k == 1 ? a[1] : a[2]);
+}
 // the sum plus the padding of an integrator value: s + (W - x) e0 when x < W (fixed_wing.py:1009-1012, 1177-1181)
 template <typename T>
 __device__ __forceinline__ T iw_value(const DevCfg<T>& c, T sum, int x, T e0) {
@@ -399,7 +404,7 @@ __device__ __forceinline__ void iw_obs(const DevCfg<T>& c, const T* v3, T* out) 
   if (!out) return;
   for (int o = 0; o < c.n_obs; o++) {
     const fw_obs_entry E = c.obs[o];
-    if (E.kind == FW_OBS_TARGET_INT) out[o] = obs_norm(E, v3[E.var]);
+    if (E.kind == FW_OBS_TARGET_INT) out[o] = obs_norm(E, pick3(v3, E.var));
   }
 }
 // a fresh episode's error history: entry 0 in its ring slot, the sums of one entry
@@ -504,13 +509,15 @@ __device__ __forceinline__ void observe_env(const C& c, const State<T>& s, int64
 
 // get_reward (fixed_wing.py:941-1111), form "absolute"
 template <typename T>
-// shp: with reward.form "potential", the previous step's shaping per function class (NaN = None) on input,
-// this step's on output (fixed_wing.py:1080-1108); null for "absolute"
+// shp (when pot): with reward.form "potential", the previous step's shaping per function class (NaN = None)
+// on input, this step's on output (fixed_wing.py:1080-1108)
 // rsc: with reward.randomize_scaling, this aircraft's column of State::rsc (row stride ld), else null
-// iwq: with an integration window, the sums of the last W errors (3) then entry 0 (3), else null
+// iwq (when iw): with an integration window, the sums of the last W errors (3) then entry 0 (3)
+// (shp / iwq are register arrays taken by reference with a flag: a pointer that may be null would take their
+// address and place them in scratch)
 __device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* der, const T* tgt, int steps,
-                                       const T (*seqA)[3], T* shp = nullptr, const T* rsc = nullptr,
-                                       int64_t ld = 0, const T* iwq = nullptr) {
+                                       const T (*seqA)[3], T (&shp)[3], bool pot, const T* rsc, int64_t ld,
+                                       const T (&iwq)[6], bool iw) {
   T tv[3] = {T(0), T(0), T(0)}, ts[3] = {T(0), T(0), T(0)};
   for (int f = 0; f < c.n_rew; f++) {
     const fw_rew_factor F = c.rew[f];
@@ -540,7 +547,7 @@ __device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* 
     } else if (F.kind == FW_REW_STATE_VALUE) {
       val = state_value(F.var, y, der);
     } else if (F.kind == FW_REW_STATE_INT_ERROR) {  // fixed_wing.py:1001-1012
-      val = iwq ? iw_value(c, iwq[F.var], steps, iwq[3 + F.var]) : T(0);
+      val = iw ? iw_value(c, pick3(iwq, F.var), steps, pick3(iwq + 3, F.var)) : T(0);
     } else {
       const int tvv[3] = {FW_V_ROLL, FW_V_PITCH, FW_V_VA};
       val = target_error(c, F.var, tgt[F.var], state_value(tvv[F.var], y, der));
@@ -552,16 +559,21 @@ __device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* 
     } else {
       val = val * val / scl;
     }
-    const T sg = sgn((T)F.sign);
-    if (F.shaping) ts[F.fun] += val * sg;
-    else tv[F.fun] += val * sg;
+    const T add = val * sgn((T)F.sign);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {  // by selects: tv[F.fun] at a runtime index would live in scratch
+      if (F.fun == k) {
+        if (F.shaping) ts[k] += add;
+        else tv[k] += add;
+      }
+    }
   }
   T r = T(0);
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     if (!c.term_present[k]) continue;
     T v;
-    if (shp) {  // potential: the shaping's change since the previous step, or nothing after a reset
+    if (pot) {  // potential: the shaping's change since the previous step, or nothing after a reset
       const T prev = shp[k];
       const T a = isnan(prev) ? tv[k] : tv[k] + (ts[k] - prev);
       v = (k == FW_FUN_EXPONENTIAL) ? T(-1) + exp(a) : a;
@@ -1312,13 +1324,13 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
     }
     if (goal_on || c.metrics || s.iws) st_(s.goal, GB_N, ld, i, b + 1u);
     if (s.shp || s.rsc || s.iws) {
-      reward = reward_of(c, y, der, tgt, steps, seqA, s.shp ? shp : nullptr, s.rsc ? s.rsc + i : nullptr, ld,
-                         s.iws ? iwq : nullptr);
+      reward = reward_of(c, y, der, tgt, steps, seqA, shp, s.shp != nullptr, s.rsc ? s.rsc + i : nullptr, ld,
+                         iwq, s.iws != nullptr);
       if (s.shp)
 #pragma unroll
         for (int k = 0; k < 3; k++) st_(s.shp, k, ld, i, shp[k]);
     } else {
-      reward = reward_of(c, y, der, tgt, steps, seqA);
+      reward = reward_of(c, y, der, tgt, steps, seqA, shp, false, (const T*)nullptr, 0, iwq, false);
     }
     if (c.resample_every > 0 && steps_tgt >= c.resample_every) {
       // target.resample_every (fixed_wing.py:570-574): sample_target (:654-746) from the state after the step,
