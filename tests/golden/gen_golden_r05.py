@@ -23,6 +23,7 @@ Fixtures:
 
 Usage:  python tests/golden/gen_golden_r05.py
 """
+import json
 import os
 import sys
 
@@ -133,6 +134,19 @@ def gen_env_intwin():
         for k, v in ep.items():
             out[name + "__" + k] = v
         out[name + "__scale_space"] = np.array(True)
+        print("env intwin %s: %d steps, last term=%r" % (name, len(ep["rew"]), ep["term"][-1]))
+    # episodes that end in a constraint violation (the fail_va / fail_omega cases of gen_golden.py): the failed
+    # step's observation and reward with the window; the extra config (steps_max too) is stored with the episode
+    rng = np.random.RandomState(509)
+    for name, extra, omega in [("fail_va", {"simulator": {"states": {5: {"constraint_max": 17.5}}}}, 60.0)]:
+        kw = copy.deepcopy(INTWIN_KW)
+        kw.update(copy.deepcopy(extra))
+        env = G.make_env(False, 2000, kw)
+        ep = G.env_episode(env, rng, False, 600, omega_deg=omega, policy="rand")
+        for k, v in ep.items():
+            out[name + "__" + k] = v
+        out[name + "__scale_space"] = np.array(True)
+        out[name + "__extra_kw"] = np.array(json.dumps(dict(extra, steps_max=2000)))
         print("env intwin %s: %d steps, last term=%r" % (name, len(ep["rew"]), ep["term"][-1]))
     np.savez_compressed(os.path.join(OUT, "env_intwin.npz"), **out)
 

@@ -572,16 +572,17 @@ def _intwin_spec(steps_max=300, scale_space=True):
 
 
 @pytest.mark.parametrize("precision", ["float64", "float32"])
-@pytest.mark.parametrize("name", ["rand", "pid", "rand_hot", "fail_late"])
+@pytest.mark.parametrize("name", ["rand", "pid", "rand_hot", "fail_late", "fail_va"])
 def test_env_integration_window_episode(name, precision):
     """integration_window 10: "integrator" observations and "int_error" rewards on the device (State::iws /
-    iwr) against the reference's own episodes (env_intwin.npz): fp64 observations and rewards within
-    1e-6 + 1e-6 / step, fp32 within 2e-3 (1 + |ref|)."""
+    iwr) against the reference's own episodes (env_intwin.npz, fail_va ending in a Va constraint violation):
+    fp64 observations and rewards within 1e-6 + 1e-6 / step, fp32 within 2e-3 (1 + |ref|)."""
     import _fixtures as F
+    from test_golden_r05 import intwin_config_kw
     from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
     d = F.load("env_intwin.npz")
     g = lambda k: d[name + "__" + k]  # noqa: E731
-    spec = _intwin_spec(300, bool(g("scale_space")))
+    spec = C.EnvSpec(config_kw=intwin_config_kw(d, name), sim_config_kw={"turbulence": False})
     eng = Engine(spec.sim, spec, 1, device=DEV, precision=precision)
     obs0 = eng.reset(init=F.env_init(g("init"))[:, None], target=g("target0")[:, None])
     f64 = precision == "float64"
