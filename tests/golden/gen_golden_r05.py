@@ -179,8 +179,37 @@ def _fail_episode(env, rng, calm):
                 target=np.array(tgt))
 
 
+# observation.normalize with entries that give no mean / var: the reference derives them from the bounds
+# (fixed_wing.py:142-161: mean = high - low, var = (high - low) / 16, or 0 / 1 for unbounded entries)
+OBSNORM_KW = {"observation": {"normalize": True, "states": {
+    0: {"mean": None, "var": None}, 1: {"mean": None}, 2: {"var": None}, 3: {"mean": None, "var": None},
+    6: {"mean": None, "var": None}, 8: {"var": None}, 9: {"mean": None, "var": None}}}}
+
+
+def gen_env_obsnorm():
+    import copy
+    out = {}
+    rng = np.random.RandomState(510)
+    for name, pol, ckw in [("rand", "rand", None), ("pid", "pid", {"action": {"scale_space": False}})]:
+        kw = copy.deepcopy(OBSNORM_KW)
+        if ckw:
+            kw.update(ckw)
+        env = G.make_env(False, 300, kw)
+        ep = G.env_episode(env, rng, False, 300, omega_deg=20.0, policy=pol)
+        for k, v in ep.items():
+            out[name + "__" + k] = v
+        out[name + "__scale_space"] = np.array(ckw is None)
+        out[name + "__obs_mean"] = np.array([float(o["mean"]) for o in env.cfg["observation"]["states"]])
+        out[name + "__obs_var"] = np.array([float(o["var"]) for o in env.cfg["observation"]["states"]])
+        out[name + "__obs_space"] = np.stack([env.observation_space.low, env.observation_space.high])
+        out[name + "__act_space"] = np.stack([env.action_space.low, env.action_space.high])
+        print("env obsnorm %s: %d steps, last term=%r" % (name, len(ep["rew"]), ep["term"][-1]))
+    out["config_kw"] = np.array(json.dumps(OBSNORM_KW))
+    np.savez_compressed(os.path.join(OUT, "env_obsnorm.npz"), **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["dryden", "pyfly", "env", "potential", "intwin"]
+    which = sys.argv[1:] or ["dryden", "pyfly", "env", "potential", "intwin", "obsnorm"]
     if "dryden" in which:
         gen_dryden_short()
     if "pyfly" in which:
@@ -191,3 +220,5 @@ if __name__ == "__main__":
         gen_env_potential()
     if "intwin" in which:
         gen_env_intwin()
+    if "obsnorm" in which:
+        gen_env_obsnorm()

@@ -637,3 +637,36 @@ def test_integration_window_reset_reads_previous_history():
     o_ora = ora.reset(iA, tA)
     np.testing.assert_allclose(obs[0].cpu().numpy()[ints], o_ora[ints], rtol=1e-9, atol=1e-9)
     eng.close()
+
+
+@pytest.mark.parametrize("precision", ["float64", "float32"])
+@pytest.mark.parametrize("name", ["rand", "pid"])
+def test_env_obs_normalize_derived(name, precision):
+    """observation.normalize with mean / var derived from the bounds (fixed_wing.py:142-161) on the device
+    against the reference's episodes (env_obsnorm.npz): fp64 within 1e-6 + 1e-6 / step, fp32 2e-3 (1 + |ref|)."""
+    import _fixtures as F
+    from test_golden_r05 import obsnorm_config_kw
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
+    d = F.load("env_obsnorm.npz")
+    g = lambda k: d[name + "__" + k]  # noqa: E731
+    spec = C.EnvSpec(config_kw=obsnorm_config_kw(d, name), sim_config_kw={"turbulence": False})
+    eng = Engine(spec.sim, spec, 1, device=DEV, precision=precision)
+    f64 = precision == "float64"
+    obs0 = eng.reset(init=F.env_init(g("init"))[:, None], target=g("target0")[:, None])
+    np.testing.assert_allclose(obs0[0].double().cpu().numpy(), g("obs")[0], rtol=1e-12 if f64 else 1e-5, atol=1e-6)
+    acts = torch.tensor(g("act"), dtype=eng.dtype, device=DEV)
+    for s in range(len(acts)):
+        obs, rew, done, _ = eng.env_step(acts[s:s + 1], auto_reset=False)
+        assert bool(done[0]) == bool(g("done")[s]), s
+        r, ref = float(rew[0]), float(g("rew")[s])
+        o = obs[0].double().cpu().numpy()
+        if f64:
+            tol = 1e-6 + 1e-6 * s
+            assert abs(r - ref) <= tol, (s, r, ref)
+            np.testing.assert_allclose(o, g("obs")[s + 1], rtol=1e-5, atol=tol)
+        else:
+            assert abs(r - ref) <= 2e-3 * (1 + abs(ref)), (s, r, ref)
+            np.testing.assert_allclose(o, g("obs")[s + 1], rtol=2e-3, atol=2e-3)
+        if bool(done[0]):
+            break
+    eng.close()

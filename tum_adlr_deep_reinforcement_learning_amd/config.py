@@ -561,9 +561,6 @@ class EnvSpec:
             raise NotImplementedError("observation.length %d / step %d" % (self.obs_length, self.obs_step))
         if (self.obs_length - 1) * self.obs_step + 2 > FW_MAX_OBS_HIST:
             raise NotImplementedError("observation history deeper than %d steps" % FW_MAX_OBS_HIST)
-        if obs_cfg.get("normalize", False) and any(o.get("mean") is None or o.get("var") is None
-                                                   for o in obs_cfg["states"] if o.get("norm", True)):
-            raise NotImplementedError("observation normalisation without explicit mean/var")
         # observation noise: val += np_random.normal(loc=mean, scale=var) (fixed_wing.py:1241-1242);
         # a zero-mean, zero-scale draw adds exactly 0.0, so it is not drawn at all
         noise = obs_cfg.get("noise")
@@ -580,8 +577,11 @@ class EnvSpec:
         self.rand_params = self._parse_model(cfg.get("simulator", {}).get("model"))
         self.scale_actions = bool(cfg["action"].get("scale_space", False))
         self.metrics_enabled = True  # track cfg["metrics"] on the device (False: skip that state traffic)
-        self.set_curriculum_level(curriculum_level)
+        # the spaces (and derived normalisation constants) read the simulator's bounds BEFORE the env config's
+        # "simulator" states are applied: the reference builds them in __init__ (fixed_wing.py:95-247) and
+        # applies those states in set_curriculum_level afterwards (:300)
         self._build_spaces()
+        self.set_curriculum_level(curriculum_level)
 
     def _parse_model(self, m):
         """The "simulator": {"model": ...} block -> fw_rand_param entries (sample_simulator_parameters,
@@ -667,6 +667,7 @@ class EnvSpec:
     def _build_spaces(self):
         cfg = self.cfg
         lo, hi = [], []
+        self._obs_bounds = []  # (high, low) per entry, before the relative-target span (fixed_wing.py:98-125)
         for o in cfg["observation"]["states"]:
             h = o.get("high")
             if h is None:
@@ -678,6 +679,7 @@ class EnvSpec:
                 low = self._state_bound(o["name"], "low")
             elif o.get("convert_to_radians", False):
                 low = float(np.radians(low))
+            self._obs_bounds.append((h, low))
             if o["type"] == "target" and o.get("value") == "relative":
                 if h != FLOAT32_MAX and low != -FLOAT32_MAX:
                     hi.append(h - low)
@@ -775,6 +777,13 @@ class EnvSpec:
             E.norm = int(norm_all and o.get("norm", True))
             E.mean = float(o.get("mean", 0.0) or 0.0)
             E.var_ = float(o.get("var", 1.0) or 1.0)
+            if norm_all:  # mean / var not given: derived from the bounds (fixed_wing.py:142-161), as written there
+                h, low = self._obs_bounds[i]
+                finite = h != FLOAT32_MAX and low != -FLOAT32_MAX
+                if o.get("mean") is None:
+                    E.mean = float(h - low) if finite else 0.0
+                if o.get("var") is None:
+                    E.var_ = float((h - low) / (4 ** 2)) if finite else 1.0
         a = cfg["action"]
         e.scale_actions = int(self.scale_actions)
         e.scale_low = float(a.get("scale_low", -1) if a.get("scale_low") is not None else -1)
