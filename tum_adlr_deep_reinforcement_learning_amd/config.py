@@ -897,8 +897,6 @@ class EnvSpec:
         if uses_iw and e.integration_window <= 0:
             # the reference sums the whole history then ([-0:]); no config does that
             raise NotImplementedError("integrator / int_error with integration_window 0")
-        if uses_iw and e.obs_noise and any(e.obs[o].kind == FW_OBS_TARGET_INT for o in range(e.n_obs)):
-            raise NotImplementedError("integrator observation with observation noise")
         return e
 
     def target_sampling(self):

@@ -398,13 +398,18 @@ template <typename T>
 __device__ __forceinline__ T iw_value(const DevCfg<T>& c, T sum, int x, T e0) {
   return x < c.iwin ? sum + T(c.iwin - x) * e0 : sum;
 }
-// the "integrator" entries of one length-1 observation row (v3: the raw values per target)
+// the "integrator" entries of one length-1 observation row (v3: the raw values per target).  The row was
+// written with 0 in their place; with observation noise that entry already carries its draw
+// (fixed_wing.py:1240-1247: normalise, then add the noise), so the value goes in as the difference.
 template <typename T>
 __device__ __forceinline__ void iw_obs(const DevCfg<T>& c, const T* v3, T* out) {
   if (!out) return;
   for (int o = 0; o < c.n_obs; o++) {
     const fw_obs_entry E = c.obs[o];
-    if (E.kind == FW_OBS_TARGET_INT) out[o] = obs_norm(E, pick3(v3, E.var));
+    if (E.kind == FW_OBS_TARGET_INT) {
+      const T v = obs_norm(E, pick3(v3, E.var));
+      out[o] = c.obs_noise ? out[o] + (v - obs_norm(E, T(0))) : v;
+    }
   }
 }
 // a fresh episode's error history: entry 0 in its ring slot, the sums of one entry
