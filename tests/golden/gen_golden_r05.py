@@ -179,6 +179,31 @@ def _fail_episode(env, rng, calm):
                 target=np.array(tgt))
 
 
+def gen_env_intwin_hist():
+    """integration_window with an observation history (length 3, step 2, vector): the integrator entries of
+    the lagged rows (fixed_wing.py:1165-1180, slice [-W-i:-i]), including an episode that ends in a
+    constraint violation (the failed step's lagged rows read the history one entry short)."""
+    import copy
+    out = {}
+    rng = np.random.RandomState(511)
+    hist = {"observation": {"length": 3, "step": 2, "shape": "vector"}}
+    for name, extra, smax, n, omega, scale in [
+            ("rand", {}, 300, 300, 20.0, 1.2),
+            ("rand_hot", {}, 300, 300, 200.0, 3.0),
+            ("fail_va", {"simulator": {"states": {5: {"constraint_max": 17.5}}}}, 2000, 600, 60.0, 1.2)]:
+        kw = copy.deepcopy(INTWIN_KW)
+        kw["observation"].update(copy.deepcopy(hist["observation"]))
+        kw.update(copy.deepcopy(extra))
+        env = G.make_env(False, smax, kw)
+        ep = G.env_episode(env, rng, False, n, act_scale=scale, omega_deg=omega, policy="rand")
+        for k, v in ep.items():
+            out[name + "__" + k] = v
+        out[name + "__scale_space"] = np.array(True)
+        out[name + "__extra_kw"] = np.array(json.dumps(dict(copy.deepcopy(extra), steps_max=smax, **hist)))
+        print("env intwin hist %s: %d steps, last term=%r" % (name, len(ep["rew"]), ep["term"][-1]))
+    np.savez_compressed(os.path.join(OUT, "env_intwin_hist.npz"), **out)
+
+
 # observation.normalize with entries that give no mean / var: the reference derives them from the bounds
 # (fixed_wing.py:142-161: mean = high - low, var = (high - low) / 16, or 0 / 1 for unbounded entries)
 OBSNORM_KW = {"observation": {"normalize": True, "states": {
@@ -209,7 +234,7 @@ def gen_env_obsnorm():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["dryden", "pyfly", "env", "potential", "intwin", "obsnorm"]
+    which = sys.argv[1:] or ["dryden", "pyfly", "env", "potential", "intwin", "obsnorm", "intwin_hist"]
     if "dryden" in which:
         gen_dryden_short()
     if "pyfly" in which:
@@ -222,3 +247,5 @@ if __name__ == "__main__":
         gen_env_intwin()
     if "obsnorm" in which:
         gen_env_obsnorm()
+    if "intwin_hist" in which:
+        gen_env_intwin_hist()

@@ -698,3 +698,37 @@ def test_integration_window_with_observation_noise():
         eng.close()
         outs.append(np.stack(rows))
     np.testing.assert_allclose(outs[1], outs[0] + 0.25, rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("name", ["rand", "rand_hot", "fail_va"])
+def test_integration_window_observation_history(name):
+    """integration_window 10 with an observation history (length 3, step 2): the integrator entries of the
+    lagged rows read slice [-W-i:-i] (fixed_wing.py:1165-1180), the reset rows the first reset's err x W,
+    and a failed step's lagged rows the history one entry short -- fp64 against the reference's own
+    episodes (env_intwin_hist.npz), rows beyond the episode up to their init-noise offset as in
+    test_gpu_obs.py."""
+    import _fixtures as F
+    from test_golden_r05 import intwin_config_kw
+    from test_gpu_obs import _check_obs
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
+    d = F.load("env_intwin_hist.npz")
+    g = lambda k: d[name + "__" + k]  # noqa: E731
+    spec = C.EnvSpec(config_kw=intwin_config_kw(d, name), sim_config_kw={"turbulence": False})
+    assert spec.obs_length == 3 and spec.n_obs == g("obs").shape[1]
+    eng = Engine(spec.sim, spec, 1, device=DEV, precision="float64")
+    eng.seed(3)
+    obs0 = eng.reset(init=F.env_init(g("init"))[:, None], target=g("target0")[:, None]).cpu().numpy()[0]
+    _check_obs(spec, obs0, g("obs")[0], 0, 1e-12, "reset")
+    acts = torch.tensor(g("act"), dtype=torch.float64, device=DEV)
+    for s in range(len(acts)):
+        obs, rew, done, _ = eng.env_step(acts[s:s + 1], auto_reset=False)
+        dn = bool(done[0])
+        assert dn == bool(g("done")[s]), s
+        o = eng.terminal_obs[0].cpu().numpy() if dn else obs[0].cpu().numpy()
+        tol = 1e-6 + 1e-6 * s
+        assert abs(float(rew[0]) - g("rew")[s]) <= tol, (s, float(rew[0]), g("rew")[s])
+        _check_obs(spec, o, g("obs")[s + 1], s + 1, tol, "step %d" % s)
+        if dn:
+            break
+    assert s == len(acts) - 1
+    eng.close()

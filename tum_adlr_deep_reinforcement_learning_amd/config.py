@@ -761,8 +761,6 @@ class EnvSpec:
                 elif val == "relative":
                     E.kind = FW_OBS_TARGET_REL
                 elif val == "integrator":  # fixed_wing.py:1160-1182
-                    if self.obs_length > 1:
-                        raise NotImplementedError("integrator target observation with observation.length > 1")
                     E.kind = FW_OBS_TARGET_INT
                 else:
                     raise NotImplementedError("target observation value %r" % val)

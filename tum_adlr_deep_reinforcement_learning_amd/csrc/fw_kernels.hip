@@ -398,17 +398,68 @@ template <typename T>
 __device__ __forceinline__ T iw_value(const DevCfg<T>& c, T sum, int x, T e0) {
   return x < c.iwin ? sum + T(c.iwin - x) * e0 : sum;
 }
-// the "integrator" entries of one length-1 observation row (v3: the raw values per target).  The row was
-// written with 0 in their place; with observation noise that entry already carries its draw
-// (fixed_wing.py:1240-1247: normalise, then add the noise), so the value goes in as the difference.
+// the "integrator" entries of observation row r (v3: the raw values per target).  The row was written with
+// 0 in their place; on the general path (observation noise, or a history row's init noise) that entry
+// already carries its draws (fixed_wing.py:1236-1247: + init noise, normalise, + noise), so the value goes
+// in as the difference.
 template <typename T>
-__device__ __forceinline__ void iw_obs(const DevCfg<T>& c, const T* v3, T* out) {
+__device__ __forceinline__ void iw_obs(const DevCfg<T>& c, const T* v3, T* out, int r = 0) {
   if (!out) return;
   for (int o = 0; o < c.n_obs; o++) {
     const fw_obs_entry E = c.obs[o];
     if (E.kind == FW_OBS_TARGET_INT) {
       const T v = obs_norm(E, pick3(v3, E.var));
-      out[o] = c.obs_noise ? out[o] + (v - obs_norm(E, T(0))) : v;
+      T& dst = out[r * c.n_obs + o];
+      dst = c.obs_general ? dst + (v - obs_norm(E, T(0))) : v;
+    }
+  }
+}
+// a reset observation: every history row is the lag-1 row (i > steps_count -> i = steps_count + 1 = 1)
+template <typename T>
+__device__ __forceinline__ void iw_obs_all_rows(const DevCfg<T>& c, const T* v3, T* out) {
+  for (int r = 0; r < c.obs_len; r++) iw_obs(c, v3, out, r);
+}
+// observation history (observation.length > 1): the raw row kept for later lags holds the integrator
+// entries' lag-1 values, so a lagged row reads slice [-W-i:-i] as the reference does (its padding condition
+// steps - i < W is the lag-1 one at step steps - i + 1).  dst: the history row just written by observe_full.
+template <typename T>
+__device__ __forceinline__ void iw_hist_row(const DevCfg<T>& c, const State<T>& s, int64_t i, const T* v3, T* dst) {
+  for (int o = 0; o < c.n_obs; o++)
+    if (c.obs[o].kind == FW_OBS_TARGET_INT) dst[(int64_t)o * s.ld + i] = pick3(v3, c.obs[o].var);
+}
+// the reset row kept for lags beyond the episode: slice [-W-steps-1:-steps-1] is empty and the padding
+// (W + 1) e0 (the current episode's entry 0), whatever the reset observation itself read
+template <typename T>
+__device__ __forceinline__ void iw_hist_init(const DevCfg<T>& c, const State<T>& s, int64_t i, const T* tgt,
+                                             const T* der) {
+  if (c.obs_hist == 0) return;
+  const T vals[3] = {der[0], der[1], der[3]};
+  T v3[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) v3[k] = target_error(c, k, tgt[k], vals[k]) * T(c.iwin + 1);
+  iw_hist_row(c, s, i, v3, s.obs_init);
+}
+// a failed step (ConstraintException): the error history was not appended, so a lagged row's slice ends one
+// entry earlier relative to steps_count, and its padding (W - (steps - i)) e0 holds one e0 less than the
+// stored lag-1 value of that step whenever the stored value was padded (row step at <= W)
+template <typename T>
+__device__ __forceinline__ void iw_obs_fail(const DevCfg<T>& c, const State<T>& s, int64_t i, int steps, uint32_t lep,
+                                            T* out) {
+  if (!out || c.obs_len <= 1) return;
+  const int64_t ld = s.ld;
+  for (int r = 1; r < c.obs_len; r++) {
+    const int lag = 1 + r * c.obs_step;
+    if (lag > steps) break;  // clamped rows: the reset row, (W + 1) e0 either way
+    const int at = steps - lag;
+    if (at > c.iwin) continue;
+    for (int o = 0; o < c.n_obs; o++) {
+      const fw_obs_entry E = c.obs[o];
+      if (E.kind != FW_OBS_TARGET_INT) continue;
+      const T v = at <= 0 ? s.obs_init[(int64_t)o * ld + i]
+                          : s.obs_ring[((int64_t)((lep + (uint32_t)at) % (uint32_t)c.obs_hist) * c.n_obs + o) * ld + i];
+      const T e0 = ld_(s.iws, IW_E0 + E.var, ld, i);
+      T& dst = out[r * c.n_obs + o];
+      dst = dst + (obs_norm(E, v - e0) - obs_norm(E, v));
     }
   }
 }
@@ -1002,7 +1053,10 @@ __global__ __launch_bounds__(BLOCK) void k_reset(const DevCfg<T>* __restrict__ c
       for (int a = 0; a < 3; a++) seq[j][a] = T(0);
     observe_env(c, s, i, s.episode[i], OBS_RESET, y, der, tgt, 0, seq, seq,
                 obs ? obs + i * (int64_t)c.n_obs * c.obs_len : nullptr, s.life[i]);
-    if (s.iws) iw_obs(c, rv, obs ? obs + i * (int64_t)c.n_obs * c.obs_len : nullptr);
+    if (s.iws) {
+      iw_obs_all_rows(c, rv, obs ? obs + i * (int64_t)c.n_obs * c.obs_len : nullptr);
+      iw_hist_init(c, s, i, tgt, der);
+    }
   }
 }
 
@@ -1043,7 +1097,8 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const DevCfg<T>* __restrict__
     T v[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) v[k] = iw_value(c, ld_(s.iws, IW_QP + k, ld, i), steps - 1, ld_(s.iws, IW_E0 + k, ld, i));
-    iw_obs(c, v, obs + i * (int64_t)c.n_obs * c.obs_len);
+    if (steps == 0) iw_obs_all_rows(c, v, obs + i * (int64_t)c.n_obs * c.obs_len);
+    else iw_obs(c, v, obs + i * (int64_t)c.n_obs * c.obs_len);
   }
 }
 
@@ -1381,7 +1436,10 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
     for (int k = 0; k < 3; k++) iwv[k] = iw_value(c, iqp[k], steps - 1, iwq[3 + k]);
   if (done && tobs_out) {
     observe_env(c, s, i, episode, omode, y, der, tgt, steps, seqA, seqC, tobs_out + i * ow, lep);
-    if (s.iws) iw_obs(c, iwv, tobs_out + i * ow);
+    if (s.iws) {
+      iw_obs(c, iwv, tobs_out + i * ow);
+      if (omode == OBS_FAIL) iw_obs_fail(c, s, i, steps, lep, tobs_out + i * ow);
+    }
   }
 
   rew_out[i] = reward;
@@ -1430,8 +1488,9 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
         T rv[3];
 #pragma unroll
         for (int k = 0; k < 3; k++) rv[k] = iw_value(c, iqp[k], -1, iwq[3 + k]);
-        iw_obs(c, rv, orow);
+        iw_obs_all_rows(c, rv, orow);
         iw_init(c, s, i, tr, dr, life0 + 1u);
+        iw_hist_init(c, s, i, tr, dr);
       }
       s.life[i] = life0 + 1u;
       FW_TSTAMP(5);
@@ -1440,7 +1499,11 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   }
 #ifndef FW_SKIP_OBS
   observe_env(c, s, i, episode, omode, y, der, tgt, steps, seqA, seqC, orow, lep);
-  if (s.iws) iw_obs(c, iwv, orow);
+  if (s.iws) {
+    iw_obs(c, iwv, orow);
+    if (omode == OBS_FAIL) iw_obs_fail(c, s, i, steps, lep, orow);
+    else if (c.obs_hist) iw_hist_row(c, s, i, iwv, s.obs_ring + (int64_t)((lep + (uint32_t)steps) % (uint32_t)c.obs_hist) * c.n_obs * ld);
+  }
 #endif
 #pragma unroll
   for (int r = 0; r < NY; r++) st_(s.y, r, ld, i, y[r]);
