@@ -160,8 +160,14 @@ def cpu_baseline(seconds=12.0, procs=None):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle import oracle as O
     O.build()  # compile once in the parent (workers only load it)
-    with mp.get_context("fork").Pool(procs) as pool:
+    # close() + join() let the workers exit on their own: leaving a `with Pool` block calls terminate(), whose
+    # SIGTERM put two "*** Aborted at" stacks into every profiler log of this command (round-5 review)
+    pool = mp.get_context("fork").Pool(procs)
+    try:
         res = pool.map(_cpu_worker, [(1000 + k, seconds) for k in range(procs)])
+    finally:
+        pool.close()
+        pool.join()
     steps = sum(r[0] for r in res)
     dt = max(r[1] for r in res)
     return {"value": steps / dt, "unit": "env-steps/s", "cores": procs, "kind": "port",

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FWSIM_ABI_VERSION 10
+#define FWSIM_ABI_VERSION 11
 
 /* ---- error codes ---------------------------------------------------------- */
 #define FW_OK 0
@@ -142,7 +142,7 @@ typedef struct fw_sim_config {
 
 /* ---- gym env configuration (fixed_wing_config.json) ------------------------ */
 #define FW_MAX_OBS 32
-#define FW_MAX_REW 8
+#define FW_MAX_REW 12   /* ABI 11: 8 -> 12 (the default 5 factors + success / step / goal classes) */
 #define FW_MAX_IWIN 256
 #define FW_MAX_WINDOW 16
 #define FW_MAX_OBS_LEN 16     /* observation.length (history rows) */
@@ -170,6 +170,13 @@ typedef struct fw_obs_entry {
 #define FW_REW_ACTION_VALUE 4
 #define FW_REW_STATE_INT_ERROR 5 /* var = target index: the sum of the last integration_window errors, padded
                                   * with the first (fixed_wing.py:1001-1012) */
+/* ABI 11 (fixed_wing.py:1020-1048) */
+#define FW_REW_SUCCESS 6        /* the step on which the env reaches its goal streak for the FIRST time in its
+                                 * lifetime (goal_achieved is never cleared, :81, 546-547): `value`, or with
+                                 * var = 1 ("timesteps") steps_max - steps_count; 0 on every other step */
+#define FW_REW_STEP 7           /* `value` on every successful step */
+#define FW_REW_GOAL 8           /* var = 0 ("per_state"): value / 3 per bounded target within its bound;
+                                 * var = 1 ("all"): value when every bounded target is within its bound */
 
 #define FW_FUN_LINEAR 0
 #define FW_FUN_QUADRATIC 1
@@ -182,11 +189,17 @@ typedef struct fw_rew_factor {
                                       * each reset draws the factor's scaling from U(scaling, scaling_hi) */
   double scaling, max, sign;         /* max = +inf if absent */
   double scaling_hi;
+  double value;                      /* ABI 11: "value" of the success / step / goal classes */
 } fw_rew_factor;
 
 /* target classes (fixed_wing.py:1363-1471) */
 #define FW_TGT_CONSTANT 0
 #define FW_TGT_COMPENSATE 1
+/* ABI 11: drawn by sample_target (fixed_wing.py:698-722) at every reset and resample, advanced by
+ * _get_next_target (:1433-1448); a target given explicitly at reset flies as "constant" for the episode
+ * (fixed_wing.py:444-448)                                                                              */
+#define FW_TGT_LINEAR 2         /* target += slope * dt; slope = +-U(slope_low, slope_high) */
+#define FW_TGT_SINUSOIDAL 3     /* amplitude sin(2 pi / period (steps_count + phase)) + bias */
 
 /* simulator parameter randomisation (FixedWingAircraft.sample_simulator_parameters,
  * fixed_wing.py:748-813: the env config's "simulator": {"model": {...}} block), one entry per
@@ -216,7 +229,7 @@ typedef struct fw_env_config {
   double target_delta[3];             /* NaN = none */
   double target_bound[3];             /* NaN = none */
   int32_t streak_req;                 /* <= 128; 0 disables goal */
-  int32_t on_success;                 /* 0 none, 1 done */
+  int32_t on_success;                 /* 0 none, 1 done, 2 new (ABI 11: sample_target on success, :551-552) */
   double streak_frac;
   int32_t n_rew;
   int32_t step_fail_timesteps;        /* reward.step_fail == "timesteps" */
@@ -251,6 +264,14 @@ typedef struct fw_env_config {
   int32_t n_rand;
   int32_t pad4_;
   fw_rand_param rand[FW_NPARAM];
+  /* ABI 11: the linear / sinusoidal target classes' draws (sample_target, fixed_wing.py:698-722), per target
+   * (roll, pitch, Va); slope and amplitude are drawn in the config's units and converted with np.radians
+   * where target_radians is set (convert_to_radians), the period is not converted                       */
+  int32_t target_radians[3];
+  int32_t pad11_;
+  double target_slope_low[3], target_slope_high[3];
+  double target_amp_low[3], target_amp_high[3];
+  double target_period_low[3], target_period_high[3];
 } fw_env_config;
 
 /* Episode-metric record written for every done env (SoA [FW_NMETRIC][N] so the stores
@@ -292,6 +313,8 @@ enum fw_init_field {
                                aircraft whose episodes started at different steps, so a wave's ring accesses
                                coalesce) and the two calls translate */
 #define FW_BLK_CMD_RING 8   /* window*3 rows, T: constrained commands, same layout (unscaled action windows) */
+#define FW_BLK_TARGET_PROPS 10 /* 12 rows, T (ABI 11; linear / sinusoidal target classes only): per target (roll, pitch,
+                                * Va) 4 rows: slope (linear) or amplitude, period, phase, bias (sinusoidal) */
 #define FW_BLK_GOAL 9       /* 4 rows, uint32: the last 128 goal-status bits ("all"), bit 0 of row 0 newest (0 before
                              * the episode's first entry).  Env handles only.  Setting it takes the episode's
                              * history length from FW_BLK_STEPS (steps_count + 1 entries): set FW_BLK_STEPS first */
@@ -322,13 +345,29 @@ int fw_seed(fw_handle* h, uint64_t seed, int64_t env_offset);
  * (fw_set_noise_lengths), which describe a buffer: set them again after it.                        */
 int fw_set_noise(fw_handle* h, const void* noise_dev, int64_t len);
 
+/* ABI 11: the env's own np_random draws from a caller tape instead of the handle's Philox streams, so a
+ * device episode can replay the reference's (FixedWingAircraft.np_random, fixed_wing.py:324-332).  tape_dev:
+ * [len][N] (handle precision), aircraft i consumes column i in order; each draw u is used as numpy's
+ * uniform(low, high) = low + (high - low) * u.  The draws, in the reference's order: at every reset
+ * (fw_reset, the auto-reset of fw_env_step / fw_env_rollout) sample_target per target (roll, pitch, Va):
+ * the initial value, then for class linear the slope and its sign (u < 0.5 flips it), for class sinusoidal
+ * the amplitude, the period and the phase (fixed_wing.py:654-722) -- also for a target given explicitly,
+ * which the reference draws and then overrides (:436-448); then one scaling per randomised reward factor
+ * (reward.randomize_scaling, :473-479).  At a resample (target.resample_every, on_success "new",
+ * :570-575): sample_target again.  Parameter randomisation (a "model" block) keeps its Philox draws.  Every
+ * call restarts the cursors at draw 0; a draw past len is NaN.  NULL: the Philox streams again.  The tape
+ * must stay alive while the handle uses it.                                                           */
+int fw_set_env_draws(fw_handle* h, const void* tape_dev, int32_t len);
+
 /* Per-env injection (env_method("reset", indices=..., turbulence_noise=...) -> FixedWingAircraft.reset
  * (**sim_reset_kw), fixed_wing.py:414-441): env_len_dev int32[N]; env i with env_len[i] > 0 reads its
  * first env_len[i] samples of the fw_set_noise buffer (column i, wrapped as above; env_len[i] <= the
- * buffer's len), env_len[i] == 0 draws from Philox.  The VecEnv auto-reset of fw_env_step /
- * fw_env_rollout zeroes env_len[i] (the SubprocVecEnv worker resets without turbulence_noise, so
- * Dryden.reset(None) draws fresh noise); fw_reset leaves it to the caller.  NULL: every env reads the
- * buffer (fw_set_noise alone).                                                                      */
+ * buffer's len), env_len[i] == 0 draws from Philox, env_len[i] < 0 reads the first -env_len[i]
+ * samples like a positive length but marks a shared (fw_set_noise-wide) sequence.  The VecEnv
+ * auto-reset of fw_env_step / fw_env_rollout zeroes a positive env_len[i] (the SubprocVecEnv worker
+ * resets without turbulence_noise, so Dryden.reset(None) draws fresh noise) and keeps a negative one,
+ * as an env without per-env lengths keeps the buffer; fw_reset leaves it to the caller.  NULL: every
+ * env reads the buffer (fw_set_noise alone).                                                        */
 int fw_set_noise_lengths(fw_handle* h, int32_t* env_len_dev);
 
 /* Masked reset.  mask_dev: uint8[N] (NULL = all).  init_dev: [FW_NINIT][N] or

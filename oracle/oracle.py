@@ -142,6 +142,12 @@ class OracleEnv:
             raise NotImplementedError("oracle: target.resample_every")
         if any(env_cfg.rew[k].randomize for k in range(env_cfg.n_rew)):
             raise NotImplementedError("oracle: reward.randomize_scaling (the device's Philox draws)")
+        # round 6 (ABI 11): pinned by the reference's own episodes on the device (tests/test_gpu_r06.py), not
+        # restated here
+        if any(env_cfg.target_class[k] >= C.FW_TGT["linear"] for k in range(3)) or env_cfg.on_success == 2 or \
+                any(env_cfg.rew[k].kind >= C.FW_REW_SUCCESS for k in range(env_cfg.n_rew)):
+            raise NotImplementedError("oracle: linear / sinusoidal targets, on_success new, success / step / goal "
+                                      "rewards")
         self.L = lib()
         self.sim_cfg, self.env_cfg, self.n_obs = sim_cfg, env_cfg, n_obs
         self.buf = ctypes.create_string_buffer(self.L.orc_env_state_size())

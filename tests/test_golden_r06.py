@@ -1,0 +1,102 @@
+"""Round 6, CPU: the env features pinned by env_r06.npz (tests/golden/gen_golden_r06.py) as the host compiles
+them into fw_env_config (ABI 11), and the fixtures' own consistency.
+
+  target classes   linear / sinusoidal draw bounds in the config's units + the np.radians flag
+                   (sample_target, fixed_wing.py:698-722); attitude_angular refused loudly
+  on_success       "none" / "done" / "new" -> 0 / 1 / 2 (fixed_wing.py:548-559)
+  reward classes   success (value, "timesteps"), step, goal (per_state, all) (fixed_wing.py:1020-1048)
+  tapes            every draw in [0, 1); the draw counts the reference's call order implies
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import _fixtures as F
+from tum_adlr_deep_reinforcement_learning_amd import config as C
+
+R06 = ["linear", "linear_fix", "sinus", "resample", "success"]
+
+
+def r06_spec(name, tmpdir):
+    """EnvSpec of an env_r06.npz case (writes the stored reference config file to tmpdir)."""
+    d = F.load("env_r06.npz")
+    path = os.path.join(str(tmpdir), name + ".json")
+    with open(path, "w") as f:
+        f.write(str(d[name + "__config_json"]))
+    spec = C.EnvSpec(config_path=path, config_kw={"steps_max": int(d[name + "__steps_max"])},
+                     sim_config_kw={"turbulence": False})
+    return spec, d
+
+
+def draws_per_sample(spec):
+    """np_random.uniform calls of one sample_target (fixed_wing.py:667-722) for this config."""
+    n = 0
+    for name in ("roll", "pitch", "Va"):
+        cls = spec.target_props[name].get("class", "constant")
+        n += 1 + (2 if cls == "linear" else 3 if cls == "sinusoidal" else 0)
+    return n
+
+
+@pytest.mark.parametrize("name", R06)
+def test_r06_config_struct(name, tmpdir):
+    spec, d = r06_spec(name, tmpdir)
+    cfg = json.loads(str(d[name + "__config_json"]))
+    e = spec.struct()
+    for i, st in enumerate(cfg["target"]["states"]):
+        cls = st.get("class", "constant")
+        assert e.target_class[i] == C.FW_TGT[cls]
+        assert e.target_radians[i] == int(bool(st.get("convert_to_radians", False)))
+        if cls == "linear":
+            assert (e.target_slope_low[i], e.target_slope_high[i]) == (st["slope_low"], st["slope_high"])
+        if cls == "sinusoidal":
+            assert (e.target_amp_low[i], e.target_amp_high[i]) == (st["amplitude_low"], st["amplitude_high"])
+            assert (e.target_period_low[i], e.target_period_high[i]) == (st.get("period_low", 250),
+                                                                          st.get("period_high", 500))
+    assert e.on_success == C.FW_ON_SUCCESS[cfg["target"].get("on_success", "none")]
+    assert e.resample_every == int(cfg["target"].get("resample_every", 0))
+    assert e.n_rew == len(cfg["reward"]["factors"])
+    for k, f in enumerate(cfg["reward"]["factors"]):
+        F_ = e.rew[k]
+        if f["class"] == "success":
+            assert F_.kind == C.FW_REW_SUCCESS
+            assert (F_.var == 1) == (f["value"] == "timesteps")
+            if f["value"] != "timesteps":
+                assert F_.value == f["value"]
+        elif f["class"] == "step":
+            assert F_.kind == C.FW_REW_STEP and F_.value == f["value"]
+        elif f["class"] == "goal":
+            assert F_.kind == C.FW_REW_GOAL and F_.var == int(f["type"] == "all") and F_.value == f["value"]
+        if isinstance(f["scaling"], list):
+            assert F_.randomize == 1 and (F_.scaling, F_.scaling_hi) == tuple(f["scaling"])
+
+
+@pytest.mark.parametrize("name", R06)
+def test_r06_tapes(name, tmpdir):
+    """The recorded draws are numpy random_sample() values, as many per episode as the reference's calls:
+    one sample_target at the reset, one per resample, plus one per randomised reward factor at the reset."""
+    spec, d = r06_spec(name, tmpdir)
+    per = draws_per_sample(spec)
+    n_rsc = sum(1 for f in spec.cfg["reward"]["factors"] if isinstance(f["scaling"], list))
+    for ep in range(int(d[name + "__episodes"])):
+        tape = d["%s__ep%d__tape" % (name, ep)]
+        assert np.all((tape >= 0) & (tape < 1))
+        resamples = (len(tape) - per - n_rsc) / per
+        assert resamples == int(resamples) and resamples >= 0, (ep, len(tape), per)
+        if name == "resample":
+            assert int(resamples) == len(d["%s__ep%d__rew" % (name, ep)]) // 60  # every 60 steps
+        if name == "success" and ep == 0:
+            assert resamples >= 2  # several successes: the success reward fires on the first one only
+
+
+def test_attitude_angular_refused(tmpdir):
+    """attitude_angular turns omega_p / q / r into targets (fixed_wing.py:671-675, 1558-1642): not built."""
+    _, d = r06_spec("linear", tmpdir)
+    cfg = json.loads(str(d["linear__config_json"]))
+    cfg["target"]["states"][0]["class"] = "attitude_angular"
+    path = os.path.join(str(tmpdir), "aa.json")
+    with open(path, "w") as f:
+        json.dump(cfg, f)
+    with pytest.raises(NotImplementedError):
+        C.EnvSpec(config_path=path, sim_config_kw={"turbulence": False}).struct()

@@ -1,0 +1,111 @@
+"""GPU tests of round 6, all through the C ABI.
+
+  env-draw tape     fw_set_env_draws (ABI 11): the reference's own episodes (env_r06.npz) replayed with the draws
+                    its np_random made -- linear / sinusoidal target classes (an explicit target at reset
+                    flying as constant), target.resample_every with reward.randomize_scaling, on_success
+                    "new" with the success / step / goal reward classes.  fp64: rewards within 1e-6 + 1e-6 /
+                    step, observations and targets likewise, done identical; fp32: within 2e-3 (1 + |ref|)
+                    (the success case: the same resample steps, the success reward on the same step, then
+                    the first 300 steps at that tolerance: fp32 flight drifts within a 1400-step PID episode)
+"""
+import numpy as np
+import pytest
+import torch
+
+import _fixtures as F
+from test_golden_r06 import R06, r06_spec
+from tum_adlr_deep_reinforcement_learning_amd import config as C
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _replay(name, precision, tmpdir, lanes=0):
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
+    spec, d = r06_spec(name, tmpdir)
+    eps = int(d[name + "__episodes"])
+    g = lambda ep, k: d["%s__ep%d__%s" % (name, ep, k)]  # noqa: E731
+    eng = Engine(spec.sim, spec, eps, device=DEV, precision=precision, lanes=lanes)
+    L = max(len(g(ep, "tape")) for ep in range(eps))
+    tape = np.full((L + 1, eps), np.nan)
+    for ep in range(eps):
+        tape[:len(g(ep, "tape")), ep] = g(ep, "tape")
+    eng.set_env_draws(tape)
+    init = np.stack([F.env_init(g(ep, "init")) for ep in range(eps)], axis=1)
+    tin = np.stack([g(ep, "target0_given") for ep in range(eps)], axis=1)
+    obs0 = eng.reset(init=init, target=tin).double().cpu().numpy()
+    n = max(len(g(ep, "rew")) for ep in range(eps))
+    out = {"obs": [obs0], "rew": [], "done": [], "tgt": [eng.get_block(C.FW_BLK_TARGET).double().cpu().numpy()]}
+    live = np.ones(eps, bool)
+    for s in range(n):
+        acts = np.zeros((eps, 3))
+        for ep in range(eps):
+            if s < len(g(ep, "act")):
+                acts[ep] = g(ep, "act")[s]
+        o, r, dn, _ = eng.env_step(torch.tensor(acts, dtype=eng.dtype, device=DEV), auto_reset=False)
+        out["obs"].append(o.double().cpu().numpy())
+        out["rew"].append(r.double().cpu().numpy())
+        out["done"].append(dn.cpu().numpy().astype(bool))
+        out["tgt"].append(eng.get_block(C.FW_BLK_TARGET).double().cpu().numpy())
+        live &= ~out["done"][-1]
+    eng.close()
+    return d, g, eps, out
+
+
+@pytest.mark.parametrize("precision", ["float64", "float32"])
+@pytest.mark.parametrize("name", R06)
+def test_env_draw_tape_replays_reference_episodes(name, precision, tmpdir):
+    d, g, eps, out = _replay(name, precision, tmpdir)
+    f64 = precision == "float64"
+    for ep in range(eps):
+        rew, obs, tgt = g(ep, "rew"), g(ep, "obs"), g(ep, "target")
+        np.testing.assert_allclose(out["obs"][0][ep], obs[0], rtol=1e-9 if f64 else 1e-5, atol=1e-9 if f64 else 1e-5)
+        np.testing.assert_allclose(out["tgt"][0][:, ep], tgt[0], rtol=0, atol=1e-12 if f64 else 1e-6)
+        steps = len(rew)
+        if not f64 and name == "success":
+            # the goal-streak steps (resamples) and the first-success reward on the same steps as the reference
+            ref_jump = np.nonzero(np.abs(np.diff(tgt[:, 0])) > 1e-9)[0]
+            dev_t = np.array([out["tgt"][s][0, ep] for s in range(steps + 1)])
+            dev_jump = np.nonzero(np.abs(np.diff(dev_t)) > 1e-6)[0]
+            assert len(dev_jump) == len(ref_jump) and np.all(np.abs(dev_jump - ref_jump) <= 2), (ref_jump, dev_jump)
+            dev_rew = np.array([out["rew"][s][ep] for s in range(steps)])
+            assert np.argmax(rew) == np.argmax(dev_rew)
+            steps = 300
+        for s in range(steps):
+            assert bool(out["done"][s][ep]) == bool(g(ep, "done")[s]), (ep, s)
+            r, ref = out["rew"][s][ep], rew[s]
+            o, t = out["obs"][s + 1][ep], out["tgt"][s + 1][:, ep]
+            if f64:
+                tol = 1e-6 + 1e-6 * s
+                assert abs(r - ref) <= tol, (ep, s, r, ref)
+                np.testing.assert_allclose(o, obs[s + 1], rtol=1e-5, atol=tol, err_msg="ep %d step %d" % (ep, s))
+                np.testing.assert_allclose(t, tgt[s + 1], rtol=1e-6, atol=tol, err_msg="ep %d step %d" % (ep, s))
+            else:
+                assert abs(r - ref) <= 2e-3 * (1 + abs(ref)), (ep, s, r, ref)
+                np.testing.assert_allclose(o, obs[s + 1], rtol=2e-3, atol=2e-3, err_msg="ep %d step %d" % (ep, s))
+                np.testing.assert_allclose(t, tgt[s + 1], rtol=2e-3, atol=2e-3, err_msg="ep %d step %d" % (ep, s))
+
+
+@pytest.mark.parametrize("lanes", [1, 4])
+def test_env_draw_tape_both_integrators(lanes, tmpdir):
+    """The tape path is integrator-independent: the sinusoidal episodes replay with either lanes setting."""
+    d, g, eps, out = _replay("sinus", "float64", tmpdir, lanes=lanes)
+    for ep in range(eps):
+        rew = g(ep, "rew")
+        dev = np.array([out["rew"][s][ep] for s in range(len(rew))])
+        assert np.all(np.abs(dev - rew) <= 1e-6 + 1e-6 * np.arange(len(rew)))
+
+
+def test_env_draw_tape_exhausted_is_nan(tmpdir):
+    """A draw past the tape's end is NaN (a wrong replay fails loudly instead of drawing Philox values)."""
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
+    spec, d = r06_spec("linear", tmpdir)
+    eng = Engine(spec.sim, spec, 2, device=DEV, precision="float64")
+    eng.set_env_draws(np.full((2, 2), 0.5))  # 2 of the 7 draws a linear reset needs
+    eng.reset()
+    t = eng.get_block(C.FW_BLK_TARGET).cpu().numpy()
+    assert np.isfinite(t[0]).all() and np.isnan(t[2]).all()  # roll from the tape; Va past its end
+    eng.set_env_draws(None)  # Philox again
+    eng.reset()
+    assert np.isfinite(eng.get_block(C.FW_BLK_TARGET).cpu().numpy()).all()
+    eng.close()

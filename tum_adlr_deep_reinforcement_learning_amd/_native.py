@@ -22,7 +22,7 @@ SOURCES = UNITS + [os.path.join(CSRC, "fw_device.hpp"), os.path.join(CSRC, "fw_q
 ARCH = os.environ.get("FWSIM_ARCH", "gfx950")
 
 _lib = None
-ABI_VERSION = 10  # include/fwsim.h FWSIM_ABI_VERSION
+ABI_VERSION = 11  # include/fwsim.h FWSIM_ABI_VERSION
 
 
 class FwError(RuntimeError):
@@ -124,6 +124,7 @@ SIGNATURES = {
     "fw_seed": (_c.c_int, [_vp, _c.c_uint64, _i64]),
     "fw_set_noise": (_c.c_int, [_vp, _vp, _i64]),
     "fw_set_noise_lengths": (_c.c_int, [_vp, _vp]),
+    "fw_set_env_draws": (_c.c_int, [_vp, _vp, _i32]),
     "fw_quad_auto_max": (_i64, []),
     "fw_reset": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "fw_sim_step": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),

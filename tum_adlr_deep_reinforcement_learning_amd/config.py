@@ -54,10 +54,11 @@ FW_TERM_NONE, FW_TERM_STEPS, FW_TERM_SUCCESS = 0, 100, 101
 
 FW_OBS_STATE, FW_OBS_TARGET_ABS, FW_OBS_TARGET_REL, FW_OBS_ACTION_WINDOW, FW_OBS_TARGET_INT = range(5)
 (FW_REW_STATE_ERROR, FW_REW_STATE_VALUE, FW_REW_ACTION_DELTA, FW_REW_ACTION_BOUND, FW_REW_ACTION_VALUE,
- FW_REW_STATE_INT_ERROR) = range(6)
+ FW_REW_STATE_INT_ERROR, FW_REW_SUCCESS, FW_REW_STEP, FW_REW_GOAL) = range(9)
 FW_FUN = {"linear": 0, "quadratic": 1, "exponential": 2}
-FW_TGT = {"constant": 0, "compensate": 1}
-FW_MAX_OBS, FW_MAX_REW, FW_MAX_WINDOW, FW_MAX_IWIN = 32, 8, 16, 256
+FW_TGT = {"constant": 0, "compensate": 1, "linear": 2, "sinusoidal": 3}
+FW_ON_SUCCESS = {"none": 0, "done": 1, "new": 2}
+FW_MAX_OBS, FW_MAX_REW, FW_MAX_WINDOW, FW_MAX_IWIN = 32, 12, 16, 256
 FW_MAX_OBS_LEN, FW_MAX_OBS_HIST = 16, 64
 
 (FW_I_ROLL, FW_I_PITCH, FW_I_YAW, FW_I_P, FW_I_Q, FW_I_R, FW_I_PN, FW_I_PE, FW_I_PD, FW_I_U, FW_I_V, FW_I_W,
@@ -65,7 +66,7 @@ FW_MAX_OBS_LEN, FW_MAX_OBS_HIST = 16, 64
  FW_I_WIND_D, FW_NINIT) = range(22)
 
 (FW_BLK_ODE, FW_BLK_DERIVED, FW_BLK_TARGET, FW_BLK_WIND, FW_BLK_STEPS, FW_BLK_COMMAND, FW_BLK_PARAMS,
- FW_BLK_ACT_RING, FW_BLK_CMD_RING, FW_BLK_GOAL) = range(10)
+ FW_BLK_ACT_RING, FW_BLK_CMD_RING, FW_BLK_GOAL, FW_BLK_TARGET_PROPS) = range(11)
 FW_DIST_GAUSSIAN, FW_DIST_UNIFORM = 0, 1
 
 # episode-metric record (include/fwsim.h FW_M_*): name -> (first column, info keys)
@@ -126,7 +127,7 @@ class FwRewFactor(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("var", ctypes.c_int32), ("window", ctypes.c_int32),
                 ("fun", ctypes.c_int32), ("shaping", ctypes.c_int32), ("randomize", ctypes.c_int32),
                 ("scaling", ctypes.c_double), ("max", ctypes.c_double), ("sign", ctypes.c_double),
-                ("scaling_hi", ctypes.c_double)]
+                ("scaling_hi", ctypes.c_double), ("value", ctypes.c_double)]
 
 
 class FwRandParam(ctypes.Structure):
@@ -157,7 +158,11 @@ class FwEnvConfig(ctypes.Structure):
                 ("obs_noise", ctypes.c_int32), ("integration_window", ctypes.c_int32),
                 ("obs_noise_mean", ctypes.c_double), ("obs_noise_std", ctypes.c_double),
                 ("n_rand", ctypes.c_int32), ("pad4_", ctypes.c_int32),
-                ("rand", FwRandParam * FW_NPARAM)]
+                ("rand", FwRandParam * FW_NPARAM),
+                ("target_radians", ctypes.c_int32 * 3), ("pad11_", ctypes.c_int32),
+                ("target_slope_low", ctypes.c_double * 3), ("target_slope_high", ctypes.c_double * 3),
+                ("target_amp_low", ctypes.c_double * 3), ("target_amp_high", ctypes.c_double * 3),
+                ("target_period_low", ctypes.c_double * 3), ("target_period_high", ctypes.c_double * 3)]
 
 
 # ---------------------------------------------------------------------------
@@ -394,35 +399,25 @@ def dryden_bank_sim(bank, noise, L, k_end):
 
 
 def dryden_fir(turb_len, dt, wingspan, intensity):
-    """FIR taps g0 (u[k-1]) and g1 (u[k]) of the six Dryden outputs for the reference's wiring.
+    """FIR taps g0 (u[k-1]) and g1 (u[k]) of the six Dryden outputs for the reference's wiring, or None when
+    the chunk is too short for the reduction (then dryden_bank, the stateful filter bank, applies).
 
     Wind passes (sim_length, dt, b) positionally into DrydenGustModel(dt, b, h)
     (pyfly.py:781-783 vs dryden.py:52), so the filter's noise spacing is
     ``turb_len`` s, its "wingspan" ``dt`` and its altitude the real wingspan.
-    lsim (first-order hold) then steps L*L/(L-1) seconds per sample, where the
-    state transition e^{A*dT} vanishes and each output is exactly
+    lsim (first-order hold, _foh) then steps L*L/(L-1) seconds per sample; where the
+    state transition e^{A*dT} vanishes (|Ad| <= 1e-30) each output is exactly
     g0*u[k-1] + g1*u[k] (and 0 at the first sample of every chunk).
     """
-    from scipy.linalg import expm  # host-side config only
-
     filt = dryden_filters(turb_len, dt, wingspan, 25.0, intensity)
     L = int(turb_len)
     dT = (L * float(turb_len)) / (L - 1) if L > 1 else float(turb_len)
     g0, g1 = np.zeros(6), np.zeros(6)
     for i, name in enumerate(["H_u", "H_v", "H_w", "H_p", "H_q", "H_r"]):
         A, B, C = _tf2ss(*filt[name])
-        n = A.shape[0]
-        M = np.zeros((n + 2, n + 2))
-        M[:n, :n] = A * dT
-        M[:n, n:n + 1] = B * dT
-        M[n, n + 1] = 1.0
-        E = expm(M)
-        Ad = E[:n, :n]
-        Bd1 = E[:n, n + 1:n + 2]
-        Bd0 = E[:n, n:n + 1] - Bd1
+        Ad, Bd0, Bd1 = _foh(A, B, dT)
         if np.max(np.abs(Ad)) > 1e-30:
-            raise NotImplementedError("Dryden chunk length %d too short for the FIR reduction "
-                                      "(|Ad|=%g); the stateful filter bank is not implemented" % (L, np.abs(Ad).max()))
+            return None  # not reducible: the filters keep state between samples
         g0[i] = float((C @ Bd0)[0, 0])
         g1[i] = float((C @ Bd1)[0, 0])
     return g0, g1
@@ -513,11 +508,11 @@ class SimSpec:
         c.turbulence = int(bool(cfg["turbulence"]))
         c.turb_len = int(cfg.get("turbulence_sim_length", 300))
         if c.turbulence:
-            try:
-                g0, g1 = dryden_fir(c.turb_len, c.dt, float(self.params["b"]), cfg["turbulence_intensity"])
+            fir = dryden_fir(c.turb_len, c.dt, float(self.params["b"]), cfg["turbulence_intensity"])
+            if fir is not None:
                 for i in range(6):
-                    c.dryden_g0[i], c.dryden_g1[i] = g0[i], g1[i]
-            except NotImplementedError:  # short chunks: the stateful filter bank (fw_sim_config.dryden_state)
+                    c.dryden_g0[i], c.dryden_g1[i] = fir[0][i], fir[1][i]
+            else:  # short chunks: the stateful filter bank (fw_sim_config.dryden_state)
                 bank = dryden_bank(c.turb_len, c.dt, float(self.params["b"]), cfg["turbulence_intensity"])
                 c.dryden_state, c.dryden_ncut = 1, int(bank["ncut"])
                 for name, n in (("ad", 28), ("e1", 28), ("b0", 12), ("b1", 12), ("c", 12)):
@@ -569,8 +564,8 @@ class EnvSpec:
             self.obs_noise = (float(noise.get("mean", 0)), float(noise.get("var", 0)))
         if cfg["reward"].get("form", "absolute") not in ("absolute", "potential"):
             raise NotImplementedError("reward.form %r" % cfg["reward"].get("form"))
-        if cfg["target"].get("on_success", "none") not in ("none", "done"):
-            raise NotImplementedError("target.on_success=%r" % cfg["target"].get("on_success"))
+        if cfg["target"].get("on_success", "none") not in FW_ON_SUCCESS:
+            raise ValueError("Unexpected goal action {}".format(cfg["target"].get("on_success")))  # fixed_wing.py:553-559
         sim_keys = set(cfg.get("simulator", {}).keys()) - {"states", "model"}
         if sim_keys:  # setattr(simulator, key, sample) of arbitrary simulator attributes (fixed_wing.py:802-813)
             raise NotImplementedError("randomised simulator attributes %s (only 'model' parameters)" % sorted(sim_keys))
@@ -798,10 +793,19 @@ class EnvSpec:
         for i, name in enumerate(tnames):
             p = self.target_props[name]
             cls = p.get("class", "constant")
-            if cls not in FW_TGT:
+            if cls == "attitude_angular":
+                # targets omega_p / q / r derived from the roll / pitch errors (fixed_wing.py:671-675, 1455-1460,
+                # 1558-1642): a target set beyond (roll, pitch, Va) -- not built
                 raise NotImplementedError("target class %r" % cls)
+            if cls not in FW_TGT:
+                raise ValueError("Unexpected target class {}".format(cls))
             if cls == "compensate" and name != "Va":
+                # Va only (fixed_wing.py:1378-1431: pitch raises NotImplementedError, others ValueError)
                 raise NotImplementedError("compensate target for %s" % name)
+            if cls == "compensate" and self.target_props["pitch"].get("class", "constant") not in \
+                    ("constant", "linear", "sinusoidal"):
+                raise ValueError("Invalid combination of state Va target class compensate and pitch target class "
+                                 "{}".format(self.target_props["pitch"].get("class")))
             e.target_class[i] = FW_TGT[cls]
             e.target_wrap[i] = int(self.sim.vars[name].wrap)
             rad = p.get("convert_to_radians", False)
@@ -810,6 +814,14 @@ class EnvSpec:
             e.target_high[i] = cv(p["high"])
             e.target_delta[i] = cv(p["delta"]) if p.get("delta") is not None else float("nan")
             e.target_bound[i] = cv(p["bound"]) if p.get("bound") is not None else float("nan")
+            # the class draws of sample_target (fixed_wing.py:698-722), in config units: np.radians on the device
+            e.target_radians[i] = int(bool(rad))
+            if cls == "linear":
+                e.target_slope_low[i], e.target_slope_high[i] = float(p["slope_low"]), float(p["slope_high"])
+            elif cls == "sinusoidal":
+                e.target_amp_low[i], e.target_amp_high[i] = float(p["amplitude_low"]), float(p["amplitude_high"])
+                e.target_period_low[i] = float(p.get("period_low", 250))
+                e.target_period_high[i] = float(p.get("period_high", 500))
         t = cfg["target"]
         names = [m["name"] for m in cfg.get("metrics", [])]
         unknown = set(names) - set(METRIC_LAYOUT)
@@ -826,7 +838,7 @@ class EnvSpec:
         if e.streak_req > 128:
             raise NotImplementedError("success_streak_req > 128")
         e.streak_frac = float(t["success_streak_fraction"])
-        e.on_success = 1 if t.get("on_success", "none") == "done" else 0
+        e.on_success = FW_ON_SUCCESS[t.get("on_success", "none")]  # fixed_wing.py:548-559
         r = cfg["reward"]
         fails = r.get("step_fail", 0)
         e.step_fail_timesteps = int(fails == "timesteps")
@@ -847,7 +859,7 @@ class EnvSpec:
         e.n_rew = len(r["factors"])
         for i, f in enumerate(r["factors"]):
             F = e.rew[i]
-            cls, typ = f["class"], f["type"]
+            cls, typ = f["class"], f.get("type")
             if cls == "action":
                 if typ == "value":
                     F.kind = FW_REW_ACTION_VALUE
@@ -871,8 +883,20 @@ class EnvSpec:
                     F.kind, F.var = FW_REW_STATE_INT_ERROR, TARGET_INDEX[f["name"]]
                 else:
                     raise NotImplementedError("state reward type %r" % typ)
+            elif cls == "success":  # fixed_wing.py:1020-1026
+                F.kind = FW_REW_SUCCESS
+                if f["value"] == "timesteps":
+                    F.var = 1
+                else:
+                    F.value = float(f["value"])
+            elif cls == "step":  # :1028-1029
+                F.kind, F.value = FW_REW_STEP, float(f["value"])
+            elif cls == "goal":  # :1031-1048
+                if typ not in ("per_state", "all"):
+                    raise ValueError("Unexpected reward type {} for class goal".format(typ))
+                F.kind, F.var, F.value = FW_REW_GOAL, int(typ == "all"), float(f["value"])
             else:
-                raise NotImplementedError("reward class %r" % cls)
+                raise ValueError("Unexpected reward component type {}".format(cls))
             fc = f["function_class"]
             if fc not in FW_FUN:
                 raise ValueError("Unexpected function class {} for {}".format(fc, f["name"]))

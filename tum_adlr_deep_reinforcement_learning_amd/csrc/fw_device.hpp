@@ -136,6 +136,10 @@ struct DevCfg {
   int target_class[3], target_wrap[3];
   T target_low[3], target_high[3], target_delta[3], target_bound[3];
   int has_delta[3], has_bound[3];
+  // linear / sinusoidal target classes (fw_env_config ABI 11): draw bounds, np.radians factor (1 or pi/180)
+  int tprops;                          // some target is linear or sinusoidal: State::tpr rows are kept
+  T tgt_rad[3], tgt_slo[3], tgt_shi[3], tgt_alo[3], tgt_ahi[3], tgt_plo[3], tgt_phi[3];
+  int goal_flag;                       // a success reward factor: State::gflag keeps goal_achieved
   T streak_frac;
   T step_fail_value;
   T term_weight[3];
@@ -1517,15 +1521,22 @@ FW_HD uint32_t goal_status_bits(const DevCfg<T>& c, const T* tgt, const T* vals)
   return bits | (all << 3);
 }
 
-// _get_next_target (fixed_wing.py:1363-1471): constant / compensate(Va)
-template <typename T>
-FW_HD void next_target(const DevCfg<T>& c, int steps_tgt, T* tgt) {
+// _get_next_target (fixed_wing.py:1363-1471): constant / compensate(Va) / linear / sinusoidal.  tp: the
+// aircraft's target properties (per target: slope or amplitude, period, phase, bias; State::tpr), read only
+// for the linear / sinusoidal classes; steps = steps_count after the step (the sinusoid's argument)
+template <typename T, typename TP>
+FW_HD void next_target(const DevCfg<T>& c, int steps_tgt, int steps, TP tp, T* tgt) {
   T res[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     T r = tgt[k];
-    if (c.target_class[k] == FW_TGT_COMPENSATE) {
-      const T pitch_tar = tgt[1];
+    if (c.target_class[k] == FW_TGT_LINEAR) {  // :1433-1435
+      r = tgt[k] + tp(4 * k) * c.dt;
+    } else if (c.target_class[k] == FW_TGT_SINUSOIDAL) {  // :1438-1448
+      r = tp(4 * k) * sin(T(2.0 * PI_D) / tp(4 * k + 1) * ((T)steps + tp(4 * k + 2))) + tp(4 * k + 3);
+    } else if (c.target_class[k] == FW_TGT_COMPENSATE) {
+      // pitch_tar: the pitch target (constant, linear) or the sinusoid's bias (:1381-1392)
+      const T pitch_tar = c.target_class[1] == FW_TGT_SINUSOIDAL ? tp(4 * 1 + 3) : tgt[1];
       const T deg = T(PI_D / 180.0);
       if (pitch_tar <= T(-2.5) * deg) {
         const T va_target = tgt[2];

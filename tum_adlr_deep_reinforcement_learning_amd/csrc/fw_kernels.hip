@@ -124,7 +124,7 @@ struct State {
   T* iws;             // [9][ld]
   const T* noise;     // injected N(0,1) turbulence noise [4][noise_len][ld] or null
   int64_t noise_len;
-  int32_t* noise_env_len;  // [ld] per-env injected length (0: Philox; zeroed by the auto-reset) or null: all
+  int32_t* noise_env_len;  // [ld] per-env injected length (> 0 own, zeroed by the auto-reset; < 0 shared; 0 Philox) or null
   uint32_t key0, key1;  // Philox key = seed
   uint32_t env_offset;
   T* met;             // [MT_ROWS][ld] streaming episode-metric sums (null: metrics off)
@@ -133,6 +133,12 @@ struct State {
   T* obs_init;        // [n_obs][ld] raw observation row at the episode's reset (null: length-1 observations)
   T* obs_ring;        // [obs_hist][n_obs][ld] raw rows of past steps, slot = (L_ep + step) % obs_hist
   T* prm;             // [FW_NPARAM][ld] per-aircraft parameters (null: no randomisation)
+  T* tpr;             // [12][ld] linear / sinusoidal target properties, per target: slope or amplitude, period,
+                      // phase, bias (null: constant / compensate targets only)
+  uint32_t* gflag;    // [ld] bit 0: goal_achieved, never cleared (fixed_wing.py:81, 546-547; null: no success reward)
+  uint32_t* dcur;     // [ld] next draw of the env-draw tape (fw_set_env_draws)
+  const T* tape;      // [tape_len][n] the env's np_random draws, or null: Philox
+  int32_t tape_len;
   // collect epilogue of k_env_step (fw_set_collect_epilogue; all null: off)
   double* col_ret;    // [n] VecNormalize discounted return, or null
   double col_gamma;
@@ -208,7 +214,8 @@ __device__ __forceinline__ void st_(T* p, int64_t row, int64_t ld, int64_t i, T 
 template <typename T>
 __device__ __forceinline__ void noise4(const State<T>& s, int64_t i, uint32_t episode, int k, T u[4]) {
   if (s.noise) {
-    const int64_t len = s.noise_env_len ? (int64_t)s.noise_env_len[i] : s.noise_len;
+    // per-env lengths: > 0 an env's own injection, < 0 the shared set_noise sequence (kept across resets), 0 Philox
+    const int64_t len = s.noise_env_len ? (int64_t)abs(s.noise_env_len[i]) : s.noise_len;
     if (len > 0) {
       const int64_t kk = (int64_t)((uint32_t)k % (uint32_t)len);  // len < 2^31 (fw_set_noise)
 #pragma unroll
@@ -571,9 +578,10 @@ template <typename T>
 // iwq (when iw): with an integration window, the sums of the last W errors (3) then entry 0 (3)
 // (shp / iwq are register arrays taken by reference with a flag: a pointer that may be null would take their
 // address and place them in scratch)
+// succ: goal_achieved_on_step (fixed_wing.py:546, 565): the first success of the env's lifetime, this step
 __device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* der, const T* tgt, int steps,
                                        const T (*seqA)[3], T (&shp)[3], bool pot, const T* rsc, int64_t ld,
-                                       const T (&iwq)[6], bool iw) {
+                                       const T (&iwq)[6], bool iw, bool succ = false) {
   T tv[3] = {T(0), T(0), T(0)}, ts[3] = {T(0), T(0), T(0)};
   for (int f = 0; f < c.n_rew; f++) {
     const fw_rew_factor F = c.rew[f];
@@ -604,6 +612,20 @@ __device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* 
       val = state_value(F.var, y, der);
     } else if (F.kind == FW_REW_STATE_INT_ERROR) {  // fixed_wing.py:1001-1012
       val = iw ? iw_value(c, pick3(iwq, F.var), steps, pick3(iwq + 3, F.var)) : T(0);
+    } else if (F.kind == FW_REW_SUCCESS) {  // fixed_wing.py:1020-1026
+      val = succ ? (F.var ? (T)(c.steps_max - steps) : (T)F.value) : T(0);
+    } else if (F.kind == FW_REW_STEP) {  // :1028-1029
+      val = (T)F.value;
+    } else if (F.kind == FW_REW_GOAL) {  // :1031-1048, _get_goal_status of the step's targets (:1346-1361)
+      const T vals[3] = {der[0], der[1], der[3]};
+      const uint32_t gb = goal_status_bits(c, tgt, vals);
+      if (F.var) {
+        val = (gb >> 3) & 1u ? (T)F.value : T(0);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 3; k++)  // value / len(self.target) per bounded target within its bound
+          val += ((gb >> k) & 1u) ? (T)F.value / T(3) : T(0);
+      }
     } else {
       const int tvv[3] = {FW_V_ROLL, FW_V_PITCH, FW_V_VA};
       val = target_error(c, F.var, tgt[F.var], state_value(tvv[F.var], y, der));
@@ -829,15 +851,79 @@ struct Draws {
   uint32_t k0, k1, cid, ep, blk;
   uint32_t r[4];
   int used;
+  uint32_t stream = 0u;
   __device__ __forceinline__ T next() {
     if (used == 4) {
-      philox(k0, k1, cid, ep, 0u, blk++, r);
+      philox(k0, k1, cid, ep, stream, blk++, r);
       used = 0;
     }
     return u01<T>(r[used++]);
   }
   __device__ __forceinline__ T uniform(T lo, T hi) { return lo + (hi - lo) * next(); }  // numpy uniform
 };
+
+// The env's own np_random (FixedWingAircraft.np_random, fixed_wing.py:324-332): the caller's tape
+// (fw_set_env_draws: aircraft i's column, from its cursor State::dcur) or a Philox source.
+template <typename T>
+struct EnvRng {
+  const State<T>& s;
+  int64_t i;
+  Draws<T>& ph;
+  uint32_t cur;
+  __device__ __forceinline__ EnvRng(const State<T>& s_, int64_t i_, Draws<T>& ph_)
+      : s(s_), i(i_), ph(ph_), cur(s_.tape ? s_.dcur[i_] : 0u) {}
+  __device__ __forceinline__ T next() {
+    if (!s.tape) return ph.next();
+    const T u = cur < (uint32_t)s.tape_len ? s.tape[(int64_t)cur * s.n + i] : T(NAN);
+    cur++;
+    return u;
+  }
+  __device__ __forceinline__ T uniform(T lo, T hi) { return lo + (hi - lo) * next(); }  // numpy uniform
+  __device__ __forceinline__ void done() const {
+    if (s.tape) s.dcur[i] = cur;
+  }
+};
+
+// sample_target (fixed_wing.py:654-746) of one aircraft: per target (roll, pitch, Va) the initial value
+// U(low, high) narrowed to the current value -+ delta, then the class's draws -- linear: the slope
+// U(slope_low, slope_high), negated when U() < 0.5, in radians where configured (:698-706); sinusoidal: the
+// amplitude (radians where configured), the period, the phase U(0, 2 pi) / (2 pi / period) and the bias that
+// puts the sinusoid through the initial value at steps_count `steps` (:708-722) -- into State::tpr.  tin:
+// explicit targets (NaN = sample); such a target is drawn all the same and then flies as "constant" for the
+// episode (reset, :436-448): slope 0, or amplitude 0 and bias = the given value.
+template <typename T>
+__device__ __forceinline__ void sample_target(const DevCfg<T>& c, const State<T>& s, int64_t i, EnvRng<T>& rng,
+                                              const T* vals, int steps, const T* tin, int64_t tin_ld, T* tgt) {
+  const T two_pi = T(2.0 * PI_D);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    T lo = c.target_low[k], hi = c.target_high[k];
+    if (c.has_delta[k]) {
+      lo = fmax(lo, vals[k] - c.target_delta[k]);
+      hi = fmax(fmin(hi, vals[k] + c.target_delta[k]), lo);
+    }
+    const T init = rng.uniform(lo, hi);
+    const T given = tin ? tin[k * tin_ld + i] : T(NAN);
+    const bool fixed = !isnan(given);
+    if (c.tprops && s.tpr) {
+      T* tp = s.tpr + (int64_t)(4 * k) * s.ld + i;
+      if (c.target_class[k] == FW_TGT_LINEAR) {
+        T slope = rng.uniform(c.tgt_slo[k], c.tgt_shi[k]);
+        if (rng.next() < T(0.5)) slope = -slope;
+        tp[0] = fixed ? T(0) : slope * c.tgt_rad[k];
+      } else if (c.target_class[k] == FW_TGT_SINUSOIDAL) {
+        const T amp = rng.uniform(c.tgt_alo[k], c.tgt_ahi[k]) * c.tgt_rad[k];
+        const T per = rng.uniform(c.tgt_plo[k], c.tgt_phi[k]);
+        const T ph = rng.uniform(T(0), two_pi) / (two_pi / per);
+        tp[0] = fixed ? T(0) : amp;
+        tp[s.ld] = per;
+        tp[2 * s.ld] = ph;
+        tp[3 * s.ld] = fixed ? given : init - amp * sin(two_pi / per * ((T)steps + ph));
+      }
+    }
+    tgt[k] = fixed ? given : init;
+  }
+}
 
 template <typename T>
 __device__ __forceinline__ void reset_lane(const DevCfg<T>& c, const State<T>& s, int64_t i, const T* init, const T* tin,
@@ -922,38 +1008,26 @@ __device__ __forceinline__ void reset_lane(const DevCfg<T>& c, const State<T>& s
     }
   }
   if (c.has_env) {
-    // sample_target (fixed_wing.py:654-746)
+    // sample_target (fixed_wing.py:654-746): Philox stream 0 after the state draws, or the env-draw tape
     const T vals[3] = {der[0], der[1], der[3]};
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      T lo = c.target_low[k], hi = c.target_high[k];
-      if (c.has_delta[k]) {
-        lo = fmax(lo, vals[k] - c.target_delta[k]);
-        hi = fmax(fmin(hi, vals[k] + c.target_delta[k]), lo);
-      }
-      const T smp = D.uniform(lo, hi);
-      const T given = tin ? tin[k * ld + i] : T(NAN);
-      tgt[k] = isnan(given) ? smp : given;
-    }
+    EnvRng<T> rng(s, i, D);
+    sample_target(c, s, i, rng, vals, 0, tin, ld, tgt);
+    if (s.tape && s.rsc)  // reward.randomize_scaling from the tape, after the targets (fixed_wing.py:473-479)
+      for (int r = 0; r < c.n_rew; r++)
+        if (c.rew[r].randomize) st_(s.rsc, r, s.ld, i, rng.uniform((T)c.rew[r].scaling, (T)c.rew[r].scaling_hi));
+    rng.done();
   }
 }
 
-// sample_target (fixed_wing.py:654-746) during an episode (target.resample_every): U(low, high) narrowed to
-// vals -+ delta, as at the reset, from Philox stream 6 keyed by (env, episode, env step)
+// sample_target (fixed_wing.py:654-746) during an episode (target.resample_every, on_success "new"): as at the
+// reset, from the env-draw tape or Philox stream 6 keyed by (env, episode, 16 x env step)
 template <typename T>
 __device__ __forceinline__ void resample_targets(const DevCfg<T>& c, const State<T>& s, int64_t i, int steps,
                                                  const T* vals, T* tgt) {
-  uint32_t r[4];
-  philox(s.key0, s.key1, s.env_offset + (uint32_t)i, s.episode[i], 6u, (uint32_t)steps, r);
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    T lo = c.target_low[k], hi = c.target_high[k];
-    if (c.has_delta[k]) {
-      lo = fmax(lo, vals[k] - c.target_delta[k]);
-      hi = fmax(fmin(hi, vals[k] + c.target_delta[k]), lo);
-    }
-    tgt[k] = lo + (hi - lo) * u01<T>(r[k]);  // numpy uniform
-  }
+  Draws<T> D{s.key0, s.key1, s.env_offset + (uint32_t)i, s.episode[i], (uint32_t)steps << 4, {0, 0, 0, 0}, 4, 6u};
+  EnvRng<T> rng(s, i, D);
+  sample_target(c, s, i, rng, vals, steps, (const T*)nullptr, 0, tgt);
+  rng.done();
 }
 
 template <typename T>
@@ -996,10 +1070,11 @@ __device__ __forceinline__ void store_env_fresh(const DevCfg<T>& c, const State<
     for (int k = 0; k < 3; k++) st_(s.target, k, ld, i, tgt[k]);
     goal_init(c, s, i, tgt, der, lep);
     st_(s.ep_ret, 0, ld, i, T(0));
+    // (State::gflag, goal_achieved, is not touched: the reference never clears it, fixed_wing.py:81)
     if (s.shp)  // self.prev_shaping[*] = None (fixed_wing.py:469-470)
 #pragma unroll
       for (int k = 0; k < 3; k++) st_(s.shp, k, ld, i, T(NAN));
-    if (s.rsc)  // reward.randomize_scaling (fixed_wing.py:473-479): Philox stream 7, one block per factor
+    if (s.rsc && !s.tape)  // reward.randomize_scaling (fixed_wing.py:473-479): Philox stream 7, one block per factor
       for (int r = 0; r < c.n_rew; r++)
         if (c.rew[r].randomize) {
           uint32_t rnd[4];
@@ -1357,6 +1432,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   if (sterm == 0) {
     const T vals[3] = {der[0], der[1], der[3]};
     uint32_t gb = 0;
+    bool success = false, succ_first = false, resample = false;
     const uint32_t b = gn;  // the new history entry
     if (goal_on) {
       // history["goal"][*].append (fixed_wing.py:536-538): the entry's nibble, and per status the window count
@@ -1376,39 +1452,58 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
       st_(s.goal, gring_row(pn), ld, i, gring_set(gw_new, pn, gb));
       st_(s.goal, GB_CNT, ld, i, gcnt);
       // np.mean(history["goal"]["all"][-streak_req:]) >= success_streak_fraction (:540-547)
-      if (steps_tgt >= c.streak_req &&
-          (double)(gcnt >> 24) / (double)c.streak_req >= (double)c.streak_frac && c.on_success == 1) {
-        done = true;
-        term = FW_TERM_SUCCESS;
+      if (steps_tgt >= c.streak_req && (double)(gcnt >> 24) / (double)c.streak_req >= (double)c.streak_frac) {
+        success = true;
+        if (c.on_success == 1) {
+          done = true;
+          term = FW_TERM_SUCCESS;
+        } else if (c.on_success == 2) {
+          resample = true;  // on_success "new" (:551-552)
+        }
       }
+    }
+    if (success && s.gflag) {  // goal_achieved_on_step = not self.goal_achieved; self.goal_achieved = True (:546-547)
+      const uint32_t f = s.gflag[i];
+      succ_first = !(f & 1u);
+      if (succ_first) s.gflag[i] = f | 1u;
     }
     if (goal_on || c.metrics || s.iws) st_(s.goal, GB_N, ld, i, b + 1u);
     if (s.shp || s.rsc || s.iws) {
       reward = reward_of(c, y, der, tgt, steps, seqA, shp, s.shp != nullptr, s.rsc ? s.rsc + i : nullptr, ld,
-                         iwq, s.iws != nullptr);
+                         iwq, s.iws != nullptr, succ_first);
       if (s.shp)
 #pragma unroll
         for (int k = 0; k < 3; k++) st_(s.shp, k, ld, i, shp[k]);
     } else {
-      reward = reward_of(c, y, der, tgt, steps, seqA, shp, false, (const T*)nullptr, 0, iwq, false);
+      reward = reward_of(c, y, der, tgt, steps, seqA, shp, false, (const T*)nullptr, 0, iwq, false, succ_first);
     }
-    if (c.resample_every > 0 && steps_tgt >= c.resample_every) {
-      // target.resample_every (fixed_wing.py:570-574): sample_target (:654-746) from the state after the step,
-      // then _get_next_target with the target step count restarted; Philox stream 6, block = the env step
+    if (resample || (c.resample_every > 0 && steps_tgt >= c.resample_every)) {
+      // on_success "new" or target.resample_every (fixed_wing.py:566-574): sample_target (:654-746) from the
+      // state after the step, then _get_next_target with the target step count restarted
       resample_targets(c, s, i, steps, vals, tgt);
       steps_tgt = 0;
     }
-    next_target(c, steps_tgt, tgt);
+    next_target(c, steps_tgt, steps, [&](int r) { return s.tpr[(int64_t)r * ld + i]; }, tgt);
     if (s.iws) {  // history["error"][k].append(self._get_error(k)) (fixed_wing.py:575-579): the window sums move on
       const int ns = (int)((lep + b) % (uint32_t)c.iwin);
       if (b != b_guess)
 #pragma unroll
         for (int k = 0; k < 3; k++) iold[k] = ld_(s.iwr, ns * 3 + k, ld, i);
+      // every W entries, once the ring holds exactly the window (slot W - 1 just written, b + 1 >= W), the sum is
+      // formed afresh from the ring, oldest entry first as np.sum over the slice (fixed_wing.py:1004-1012): the
+      // running total's rounding cannot build up over a long episode (round-5 advice).  ns = (life + 1) % W is
+      // the same on every lane, so the branch is wave-uniform
+      const bool resum = ns == c.iwin - 1 && b + 1u >= (uint32_t)c.iwin;
 #pragma unroll
       for (int k = 0; k < 3; k++) {
         const T err = target_error(c, k, tgt[k], vals[k]);
         iqp[k] = iwq[k];
         iwq[k] = b >= (uint32_t)c.iwin ? (iwq[k] + err) - iold[k] : iwq[k] + err;
+        if (resum) {
+          T q = T(0);
+          for (int j = 0; j + 1 < c.iwin; j++) q += ld_(s.iwr, j * 3 + k, ld, i);
+          iwq[k] = q + err;
+        }
         st_(s.iwr, ns * 3 + k, ld, i, err);
         st_(s.iws, IW_Q + k, ld, i, iwq[k]);
         st_(s.iws, IW_QP + k, ld, i, iqp[k]);
@@ -1471,7 +1566,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
     if (do_reset) {
       T yr[NY], dr[8], wr[3], tr[3];
       // the worker's env.reset() passes no turbulence_noise: Dryden.reset(None) (dryden.py:184-188)
-      if (s.noise_env_len) s.noise_env_len[i] = 0;
+      if (s.noise_env_len && s.noise_env_len[i] > 0) s.noise_env_len[i] = 0;  // (the shared sequence stays)
       reset_lane(c, s, i, (const T*)nullptr, (const T*)nullptr, yr, dr, wr, tr);
       store_env_fresh(c, s, i, yr, dr, wr, tr, life0 + 1u);
 #ifndef FW_MET_SKIP_INIT
@@ -1634,6 +1729,9 @@ __device__ __forceinline__ void collect_merge(const double* rec0, double* lvl, u
     if (l == 0) t = __hip_atomic_fetch_add(cnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     t = __shfl(t, 0);
     if (t != (uint32_t)(gs - 1)) return;  // not the last arrival: the node's last block merges it
+    // acquire side of the ticket: no load of merge_node's (get64, which bypasses the CU's L1) may be issued
+    // before the ticket's result is known (round-5 advice: only the loop-head clobber ordered them)
+    asm volatile("" ::: "memory");
     if (l == 0) __hip_atomic_store(cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
     double N, mean, m2;
     double warm = 0.0;  // the statistics' lines, fetched under the merge (update_from_moments re-reads them)
@@ -1905,12 +2003,19 @@ struct fw_handle {
   size_t o_shp = 0;         // potential-form shaping rows (env->reward_potential at create; 0 = none)
   size_t o_rsc = 0;         // per-episode reward scalings (a randomised factor at create; 0 = none)
   size_t o_iwr = 0, o_iws = 0;  // integration-window ring and sums (env->integration_window > 0 at create)
+  size_t o_tpr = 0;         // linear / sinusoidal target properties (such a target class at create; 0 = none)
+  size_t o_gflag = 0;       // goal_achieved flags (a success reward factor at create; 0 = none)
+  size_t o_dcur = 0;        // env-draw tape cursors (env handles)
+  const void* tape = nullptr;  // fw_set_env_draws
+  int32_t tape_len = 0;
   int iwin = 0;
   int rand_active = 0;      // the current config randomises parameters (kernels read the rows)
   int lanes_opt = FW_LANES_AUTO;  // fw_set_lanes: 0 = automatic, 1, 4
   int quad_ok = 1;          // the config allows the quad integrator (no wrapped ODE-state variable)
   fw_collect_epilogue col{};  // fw_set_collect_epilogue (all null: off)
   size_t o_colws = 0, o_colcnt = 0;  // in-launch merge tree workspace (records above level 0, counters)
+  size_t colcnt_bytes = 0;           // bytes of the tree's arrival counters (zeroed again by clear_tree)
+  bool tree_dirty = false;           // an env step with the tree failed: counters may hold stale arrivals
 };
 
 namespace {
@@ -2082,6 +2187,19 @@ void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
       d.term_weight[k] = (T)e.term_weight[k];
       d.term_present[k] = e.term_present[k];
     }
+    d.tprops = 0;
+    for (int k = 0; k < 3; k++) {
+      d.tprops |= (e.target_class[k] == FW_TGT_LINEAR || e.target_class[k] == FW_TGT_SINUSOIDAL) ? 1 : 0;
+      d.tgt_rad[k] = e.target_radians[k] ? (T)(3.141592653589793 / 180.0) : T(1);  // np.radians: x * (pi / 180)
+      d.tgt_slo[k] = (T)e.target_slope_low[k];
+      d.tgt_shi[k] = (T)e.target_slope_high[k];
+      d.tgt_alo[k] = (T)e.target_amp_low[k];
+      d.tgt_ahi[k] = (T)e.target_amp_high[k];
+      d.tgt_plo[k] = (T)e.target_period_low[k];
+      d.tgt_phi[k] = (T)e.target_period_high[k];
+    }
+    d.tprops = d.tprops && h->o_tpr;
+    d.goal_flag = h->o_gflag != 0;
     d.streak_frac = (T)e.streak_frac;
     d.step_fail_value = (T)e.step_fail_value;
     d.metrics = h->metrics && e.metrics;
@@ -2139,9 +2257,18 @@ int validate(const fw_sim_config* s, const fw_env_config* e) {
     for (int o = 0; o < e->n_obs; o++)
       if (e->obs[o].kind == FW_OBS_ACTION_WINDOW && (e->obs[o].window < 1 || e->obs[o].window > FW_MAX_WINDOW))
         return set_err(FW_E_UNSUPPORTED, "action window out of range");
-    for (int r = 0; r < e->n_rew; r++)
+    for (int r = 0; r < e->n_rew; r++) {
       if (e->rew[r].kind == FW_REW_ACTION_DELTA && (e->rew[r].window < 1 || e->rew[r].window > FW_MAX_WINDOW))
         return set_err(FW_E_UNSUPPORTED, "reward window out of range");
+      if (e->rew[r].kind < FW_REW_STATE_ERROR || e->rew[r].kind > FW_REW_GOAL)
+        return set_err(FW_E_INVALID, "unknown reward factor kind");
+    }
+    for (int k = 0; k < 3; k++)
+      if (e->target_class[k] < FW_TGT_CONSTANT || e->target_class[k] > FW_TGT_SINUSOIDAL)
+        return set_err(FW_E_INVALID, "unknown target class");
+    if (e->target_class[2] == FW_TGT_COMPENSATE && e->target_class[1] == FW_TGT_COMPENSATE)
+      return set_err(FW_E_UNSUPPORTED, "compensate Va with a compensate pitch target (fixed_wing.py:1386-1392)");
+    if (e->on_success < 0 || e->on_success > 2) return set_err(FW_E_INVALID, "on_success must be 0 (none), 1 (done) or 2 (new)");
   }
   return FW_OK;
 }
@@ -2299,6 +2426,11 @@ State<T> state_of(const fw_handle* h) {
   s.rsc = h->o_rsc ? (T*)(b + h->o_rsc) : nullptr;
   s.iwr = h->o_iwr ? (T*)(b + h->o_iwr) : nullptr;
   s.iws = h->o_iws ? (T*)(b + h->o_iws) : nullptr;
+  s.tpr = h->o_tpr ? (T*)(b + h->o_tpr) : nullptr;
+  s.gflag = h->o_gflag ? (uint32_t*)(b + h->o_gflag) : nullptr;
+  s.dcur = h->o_dcur ? (uint32_t*)(b + h->o_dcur) : nullptr;
+  s.tape = (h->tape && h->o_dcur) ? (const T*)h->tape : nullptr;
+  s.tape_len = h->tape_len;
   s.col_ret = h->col.ret;
   s.col_gamma = h->col.gamma;
   s.col_rec = h->col.records;
@@ -2315,6 +2447,14 @@ unsigned grid_of(const fw_handle* h) { return (unsigned)((h->n + BLOCK - 1) / BL
 int check_launch() {
   FW_HIP(hipGetLastError());
   return FW_OK;
+}
+
+// The merge tree's arrival counters are reset by each node's last arriver; a launch that did not run to
+// its end leaves counts behind that would make every later tree merge at the wrong arrival.  A failed env
+// step with the tree on zeroes them on its stream and marks the handle, and the next
+// fw_set_collect_epilogue that turns the tree on zeroes them again after a device synchronisation.
+void clear_tree(fw_handle* h, hipStream_t st) {
+  if (h->o_colws && h->colcnt_bytes) (void)hipMemsetAsync((char*)h->base + h->o_colcnt, 0, h->colcnt_bytes, st);
 }
 
 }  // namespace
@@ -2456,6 +2596,14 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
   if (env && env->n_rand > 0) {  // per-aircraft parameters (simulator parameter randomisation)
     h->o_prm = off; off += (size_t)FW_NPARAM * row;
   }
+  if (env) {  // linear / sinusoidal targets: their drawn properties; success rewards: goal_achieved; tape cursors
+    bool tp = false, sf = false;
+    for (int k = 0; k < 3; k++) tp = tp || env->target_class[k] == FW_TGT_LINEAR || env->target_class[k] == FW_TGT_SINUSOIDAL;
+    for (int r = 0; r < env->n_rew; r++) sf = sf || env->rew[r].kind == FW_REW_SUCCESS;
+    if (tp) { h->o_tpr = off; off += (size_t)12 * row; }
+    if (sf) { h->o_gflag = off; off += align_up((size_t)h->ld * 4, 256); }
+    h->o_dcur = off; off += align_up((size_t)h->ld * 4, 256);
+  }
   if (env && env->obs_length > 1) {  // observation history: first row of the episode + ring of past rows
     const int step = env->obs_step > 1 ? env->obs_step : 1;
     h->obs_hist = (env->obs_length - 1) * step + 2;
@@ -2467,6 +2615,7 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
     fw_stats::merge_tree_size((h->n * 4 + BLOCK - 1) / BLOCK, &mr, &mc);
     h->o_colws = off; off += align_up((size_t)mr * (1 + 2 * COL_MAXD) * sizeof(double), 256);
     h->o_colcnt = off; off += align_up((size_t)mc * sizeof(uint32_t), 256);  // zeroed below, reset by the tree
+    h->colcnt_bytes = (size_t)mc * sizeof(uint32_t);
   }
   // rows are ld elements apart: the padding above is folded into ld for simplicity
   h->base_bytes = off;
@@ -2534,6 +2683,18 @@ int fw_set_noise(fw_handle* h, const void* noise_dev, int64_t len) {
   return FW_OK;
 }
 
+int fw_set_env_draws(fw_handle* h, const void* tape_dev, int32_t len) {
+  if (!h) return set_err(FW_E_INVALID, "NULL handle");
+  if (!h->has_env || !h->o_dcur) return set_err(FW_E_INVALID, "fw_set_env_draws: handle has no env");
+  if (tape_dev && len < 1) return set_err(FW_E_INVALID, "fw_set_env_draws: len must be >= 1");
+  FW_HIP(hipSetDevice(h->device));
+  FW_HIP(hipDeviceSynchronize());  // (launches in flight keep the tape they were given)
+  FW_HIP(hipMemset((char*)h->base + h->o_dcur, 0, (size_t)h->ld * 4));
+  h->tape = tape_dev;
+  h->tape_len = tape_dev ? len : 0;
+  return FW_OK;
+}
+
 int fw_set_noise_lengths(fw_handle* h, int32_t* env_len_dev) {
   if (!h) return set_err(FW_E_INVALID, "NULL handle");
   if (env_len_dev && !h->noise) return set_err(FW_E_INVALID, "fw_set_noise_lengths: set the noise buffer first");
@@ -2569,10 +2730,24 @@ int fw_update_config(fw_handle* h, const fw_sim_config* sim, const fw_env_config
     for (int r = 0; r < env->n_rew; r++)
       if (env->rew[r].randomize && !h->o_rsc)
         return set_err(FW_E_UNSUPPORTED, "reward.randomize_scaling must be set when the handle is created");
+    // the per-episode scaling rows are drawn at reset for the factors randomised then: a factor randomised
+    // only from now on would divide by its still-zero row until the aircraft's next reset
+    if (h->o_rsc) {
+      bool same = env->n_rew == h->env.n_rew;
+      for (int r = 0; same && r < env->n_rew; r++) same = (env->rew[r].randomize != 0) == (h->env.rew[r].randomize != 0);
+      if (!same)
+        return set_err(FW_E_UNSUPPORTED, "reward.randomize_scaling: the randomised factors cannot change after create");
+    }
     if (env->integration_window != h->iwin)
       return set_err(FW_E_UNSUPPORTED, "integration_window must be the one the handle was created with");
     if (env->reward_potential && !h->o_shp)
       return set_err(FW_E_UNSUPPORTED, "reward.form \"potential\" must be set when the handle is created");
+    for (int k = 0; k < 3; k++)
+      if ((env->target_class[k] == FW_TGT_LINEAR || env->target_class[k] == FW_TGT_SINUSOIDAL) && !h->o_tpr)
+        return set_err(FW_E_UNSUPPORTED, "linear / sinusoidal target classes must be configured when the handle is created");
+    for (int r = 0; r < env->n_rew; r++)
+      if (env->rew[r].kind == FW_REW_SUCCESS && !h->o_gflag)
+        return set_err(FW_E_UNSUPPORTED, "a success reward factor must be configured when the handle is created");
     h->env = *env;
   }
   if (sim->turbulence && sim->dryden_state && !h->o_dry)
@@ -2629,11 +2804,16 @@ int fw_env_step(fw_handle* h, const void* actions_dev, void* obs_dev, void* rewa
   if (!h->has_env) return set_err(FW_E_INVALID, "handle has no env config");
   FW_HIP(hipSetDevice(h->device));
   hipStream_t st = (hipStream_t)stream;
-  if (h->precision == FW_F64)
-    return fwl::env_step<double>(h, st, actions_dev, obs_dev, reward_dev, done_dev, term_dev, terminal_obs_dev,
-                                 episode_dev, stats_dev, auto_reset);
-  return fwl::env_step<float>(h, st, actions_dev, obs_dev, reward_dev, done_dev, term_dev, terminal_obs_dev,
-                              episode_dev, stats_dev, auto_reset);
+  const int r = h->precision == FW_F64
+                    ? fwl::env_step<double>(h, st, actions_dev, obs_dev, reward_dev, done_dev, term_dev, terminal_obs_dev,
+                                            episode_dev, stats_dev, auto_reset)
+                    : fwl::env_step<float>(h, st, actions_dev, obs_dev, reward_dev, done_dev, term_dev, terminal_obs_dev,
+                                           episode_dev, stats_dev, auto_reset);
+  if (r != FW_OK && h->col.merged) {
+    clear_tree(h, st);
+    h->tree_dirty = true;
+  }
+  return r;
 }
 
 int fw_env_rollout(fw_handle* h, int32_t n_steps, const void* actions_dev, void* obs_dev, void* reward_dev,
@@ -2689,6 +2869,12 @@ int fw_set_collect_epilogue(fw_handle* h, const fw_collect_epilogue* epi) {
     return set_err(FW_E_INVALID, "fw_set_collect_epilogue: merged needs the records buffer (the tree's level 0)");
   if (epi->rms && !epi->merged) return set_err(FW_E_INVALID, "fw_set_collect_epilogue: rms needs merged");
   h->col = *epi;
+  if (epi->merged && h->tree_dirty) {  // no arrival left over from a failed launch
+    FW_HIP(hipSetDevice(h->device));
+    FW_HIP(hipDeviceSynchronize());
+    FW_HIP(hipMemset((char*)h->base + h->o_colcnt, 0, h->colcnt_bytes));
+    h->tree_dirty = false;
+  }
   return FW_OK;
 }
 
@@ -2796,6 +2982,9 @@ static int block_info(const fw_handle* h, int32_t block, size_t* off, int* rows,
     case FW_BLK_GOAL:
       if (!h->has_env) return set_err(FW_E_INVALID, "handle has no env (no goal history)");
       *off = h->o_goal; *rows = 4; *esz = 4; return FW_OK;
+    case FW_BLK_TARGET_PROPS:
+      if (!h->o_tpr) return set_err(FW_E_INVALID, "handle has no linear / sinusoidal targets");
+      *off = h->o_tpr; *rows = 12; *esz = T_; return FW_OK;
     default: return set_err(FW_E_INVALID, "unknown state block");
   }
 }

@@ -146,25 +146,47 @@ class Engine:
         self._noise = buf
         self._push_noise()
 
+    def set_env_draws(self, tape):
+        """fw_set_env_draws: the env's own np_random draws (sample_target at every reset / resample, the
+        randomised reward scalings, fixed_wing.py:436-479, 566-575, 654-746) taken in order from ``tape``
+        [len][n] (numpy's ``random_sample()`` values: each draw is used as ``low + (high - low) * u``) instead
+        of the Philox streams, so a device episode replays the reference's.  None: Philox again.  Restarts
+        every env's cursor at draw 0; draws past the end are NaN."""
+        if tape is None:
+            self._tape = None
+            _native.check(self.lib.fw_set_env_draws(self.h, None, 0), "fw_set_env_draws")
+            return
+        a = torch.as_tensor(np.asarray(tape), dtype=self.dtype)
+        if a.dim() != 2 or a.shape[1] != self.n or a.shape[0] < 1:
+            raise ValueError("tape must be [len][n] with len >= 1")
+        self._tape = a.to(self.device).contiguous()
+        torch.cuda.current_stream(self.device).synchronize()
+        _native.check(self.lib.fw_set_env_draws(self.h, _ptr(self._tape), int(a.shape[0])), "fw_set_env_draws")
+        self.config_version += 1  # a captured step bakes in the tape's address
+
     def set_env_noise(self, indices, noise):
         """Per-env injection (PyFly.reset(turbulence_noise=...) of the envs in ``indices``, pyfly.py:1262):
         ``noise`` [4][len] N(0,1) samples for all of them, or None = those envs draw from Philox again.
         The other envs keep what they had (a set_noise injection included); an env's injection ends at its
         next VecEnv auto-reset (fw_set_noise_lengths) or at a reset of it without noise (FixedWingVecEnv).
-        Applies to the envs' next reset (call before ``reset(mask=...)``)."""
+        Applies to the envs' next reset (call before ``reset(mask=...)``).  A set_noise sequence is an engine-wide
+        override: the envs that never got their own injection keep reading it across resets, whatever the call
+        history (round-5 advice); an env whose own injection ends draws from Philox."""
         idx = torch.as_tensor(np.asarray(list(indices), dtype=np.int64))
         if getattr(self, "_env_len", None) is None:
             if noise is None:
                 return
             ld = (self.n + 63) // 64 * 64
             if self._noise is not None:  # a set_noise buffer: every env keeps reading it until its own injection
-                self._env_len = torch.full((self.n,), int(self._noise.shape[1]), dtype=torch.int32, device=self.device)
+                # (a negative length marks the shared sequence: it survives resets, as it does without per-env lengths)
+                self._env_len = torch.full((self.n,), -int(self._noise.shape[1]), dtype=torch.int32, device=self.device)
                 self._noise = self._noise.clone()
             else:
                 self._env_len = torch.zeros(self.n, dtype=torch.int32, device=self.device)
                 self._noise = torch.zeros(4, 1, ld, dtype=self.dtype, device=self.device)
-        if noise is None:
-            self._env_len[idx.to(self.device)] = 0
+        if noise is None:  # ends the per-env injections of these envs (a shared set_noise sequence stays)
+            cols = idx.to(self.device)
+            self._env_len[cols] = torch.where(self._env_len[cols] > 0, 0, self._env_len[cols])
         else:
             a = torch.as_tensor(np.asarray(noise), dtype=self.dtype)
             if a.dim() != 2 or a.shape[0] != 4 or a.shape[1] < 1:

@@ -362,6 +362,11 @@ class FixedWingVecEnv(VecEnv):
             s, _ = self.engine.steps()
             s = s.cpu().numpy()
             return [int(s[i]) for i in idx]
+        host = self._host_attrs()
+        if attr_name == "use_curriculum" and all(attr_name in host[i] for i in idx):
+            # a plain attribute in the reference (fixed_wing.py:299, 412: set True by __init__ and
+            # set_curriculum_level, never read): a set_attr value stands until the next set_curriculum_level
+            return [host[i][attr_name] for i in idx]
         if attr_name in ("scale_actions", "goal_enabled", "integration_window", "curriculum_level", "use_curriculum",
                          "obs_norm"):
             val = {"scale_actions": self.spec.scale_actions,
@@ -370,7 +375,6 @@ class FixedWingVecEnv(VecEnv):
                    "curriculum_level": getattr(self.spec, "curriculum_level", 1),
                    "use_curriculum": True, "obs_norm": self.spec.cfg["observation"].get("normalize", False)}[attr_name]
             return [val for _ in idx]
-        host = self._host_attrs()
         if all(attr_name in host[i] for i in idx):  # set earlier by set_attr
             return [host[i][attr_name] for i in idx]
         raise AttributeError("FixedWingVecEnv has no per-env attribute %r" % attr_name)
@@ -449,6 +453,8 @@ class FixedWingVecEnv(VecEnv):
         """FixedWingAircraft.set_curriculum_level (fixed_wing.py:334-412) for all envs."""
         self.spec.set_curriculum_level(level)
         self.engine.update_config(self.spec.sim, self.spec)
+        for h in self._host_attrs():  # fixed_wing.py:412: use_curriculum = True again
+            h.pop("use_curriculum", None)
 
     def _reset_some(self, idx, state=None, target=None, turbulence_noise=None):
         """FixedWingAircraft.reset(state=..., target=...) for the envs in ``idx``."""
