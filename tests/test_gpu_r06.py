@@ -60,7 +60,7 @@ def test_env_draw_tape_replays_reference_episodes(name, precision, tmpdir):
     for ep in range(eps):
         rew, obs, tgt = g(ep, "rew"), g(ep, "obs"), g(ep, "target")
         np.testing.assert_allclose(out["obs"][0][ep], obs[0], rtol=1e-9 if f64 else 1e-5, atol=1e-9 if f64 else 1e-5)
-        np.testing.assert_allclose(out["tgt"][0][:, ep], tgt[0], rtol=0, atol=1e-12 if f64 else 1e-6)
+        np.testing.assert_allclose(out["tgt"][0][:, ep], tgt[0], rtol=0 if f64 else 1e-6, atol=1e-12 if f64 else 1e-6)
         steps = len(rew)
         if not f64 and name == "success":
             # the goal-streak steps (resamples) and the first-success reward on the same steps as the reference
