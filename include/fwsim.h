@@ -228,7 +228,7 @@ typedef struct fw_env_config {
   double target_low[3], target_high[3];
   double target_delta[3];             /* NaN = none */
   double target_bound[3];             /* NaN = none */
-  int32_t streak_req;                 /* <= 128; 0 disables goal */
+  int32_t streak_req;                 /* <= 4096 (ABI 11; 128 before); 0 disables goal */
   int32_t on_success;                 /* 0 none, 1 done, 2 new (ABI 11: sample_target on success, :551-552) */
   double streak_frac;
   int32_t n_rew;

@@ -25,6 +25,9 @@ and episodes reset with an explicit state and SAMPLED targets:
              and goal (per_state, all) (:1020-1048), a PID controller that reaches its goal streak: the
              success reward fires on the first success of the env's lifetime only (goal_achieved, :81, 546-547)
 
+env_streak.npz: success_streak_req 200 and 300 (fixed_wing.py:540-547 has no limit; rounds 1-5 stopped at 128),
+on_success "done", PID episodes from explicit states and targets (no np_random draws involved)
+
 Usage:  python tests/golden/gen_golden_r06.py
 """
 import copy
@@ -171,5 +174,30 @@ def gen_env_r06():
     np.savez_compressed(os.path.join(OUT, "env_r06.npz"), **out)
 
 
+STREAK_CASES = {
+    # name -> success_streak_req: the goal history beyond rounds 1-5's 128 entries (byte counts up to 255, 16-bit
+    # counts above), on_success "done", PID episodes with explicit targets (gen_golden.env_episode)
+    "streak200": 200,
+    "streak300": 300,
+}
+
+
+def gen_env_streak():
+    out = {}
+    rng = np.random.RandomState(607)
+    for name, req in STREAK_CASES.items():
+        ckw = {"action": {"scale_space": False},
+               "target": {"on_success": "done", "success_streak_fraction": 0.95, "success_streak_req": req}}
+        env = G.make_env(False, 1500, ckw)
+        for ep in range(3):
+            res = G.env_episode(env, rng, False, 1500, omega_deg=20.0, policy="pid")
+            for k, v in res.items():
+                out["%s__ep%d__%s" % (name, ep, k)] = v
+            print("streak %s ep%d: %d steps, last term=%r" % (name, ep, len(res["rew"]), res["term"][-1]))
+        out[name + "__req"] = np.array(req)
+    np.savez_compressed(os.path.join(OUT, "env_streak.npz"), **out)
+
+
 if __name__ == "__main__":
     gen_env_r06()
+    gen_env_streak()

@@ -30,7 +30,7 @@ def _engine(sim_spec, env_spec=None, n=1, precision="float64", lanes=None):
 
 
 # both integrators: one lane per aircraft and the lane quad (fw_quad.hpp)
-LANES = pytest.mark.parametrize("lanes", [1, 4])
+LANES = pytest.mark.parametrize("lanes", [1, 2, 4])  # one lane, the pair (round 6), the quad
 
 
 def _rel(a, b):
@@ -230,7 +230,7 @@ def _batch_vs_oracle(n, steps, seed):
             break
 
 
-@pytest.mark.parametrize("n,lanes", [(65536, 1), (65536, 4), (262144 + 37, 1)])
+@pytest.mark.parametrize("n,lanes", [(65536, 1), (65536, 2), (65536, 4), (262144 + 37, 1)])
 def test_full_size_properties_fp32(n, lanes):
     """65536 envs (configs[2]) and a ragged batch above the largest config (262144 + 37), 300 steps of
     U(-1,1) actions with auto-reset: finite, bounded, deterministic, shard-invariant -- bit for bit for a

@@ -109,3 +109,43 @@ def test_env_draw_tape_exhausted_is_nan(tmpdir):
     eng.reset()
     assert np.isfinite(eng.get_block(C.FW_BLK_TARGET).cpu().numpy()).all()
     eng.close()
+
+
+@pytest.mark.parametrize("precision", ["float64", "float32"])
+@pytest.mark.parametrize("name", ["streak200", "streak300"])
+def test_success_streak_beyond_128(name, precision):
+    """success_streak_req 200 / 300 (the goal ring beyond 128 entries; 16-bit window counts above 255) against
+    the reference's PID episodes that end on their goal streak (env_streak.npz): fp64 the same done step and
+    termination, rewards within 1e-6 + 1e-6 / step; fp32 the done step within 2 steps."""
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
+    d = F.load("env_streak.npz")
+    req = int(d[name + "__req"])
+    spec = C.EnvSpec(config_kw={"steps_max": 1500, "action": {"scale_space": False},
+                                "target": {"on_success": "done", "success_streak_fraction": 0.95,
+                                           "success_streak_req": req}},
+                     sim_config_kw={"turbulence": False})
+    assert spec.struct().streak_req == req
+    g = lambda ep, k: d["%s__ep%d__%s" % (name, ep, k)]  # noqa: E731
+    eps = 3
+    eng = Engine(spec.sim, spec, eps, device=DEV, precision=precision)
+    eng.reset(init=np.stack([F.env_init(g(ep, "init")) for ep in range(eps)], axis=1),
+              target=np.stack([g(ep, "target0") for ep in range(eps)], axis=1))
+    n = max(len(g(ep, "rew")) for ep in range(eps))
+    done_at = np.full(eps, -1)
+    for s in range(n):
+        acts = np.stack([g(ep, "act")[min(s, len(g(ep, "act")) - 1)] for ep in range(eps)])
+        o, r, dn, t = eng.env_step(torch.tensor(acts, dtype=eng.dtype, device=DEV), auto_reset=False)
+        r, dn, t = r.double().cpu().numpy(), dn.cpu().numpy().astype(bool), t.cpu().numpy()
+        for ep in range(eps):
+            if done_at[ep] >= 0 or s >= len(g(ep, "rew")):
+                continue
+            if precision == "float64":
+                assert abs(r[ep] - g(ep, "rew")[s]) <= 1e-6 + 1e-6 * s, (ep, s)
+                assert bool(dn[ep]) == bool(g(ep, "done")[s]), (ep, s)
+            if dn[ep]:
+                done_at[ep] = s
+                ref_term = str(g(ep, "term")[-1])
+                assert t[ep] == (C.FW_TERM_SUCCESS if ref_term == "success" else C.FW_TERM_STEPS), (ep, t[ep], ref_term)
+    for ep in range(eps):
+        assert abs(done_at[ep] - (len(g(ep, "rew")) - 1)) <= (0 if precision == "float64" else 2), (ep, done_at)
+    eng.close()

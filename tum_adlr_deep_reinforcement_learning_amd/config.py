@@ -835,8 +835,8 @@ class EnvSpec:
         if self.obs_noise is not None:
             e.obs_noise, (e.obs_noise_mean, e.obs_noise_std) = 1, self.obs_noise
         e.streak_req = int(t["success_streak_req"])
-        if e.streak_req > 128:
-            raise NotImplementedError("success_streak_req > 128")
+        if e.streak_req > 4096:  # (the goal-history ring grows with it: 4096 entries = 2 KB per aircraft)
+            raise NotImplementedError("success_streak_req > 4096")
         e.streak_frac = float(t["success_streak_fraction"])
         e.on_success = FW_ON_SUCCESS[t.get("on_success", "none")]  # fixed_wing.py:548-559
         r = cfg["reward"]

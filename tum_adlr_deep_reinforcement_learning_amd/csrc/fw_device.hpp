@@ -140,6 +140,11 @@ struct DevCfg {
   int tprops;                          // some target is linear or sinusoidal: State::tpr rows are kept
   T tgt_rad[3], tgt_slo[3], tgt_shi[3], tgt_alo[3], tgt_ahi[3], tgt_plo[3], tgt_phi[3];
   int goal_flag;                       // a success reward factor: State::gflag keeps goal_achieved
+  // goal-status history ring (fw_kernels.hip GB_*): 8 x gring_words entries (a power of two >= 128 and >=
+  // success_streak_req), words 16.. after the count rows; window counts as bytes, or (gcnt_wide: streak_req > 255)
+  // as 16-bit fields in two words (the second at row gcnt2_row)
+  uint32_t gring_mask;
+  int gcnt_wide, gcnt2_row;
   T streak_frac;
   T step_fail_value;
   T term_weight[3];
@@ -731,6 +736,7 @@ FW_HD double min_step_at(double t) {
 }
 
 #include "fw_quad.hpp"
+#include "fw_pair.hpp"
 
 #ifndef FW_TAIL_QUAD
 #define FW_TAIL_QUAD 16  // one-lane waves hand their last <= this many integrating aircraft to lane quads (0 = off)
@@ -1331,7 +1337,7 @@ struct KeepY {  // default: y stays live in registers across the integration
 // state from memory (the kernels do: keeping 19 values live across the RK loop
 // costs registers the loop needs).
 // Q = 4: the integration runs on the lane quad of the aircraft (fw_quad.hpp; qr = lane in the quad,
-// every lane of the quad returns the same result).
+// every lane of the quad returns the same result); Q = 2: on its lane pair (fw_pair.hpp, round 6).
 // HO: the one-lane integration's tail handoff (rk45; ho = the block's qd::HoSlot array in LDS).
 template <int Q = 1, bool HO = false, typename T, typename C, typename A, typename R = KeepY>
 FW_HD int sim_step_masked(const C& c, const A& a, T* y, T* der, T* cmd, const T* wind, const T* tl, const T* ta, int& nfev,
@@ -1355,6 +1361,7 @@ FW_HD int sim_step_masked(const C& c, const A& a, T* y, T* der, T* cmd, const T*
 #pragma unroll
   for (int i = 0; i < NY; i++) y1[i] = y[i];
   if constexpr (Q == 4) term = qd::rk45_quad(c, a, X, y1, nfev, nacc, qr);
+  else if constexpr (Q == 2) term = pr::rk45_pair(c, a, X, y1, nfev, nacc, qr, sy, stride);
   else term = rk45<T, C, A, HO>(c, a, X, y1, sy, sf, stride, nfev, nacc, FW_ER_LDS ? sf + NP * stride : nullptr, ho);
   reload(y);
   if (term < 0) {  // solver failure: y1 = the last accepted sub-step (rk45 wrote Y back), saved as usual

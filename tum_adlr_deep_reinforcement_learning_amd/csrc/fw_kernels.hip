@@ -69,7 +69,10 @@ constexpr int BLOCK = FW_BLOCK;
 #ifndef FW_QUAD_MIN_WAVES
 #define FW_QUAD_MIN_WAVES 1  // ... of their quad (Q = 4) instances
 #endif
-#define FW_WAVES(Q) ((Q) == 4 ? FW_QUAD_MIN_WAVES : FW_MIN_WAVES)
+#ifndef FW_PAIR_MIN_WAVES
+#define FW_PAIR_MIN_WAVES 2  // ... of their pair (Q = 2) instances: two waves per SIMD (256 registers), the point of the pair
+#endif
+#define FW_WAVES(Q) ((Q) == 4 ? FW_QUAD_MIN_WAVES : (Q) == 2 ? FW_PAIR_MIN_WAVES : FW_MIN_WAVES)
 #ifndef FW_HALF_WAVE
 // A/B only (tools/r05_halfwave.sh; with FW_MIN_WAVES=2): one-lane k_env_step waves step 32 aircraft (lanes 0..31),
 // twice the waves, so a second wave can share each SIMD.  No collect epilogue, no tail handoff to the idle lanes.
@@ -167,13 +170,38 @@ constexpr uint32_t M_NONE = 0xFFFFu;
 // reset state, one entry per successful step, fixed_wing.py:462-466, 536-538) keeps its four statuses
 // (goal_status_bits: roll / pitch / Va within bound, all) in nibble (lep + e) % 8 of ring word ((lep + e) % 128) / 8
 // -- indexed by the LIFETIME position, so every lane of a wave touches the same word row.  GB_CNT holds the ones
-// among the last success_streak_req entries per status (one byte each, "all" in byte 3), GB_N the entry count.
+// among the last success_streak_req entries per status (one byte each, "all" in byte 3; 16 bits each in two words
+// when success_streak_req > 255, round 6: GCnt), GB_N the entry count.  Round 6: the ring holds a power of two
+// >= success_streak_req entries (at least 128); words beyond 16 follow the count rows (gring_row).
 // A step reads the word the new entry goes to, the word holding the entry that leaves the window, the counts and
 // the entry count (16 B) and writes three of them back: the 128-bit shift register of rounds 1-4 plus the
 // metrics' per-target bit buffers moved 76 B per step.
 constexpr int GB_RING = 0, GB_CNT = 16, GB_N = 17, GB_ROWS = 18;
 constexpr uint32_t LIFE0 = 1u << 20;  // State::life at handle creation
-__device__ __forceinline__ int gring_row(uint32_t pos) { return GB_RING + (int)((pos & 127u) >> 3); }
+// ring word w of the history (mask = entries - 1): words 0..15 in rows 0..15, words 16.. (success_streak_req > 128,
+// round 6) after the count rows
+__host__ __device__ __forceinline__ int gring_row(uint32_t pos, uint32_t mask) {
+  const int w = (int)((pos & mask) >> 3);
+  return GB_RING + (w < 16 ? w : w + 2);
+}
+// the window counts per status (roll, pitch, Va, all): four bytes in GB_CNT, or -- streak_req > 255 -- 16-bit
+// fields in GB_CNT (roll, pitch) and the row gcnt2_row (Va, all)
+struct GCnt {
+  uint32_t w0, w1;
+  bool wide;
+  __device__ __forceinline__ uint32_t get(int k) const {
+    return wide ? ((k < 2 ? w0 : w1) >> (16 * (k & 1))) & 0xFFFFu : (w0 >> (8 * k)) & 0xFFu;
+  }
+  __device__ __forceinline__ void set(int k, uint32_t v) {
+    if (wide) {
+      const int sh = 16 * (k & 1);
+      if (k < 2) w0 = (w0 & ~(0xFFFFu << sh)) | (v << sh);
+      else w1 = (w1 & ~(0xFFFFu << sh)) | (v << sh);
+    } else {
+      w0 = (w0 & ~(0xFFu << (8 * k))) | (v << (8 * k));
+    }
+  }
+};
 __device__ __forceinline__ uint32_t gring_get(uint32_t w, uint32_t pos) { return (w >> (4u * (pos & 7u))) & 0xFu; }
 __device__ __forceinline__ uint32_t gring_set(uint32_t w, uint32_t pos, uint32_t nib) {
   const uint32_t sh = 4u * (pos & 7u);
@@ -766,7 +794,7 @@ struct Met {
 // Writes the new error into the end-error ring.
 template <typename T>
 __device__ __forceinline__ void metrics_step(const DevCfg<T>& c, const State<T>& s, int64_t i, Met<T>& M,
-                                             const T* tgt, const T* vals, uint32_t gb, uint32_t gcnt, uint32_t b,
+                                             const T* tgt, const T* vals, uint32_t gb, const GCnt& gcnt, uint32_t b,
                                              uint32_t lep) {
   const uint32_t n0 = b;  // entries before this one
   if (b != M.b) {  // stepping on after a failed (done) step without reset: the entry's slots moved
@@ -802,7 +830,7 @@ __device__ __forceinline__ void metrics_step(const DevCfg<T>& c, const State<T>&
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t bit = (gb >> k) & 1u;
-      const bool set = settled_n(c, (gcnt >> (8 * k)) & 0xFFu, n0 + 1u);
+      const bool set = settled_n(c, gcnt.get(k), n0 + 1u);
       M.u[M16_GC + k] += bit;
       M.dirty |= bit << (MD_U + k);
       if (M.u[M16_SET + k] == M_NONE && set) {
@@ -1045,8 +1073,13 @@ __device__ __forceinline__ void goal_init(const DevCfg<T>& c, const State<T>& s,
   if (c.streak_req > 0) {
     const T vals[3] = {der[0], der[1], der[3]};
     const uint32_t gb = goal_status_bits(c, tgt, vals);
-    st_(s.goal, gring_row(lep), ld, i, gring_set(0u, lep, gb));
-    st_(s.goal, GB_CNT, ld, i, (gb & 1u) | ((gb >> 1) & 1u) << 8 | ((gb >> 2) & 1u) << 16 | ((gb >> 3) & 1u) << 24);
+    st_(s.goal, gring_row(lep, c.gring_mask), ld, i, gring_set(0u, lep, gb));
+    if (c.gcnt_wide) {
+      st_(s.goal, GB_CNT, ld, i, (gb & 1u) | ((gb >> 1) & 1u) << 16);
+      st_(s.goal, c.gcnt2_row, ld, i, ((gb >> 2) & 1u) | ((gb >> 3) & 1u) << 16);
+    } else {
+      st_(s.goal, GB_CNT, ld, i, (gb & 1u) | ((gb >> 1) & 1u) << 8 | ((gb >> 2) & 1u) << 16 | ((gb >> 3) & 1u) << 24);
+    }
   }
   st_(s.goal, GB_N, ld, i, 1u);
 }
@@ -1197,7 +1230,7 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_sim_step(const DevCfg<T>
                                                     uint8_t* __restrict__ success, int32_t* __restrict__ term_out,
                                                     int32_t* __restrict__ stats) {
   const int64_t tid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-  const int64_t i = tid / Q;  // Q = 4: lanes 4i..4i+3 integrate aircraft i (fw_quad.hpp)
+  const int64_t i = tid / Q;  // Q = 4: lanes 4i..4i+3 integrate aircraft i (fw_quad.hpp); Q = 2: lanes 2i, 2i+1
   const int qr = (int)(tid % Q);
   if (i >= s.n) return;
   const C& c = *reinterpret_cast<const C*>(cfgp);  // structural specialisation view (fw_device.hpp SpecCfg)
@@ -1215,7 +1248,7 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_sim_step(const DevCfg<T>
   turbulence_at(c, s, i, s.episode[i], k, tl, ta, qr == 0);
   int nfev = 0, nacc = 0;
   uint32_t dmask = 0;
-  __shared__ V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];  // y, f (+ error sum) of the block's aircraft (pairs)
+  __shared__ V2<T> lds[(Q == 1 ? lds_slots<T>() * NP : Q == 2 ? pr::LDS_PAIRS : 1) * BLOCK];  // y, f (+ error sum)
   constexpr bool HO = Q == 1 && !RP && FW_TAIL_QUAD > 0;
   static_assert(!HO || BLOCK == 64, "the tail handoff works per one-wave block");
   __shared__ qd::HoSlot<T> ho[HO ? BLOCK : 1];
@@ -1294,7 +1327,8 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   // ---- epilogue inputs: action / command histories (newest first), goal register, metric state ----
   T seqA[RING + 1][3], seqC[RING + 1][3];
   // goal history (GB_*): entry count, counts, the ring words of the new entry and of the entry leaving the window
-  uint32_t gn = 1u, gcnt = 0u, gw_new = 0u, gw_old = 0u;
+  uint32_t gn = 1u, gw_new = 0u, gw_old = 0u;
+  GCnt gcnt{0u, 0u, c.gcnt_wide != 0};
   const bool goal_on = c.streak_req > 0;
   const uint32_t req = goal_on ? (uint32_t)c.streak_req : 0u;
   // every step but a terminal failure appends a history entry, so the new entry's index is steps0 + 1 unless the
@@ -1337,9 +1371,10 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
       }
     }
     if (goal_on) {
-      gw_new = ld_(s.goal, gring_row(lep + b_guess), ld, i);
-      gw_old = ld_(s.goal, gring_row(lep + b_guess - req), ld, i);
-      gcnt = ld_(s.goal, GB_CNT, ld, i);
+      gw_new = ld_(s.goal, gring_row(lep + b_guess, c.gring_mask), ld, i);
+      gw_old = ld_(s.goal, gring_row(lep + b_guess - req, c.gring_mask), ld, i);
+      gcnt.w0 = ld_(s.goal, GB_CNT, ld, i);
+      if (c.gcnt_wide) gcnt.w1 = ld_(s.goal, c.gcnt2_row, ld, i);
     }
     if (c.metrics) {
       M.load(s, i, lep, b_guess);
@@ -1440,19 +1475,17 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
       gb = goal_status_bits(c, tgt, vals);
       const uint32_t pn = lep + b, po = pn - req;
       if (b != b_guess) {
-        gw_new = ld_(s.goal, gring_row(pn), ld, i);
-        gw_old = ld_(s.goal, gring_row(po), ld, i);
+        gw_new = ld_(s.goal, gring_row(pn, c.gring_mask), ld, i);
+        gw_old = ld_(s.goal, gring_row(po, c.gring_mask), ld, i);
       }
       const uint32_t leave = b >= req ? gring_get(gw_old, po) : 0u;
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint32_t ck = ((gcnt >> (8 * k)) & 0xFFu) - ((leave >> k) & 1u) + ((gb >> k) & 1u);
-        gcnt = (gcnt & ~(0xFFu << (8 * k))) | (ck << (8 * k));
-      }
-      st_(s.goal, gring_row(pn), ld, i, gring_set(gw_new, pn, gb));
-      st_(s.goal, GB_CNT, ld, i, gcnt);
+      for (int k = 0; k < 4; k++) gcnt.set(k, gcnt.get(k) - ((leave >> k) & 1u) + ((gb >> k) & 1u));
+      st_(s.goal, gring_row(pn, c.gring_mask), ld, i, gring_set(gw_new, pn, gb));
+      st_(s.goal, GB_CNT, ld, i, gcnt.w0);
+      if (c.gcnt_wide) st_(s.goal, c.gcnt2_row, ld, i, gcnt.w1);
       // np.mean(history["goal"]["all"][-streak_req:]) >= success_streak_fraction (:540-547)
-      if (steps_tgt >= c.streak_req && (double)(gcnt >> 24) / (double)c.streak_req >= (double)c.streak_frac) {
+      if (steps_tgt >= c.streak_req && (double)gcnt.get(3) / (double)c.streak_req >= (double)c.streak_frac) {
         success = true;
         if (c.on_success == 1) {
           done = true;
@@ -1872,7 +1905,7 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_env_step(const DevCfg<T>
   const bool collect = s.col_rec || s.col_ret || s.col_ctrl;
   if (i >= s.n && !collect) return;
   const C& c = *reinterpret_cast<const C*>(cfgp);  // structural specialisation view (fw_device.hpp SpecCfg)
-  __shared__ __attribute__((aligned(16))) V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];  // y, f (+ error sum) of the block's aircraft (pairs)
+  __shared__ __attribute__((aligned(16))) V2<T> lds[(Q == 1 ? lds_slots<T>() * NP : Q == 2 ? pr::LDS_PAIRS : 1) * BLOCK];  // y, f (+ error sum) of the block's aircraft (pairs; Q = 2: the pair integrator's Y / F / ER)
   static_assert(Q != 1 || RP || FW_TAIL_QUAD == 0 || BLOCK == 64, "the tail handoff works per one-wave block");
   __shared__ qd::HoSlot<T> ho[Q == 1 && !RP ? BLOCK : 1];
   static_assert(BLOCK == 64, "collect_epilogue: one-wave blocks");
@@ -2016,6 +2049,8 @@ struct fw_handle {
   size_t o_colws = 0, o_colcnt = 0;  // in-launch merge tree workspace (records above level 0, counters)
   size_t colcnt_bytes = 0;           // bytes of the tree's arrival counters (zeroed again by clear_tree)
   bool tree_dirty = false;           // an env step with the tree failed: counters may hold stale arrivals
+  uint32_t gring_mask = 127u;        // goal-history ring entries - 1 (a power of two >= 128, >= success_streak_req)
+  int goal_rows = 18;                // GB_* rows (18 + ring words beyond 16 + a second count word when wide)
 };
 
 namespace {
@@ -2166,6 +2201,9 @@ void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
     d.scale_actions = e.scale_actions;
     d.has_bounds = e.has_bounds;
     d.streak_req = e.streak_req;
+    d.gring_mask = h->gring_mask;
+    d.gcnt_wide = e.streak_req > 255;
+    d.gcnt2_row = GB_ROWS + (int)((h->gring_mask + 1u) / 8u - 16u);
     d.on_success = e.on_success;
     d.n_rew = e.n_rew;
     d.step_fail_timesteps = e.step_fail_timesteps;
@@ -2244,7 +2282,7 @@ int validate(const fw_sim_config* s, const fw_env_config* e) {
     if (e->steps_max > 65535) return set_err(FW_E_UNSUPPORTED, "steps_max > 65535");
     if (e->metrics && (e->steps_max < 1 || e->steps_max > 65534))  // 16-bit entry indices, 0xFFFF = none
       return set_err(FW_E_UNSUPPORTED, "episode metrics need 1 <= steps_max <= 65534");
-    if (e->streak_req > 128) return set_err(FW_E_UNSUPPORTED, "success_streak_req > 128");
+    if (e->streak_req > 4096) return set_err(FW_E_UNSUPPORTED, "success_streak_req > 4096");
     if (e->obs_length < 0 || e->obs_length > FW_MAX_OBS_LEN || e->obs_step < 0 ||
         (e->obs_length > 1 && (e->obs_length - 1) * std::max(e->obs_step, 1) + 2 > FW_MAX_OBS_HIST))
       return set_err(FW_E_UNSUPPORTED, "observation length / step out of range");
@@ -2351,7 +2389,7 @@ int lanes_of(const fw_handle* h) {
     const char* e = std::getenv("FWSIM_LANES");
     return e ? std::atoi(e) : 0;
   }();
-  if (env_lanes == 1 || env_lanes == 4) return env_lanes;
+  if (env_lanes == 1 || env_lanes == 2 || env_lanes == 4) return env_lanes;
   return h->n <= FW_QUAD_AUTO_MAX ? 4 : 1;
 }
 
@@ -2374,14 +2412,26 @@ int lanes_of(const fw_handle* h) {
 #define FW_LAUNCH_SPEC(KERNEL, T, h, st, ...) FW_LAUNCH_SPEC_AS(KERNEL, GymX8Cfg, PyflyX8Cfg, T, h, st, __VA_ARGS__)
 
 // ... and Q = lanes per aircraft (1, or 4 for the quad integrator)
-#define FW_LAUNCH_SPEC_Q(KERNEL, T, h, st, ...)                                                                   \
+#define FW_LAUNCH_SPEC_Q(KERNEL, PAIR, T, h, st, ...)                                                             \
   do {                                                                                                             \
     const dim3 b_(BLOCK);                                                                                          \
-    const int q_ = lanes_of(h);                                                                                    \
+    const int q0_ = lanes_of(h);                                                                                   \
+    const int q_ = (!(PAIR) && q0_ == 2) ? 1 : q0_; /* no pair instances of this kernel: one lane */               \
     const dim3 g_((unsigned)(((h)->n * q_ + (FW_HALF_WAVE && q_ == 1 ? 32 : BLOCK) - 1) /                          \
                              (FW_HALF_WAVE && q_ == 1 ? 32 : BLOCK)));                                            \
     const DevCfg<T>* d_ = (const DevCfg<T>*)(h)->dcfg;                                                             \
-    if (q_ == 4) {                                                                                                 \
+    bool done_ = false;                                                                                            \
+    if constexpr (PAIR) {                                                                                          \
+      if (q_ == 2) {                                                                                               \
+        done_ = true;                                                                                              \
+        if ((h)->rand_active) hipLaunchKernelGGL((KERNEL<T, DevCfg<T>, true, 2>), g_, b_, 0, st, d_, __VA_ARGS__); \
+        else if ((h)->spec == 1) hipLaunchKernelGGL((KERNEL<T, GymX8Cfg<T>, false, 2>), g_, b_, 0, st, d_, __VA_ARGS__); \
+        else if ((h)->spec == 2) hipLaunchKernelGGL((KERNEL<T, PyflyX8Cfg<T>, false, 2>), g_, b_, 0, st, d_, __VA_ARGS__); \
+        else hipLaunchKernelGGL((KERNEL<T, DevCfg<T>, false, 2>), g_, b_, 0, st, d_, __VA_ARGS__);                \
+      }                                                                                                            \
+    }                                                                                                              \
+    if (done_) {                                                                                                   \
+    } else if (q_ == 4) {                                                                                          \
       if ((h)->rand_active) hipLaunchKernelGGL((KERNEL<T, DevCfg<T>, true, 4>), g_, b_, 0, st, d_, __VA_ARGS__);   \
       else if ((h)->spec == 1) hipLaunchKernelGGL((KERNEL<T, GymX8Cfg<T>, false, 4>), g_, b_, 0, st, d_, __VA_ARGS__); \
       else if ((h)->spec == 2) hipLaunchKernelGGL((KERNEL<T, PyflyX8Cfg<T>, false, 4>), g_, b_, 0, st, d_, __VA_ARGS__); \
@@ -2465,20 +2515,20 @@ namespace fwl {
 template <typename T>
 int sim_step(fw_handle* h, hipStream_t st, const void* cmd, void* cmd_out, uint8_t* success, int32_t* term,
              int32_t* stats) {
-  FW_LAUNCH_SPEC_Q(k_sim_step, T, h, st, state_of<T>(h), (const T*)cmd, (T*)cmd_out, success, term, stats);
+  FW_LAUNCH_SPEC_Q(k_sim_step, true, T, h, st, state_of<T>(h), (const T*)cmd, (T*)cmd_out, success, term, stats);
   return check_launch();
 }
 template <typename T>
 int env_step(fw_handle* h, hipStream_t st, const void* actions, void* obs, void* reward, uint8_t* done, int32_t* term,
              void* tobs, void* episode, int32_t* stats, int32_t auto_reset) {
-  FW_LAUNCH_SPEC_Q(k_env_step, T, h, st, state_of<T>(h), (const T*)actions, (T*)obs, (T*)reward, done, term, (T*)tobs,
+  FW_LAUNCH_SPEC_Q(k_env_step, true, T, h, st, state_of<T>(h), (const T*)actions, (T*)obs, (T*)reward, done, term, (T*)tobs,
                    (T*)episode, stats, auto_reset);
   return check_launch();
 }
 template <typename T>
 int env_rollout(fw_handle* h, hipStream_t st, int32_t n_steps, const void* actions, void* obs, void* reward,
                 uint8_t* done, int32_t* term, void* tobs, void* episode, int32_t* stats, int32_t auto_reset) {
-  FW_LAUNCH_SPEC_Q(k_env_rollout, T, h, st, state_of<T>(h), n_steps, (const T*)actions, (T*)obs, (T*)reward, done,
+  FW_LAUNCH_SPEC_Q(k_env_rollout, false, T, h, st, state_of<T>(h), n_steps, (const T*)actions, (T*)obs, (T*)reward, done,
                    term, (T*)tobs, (T*)episode, stats, auto_reset);
   return check_launch();
 }
@@ -2570,7 +2620,13 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
   h->o_act = off; off += (size_t)h->act_window * 3 * row;
   h->o_cmdring = off; off += (size_t)h->cmd_window * 3 * row;
   h->o_steps = off; off += row32;
-  h->o_goal = off; off += (size_t)GB_ROWS * row32;
+  if (env) {  // goal ring: the power of two >= success_streak_req entries (at least the 128 of rounds 1-5)
+    uint32_t entries = 128u;
+    while ((int64_t)entries < (int64_t)env->streak_req) entries <<= 1;
+    h->gring_mask = entries - 1u;
+    h->goal_rows = GB_ROWS + (int)(entries / 8u - 16u) + (env->streak_req > 255 ? 1 : 0);
+  }
+  h->o_goal = off; off += (size_t)h->goal_rows * row32;
   h->o_episode = off; off += row32;
   h->o_life = off; off += row32;
   if (h->metrics) {
@@ -2738,6 +2794,12 @@ int fw_update_config(fw_handle* h, const fw_sim_config* sim, const fw_env_config
       if (!same)
         return set_err(FW_E_UNSUPPORTED, "reward.randomize_scaling: the randomised factors cannot change after create");
     }
+    {  // the goal ring and the count width were sized for the streak window at create
+      uint32_t entries = 128u;
+      while ((int64_t)entries < (int64_t)env->streak_req) entries <<= 1;
+      if (entries > h->gring_mask + 1u || (env->streak_req > 255) != (h->env.streak_req > 255))
+        return set_err(FW_E_UNSUPPORTED, "success_streak_req beyond the goal history sized at create");
+    }
     if (env->integration_window != h->iwin)
       return set_err(FW_E_UNSUPPORTED, "integration_window must be the one the handle was created with");
     if (env->reward_potential && !h->o_shp)
@@ -2833,9 +2895,10 @@ int fw_env_rollout(fw_handle* h, int32_t n_steps, const void* actions_dev, void*
 
 int fw_set_lanes(fw_handle* h, int32_t lanes) {
   if (!h) return set_err(FW_E_INVALID, "NULL handle");
-  if (lanes != FW_LANES_AUTO && lanes != 1 && lanes != 4) return set_err(FW_E_INVALID, "lanes must be 0 (auto), 1 or 4");
-  if (lanes == 4 && !h->quad_ok)
-    return set_err(FW_E_INVALID, "lanes = 4 needs a config without wrapped ODE-state variables");
+  if (lanes != FW_LANES_AUTO && lanes != 1 && lanes != 2 && lanes != 4)
+    return set_err(FW_E_INVALID, "lanes must be 0 (auto), 1, 2 or 4");
+  if ((lanes == 4 || lanes == 2) && !h->quad_ok)
+    return set_err(FW_E_INVALID, "lanes = 2 / 4 need a config without wrapped ODE-state variables");
   h->lanes_opt = lanes;
   return FW_OK;
 }
@@ -2926,7 +2989,7 @@ static int ring_copy(fw_handle* h, int32_t block, size_t off, size_t esz, const 
 // the 128 ring positions and recounts the "all" window; the per-target statuses and counts (metrics) stay.
 __global__ void k_goal_xlate(uint32_t* __restrict__ goal, int64_t ld, uint32_t* __restrict__ reg, int64_t n,
                              const uint32_t* __restrict__ life, const uint32_t* __restrict__ steps, int req,
-                             int to_abi) {
+                             int to_abi, uint32_t gm) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const uint32_t N = to_abi ? goal[GB_N * ld + i] : (steps[i] & 0xFFFFu) + 1u;
@@ -2936,7 +2999,7 @@ __global__ void k_goal_xlate(uint32_t* __restrict__ goal, int64_t ld, uint32_t* 
     uint32_t w[4] = {0u, 0u, 0u, 0u};
     for (uint32_t j = 0; j < 128u && j < N; j++) {
       const uint32_t pos = newest - j;
-      w[j >> 5] |= ((gring_get(goal[gring_row(pos) * ld + i], pos) >> 3) & 1u) << (j & 31u);
+      w[j >> 5] |= ((gring_get(goal[gring_row(pos, gm) * ld + i], pos) >> 3) & 1u) << (j & 31u);
     }
     for (int r = 0; r < 4; r++) reg[r * n + i] = w[r];
     return;
@@ -2944,7 +3007,7 @@ __global__ void k_goal_xlate(uint32_t* __restrict__ goal, int64_t ld, uint32_t* 
   uint32_t cnt = 0u;
   for (uint32_t j = 0; j < 128u; j++) {
     const uint32_t pos = newest - j, bit = (reg[(j >> 5) * n + i] >> (j & 31u)) & 1u;
-    uint32_t* wp = goal + gring_row(pos) * ld + i;
+    uint32_t* wp = goal + gring_row(pos, gm) * ld + i;
     *wp = gring_set(*wp, pos, (gring_get(*wp, pos) & 7u) | (bit << 3));
     if ((int)j < req && j < N) cnt += bit;
   }
@@ -2954,10 +3017,12 @@ __global__ void k_goal_xlate(uint32_t* __restrict__ goal, int64_t ld, uint32_t* 
 
 static int goal_copy(fw_handle* h, const void* src, void* dst, int to_abi, hipStream_t st) {
   char* b = (char*)h->base;
+  if (!to_abi && h->has_env && h->env.streak_req > 128)  // the 128-bit register cannot hold the window
+    return set_err(FW_E_UNSUPPORTED, "FW_BLK_GOAL: setting the goal history needs success_streak_req <= 128");
   hipLaunchKernelGGL(k_goal_xlate, dim3((unsigned)((h->n + 255) / 256)), dim3(256), 0, st, (uint32_t*)(b + h->o_goal),
                      (int64_t)h->ld, to_abi ? (uint32_t*)dst : (uint32_t*)const_cast<void*>(src), h->n,
                      (const uint32_t*)(b + h->o_life), (const uint32_t*)(b + h->o_steps),
-                     h->has_env ? std::max(h->env.streak_req, 0) : 0, to_abi);
+                     h->has_env ? std::max(h->env.streak_req, 0) : 0, to_abi, h->gring_mask);
   return check_launch();
 }
 
