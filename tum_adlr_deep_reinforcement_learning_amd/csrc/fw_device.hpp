@@ -68,6 +68,18 @@ FW_HD int32_t pack_stats(int nfev, int nacc, uint32_t dmask) {
 #if FW_RK_UNROLL && !FW_FOLD_INPLACE
 #error "FW_RK_UNROLL needs FW_FOLD_INPLACE"
 #endif
+#ifndef FW_YF_REGS
+#define FW_YF_REGS 1  // one-lane rk45: the accepted y / f in registers (AGPR room at one wave per SIMD) instead of LDS: long window -9 % (profiles/r06_lanes_sweep.log)
+#endif
+#if FW_YF_REGS && !FW_RK_UNROLL
+#error "FW_YF_REGS needs FW_RK_UNROLL"
+#endif
+#ifndef FW_Q1_SIGMA_1RCP
+#define FW_Q1_SIGMA_1RCP 0  // one-lane rhs(): fp32 stall blend with one reciprocal, as rhs_quad (A/B)
+#endif
+#ifndef FW_Q1_IVA_SEL
+#define FW_Q1_IVA_SEL 0  // one-lane rhs(): 1 / Va from 1 / Va_raw where Va clips only from below (A/B)
+#endif
 #ifndef FW_RELAUNDER
 #define FW_RELAUNDER 0  // 1: re-issue config scalar loads per RHS (helped the generic kernel; -4.5% slower on the specialised one)
 #endif  // RHS evaluations per step before the step is declared a solver failure
@@ -160,6 +172,7 @@ struct DevCfg {
   T obs_noise_mean, obs_noise_std;
   fw_obs_entry obs[FW_MAX_OBS];
   fw_rew_factor rew[FW_MAX_REW];
+  static constexpr int const_limits = 0;  // (SpecCfg views: limit values compile-time constants)
 };
 
 // Compile-time specialisations of a configuration's STRUCTURE (which variables
@@ -585,11 +598,12 @@ FW_HD int rhs(const C& c0, const A& a, const StepCtx<T>& X, bool first, const T*
     sa = rxz2 > T(0) ? va[2] * irxz : T(0);
     ca = rxz2 > T(0) ? va[0] * irxz : T(1);
   }
+  T iVr = T(0);
   if (c.trig_beta) {
     sb = sin(beta);
     cb = cos(beta);
   } else {  // sin / cos of beta = asin(v / Va): v / Va and sqrt(u^2 + w^2) / Va
-    const T iVr = frcp(Va_raw);
+    iVr = frcp(Va_raw);
     sb = va[1] * iVr;
     cb = rxz * iVr;
   }
@@ -601,8 +615,13 @@ FW_HD int rhs(const C& c0, const A& a, const StepCtx<T>& X, bool first, const T*
   T ex1, ex2;
   if constexpr (sizeof(T) == 4) {  // exp(-M (alpha - a0)), exp(M (alpha + a0)) as exp2 of one fma each
     const T l2e = T(1.4426950408889634), k = a.M * l2e, k0 = a.M * a.a0 * l2e;
-    ex1 = __builtin_amdgcn_exp2f(fmaf(-k, alpha, k0));
-    ex2 = __builtin_amdgcn_exp2f(fmaf(k, alpha, k0));
+    if constexpr (FW_Q1_SIGMA_1RCP) {  // exponents clamped at 2^120: S + C below stays finite (rhs_quad)
+      ex1 = __builtin_amdgcn_exp2f(fminf(fmaf(-k, alpha, k0), T(120)));
+      ex2 = __builtin_amdgcn_exp2f(fminf(fmaf(k, alpha, k0), T(120)));
+    } else {
+      ex1 = __builtin_amdgcn_exp2f(fmaf(-k, alpha, k0));
+      ex2 = __builtin_amdgcn_exp2f(fmaf(k, alpha, k0));
+    }
   } else {
     ex1 = fexp(-a.M * (alpha - a.a0));
     ex2 = fexp(a.M * (alpha + a.a0));
@@ -611,15 +630,32 @@ FW_HD int rhs(const C& c0, const A& a, const StepCtx<T>& X, bool first, const T*
   // e1 e2 = exp(2 M a0) = C, the denominator is S + C with S = 1+e1+e2, so
   // sigma = 1 / (1 + C/S): the same value, but it never forms the ~1e38 product
   // (whose fp32 reciprocal flushes to 0 and flips sigma from 1 to 0 deep in
-  // stall) and it is exactly 1 when an exponential overflows.
-  const T sigma = frcp(T(1) + a.sig_c * frcp(T(1) + ex1 + ex2));
+  // stall) and it is exactly 1 when an exponential overflows.  FW_Q1_SIGMA_1RCP (fp32): S / (S + C) with
+  // the exponents clamped, one reciprocal (where the clamp acts C / S < 1e-15 and sigma rounds to 1 either way)
+  T sigma;
+  if constexpr (sizeof(T) == 4 && FW_Q1_SIGMA_1RCP) {
+    const T S = T(1) + ex1 + ex2;
+    sigma = S * frcp(S + a.sig_c);
+  } else {
+    sigma = frcp(T(1) + a.sig_c * frcp(T(1) + ex1 + ex2));
+  }
   const T osig = T(1) - sigma;
   // sgn(alpha) sin(alpha)^2 = sin(alpha) |sin(alpha)|: sin has alpha's sign on [-pi, pi] and the
   // product is 0 where it does not (pyfly.py:1547-1579 multiply by np.sign(alpha))
   const T ssa = sa * fabs(sa);
   const T CLlin = a.CL0 + a.CLa * alpha;
   const T CL = osig * CLlin + sigma * (T(2) * ssa * ca);
-  const T iVa = frcp(Va);
+  T iVa;
+  if constexpr (FW_Q1_IVA_SEL && C::const_limits) {
+    // X8 limits: Va clips only from below (at 1e-6), so Va == Va_raw unless Va_raw < vmin, and 1 / Va is the
+    // reciprocal already formed for beta (the trig_beta-free branch above needs iVr)
+    if (!c.trig_beta && !(c.lim[FW_V_VA].vmax < T(__builtin_inf())))  // (compile-time for the X8 views)
+      iVa = Va_raw >= c.lim[FW_V_VA].vmin ? iVr : T(1) / c.lim[FW_V_VA].vmin;  // Va = max(Va_raw, vmin)
+    else
+      iVa = frcp(Va);
+  } else {
+    iVa = frcp(Va);
+  }
   const T qn = q * iVa;  // q / Va
   // lift / drag / pitch moment per unit dynamic pressure (pyfly.py:1529-1579)
   const T flift = a.qS * V2a * (CL + a.kCLq * qn + a.CLde * elev);
@@ -757,8 +793,19 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
 
   // y and f (the accepted state and its derivative) live in LDS slots of this
   // lane (pair p at s[p * stride]); the stage accumulators stay in VGPRs.
-#define Y(p) sy[(p) * stride]
-#define F(p) sf[(p) * stride]
+  // FW_YF_REGS (fp32): in registers instead (written to the LDS slots before a tail handoff, which reads them there)
+  constexpr bool YFR = FW_YF_REGS && sizeof(T) == 4;  // (fp64: the instances already spill; not measured)
+  V Yr[YFR ? NP : 1], Fr[YFR ? NP : 1];
+  auto Yp = [&](int p) -> V& {
+    if constexpr (YFR) return Yr[p];
+    else return sy[p * stride];
+  };
+  auto Fp = [&](int p) -> V& {
+    if constexpr (YFR) return Fr[p];
+    else return sf[p * stride];
+  };
+#define Y(p) Yp(p)
+#define F(p) Fp(p)
 #if FW_ER_LDS
   // error accumulator in this lane's third LDS slot (registers go to the live stage vectors)
 #define ERV(p) se[(p) * stride]
@@ -907,6 +954,13 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
       const int na = __popcll(am);  // (lanes of the wave's aircraft past N have returned: quads need 4 na live lanes)
       if (na > 0 && na <= c.tail_quad && 4 * na <= __popcll(__ballot(true))) {
         handoff = true;
+        if constexpr (YFR) {
+#pragma unroll
+          for (int p = 0; p < NP; p++) {
+            sy[p * stride] = Yr[p];
+            sf[p * stride] = Fr[p];
+          }
+        }
         break;
       }
     }
@@ -1204,7 +1258,10 @@ rk_done:
 #endif
 #pragma unroll
   for (int p = 0; p < NP; p++) {
-    const V v = Y(p);
+    V v = Y(p);
+    if constexpr (YFR) {
+      if (handoff) v = sy[p * stride];  // (the quads wrote the handed-off aircraft's y to the slots)
+    }
     y_io[2 * p] = v.x;
     if (2 * p + 1 < NY) y_io[2 * p + 1] = v.y;
   }
