@@ -160,8 +160,25 @@ typedef struct fw_collect_io {
   float *obs_rows, *act_rows, *val_rows, *logp_rows, *rew_rows;
   uint8_t* start_rows;
   int64_t n;
+  /* ABI 12: the statistics update the env step deferred (fwsim.h fw_collect_epilogue.defer; the fields of
+   * fw_collect_pending).  When pend is set and t >= 1, every block merges the pend_cnt records and applies
+   * update_from_moments to the statistics the env step found (rms_prev) before normalising; block 0 writes
+   * the updated statistics to rms (in place) and the merged record (merged [1 + 2D], may be NULL).  At
+   * t = 0 nothing is pending (the previous collection ended with fw_vecnorm_pending_update).  NULL: off. */
+  const double* pend;
+  int64_t pend_stride;
+  int32_t pend_cnt, has_ret;
+  double* merged;
+  const double* rms_prev;
 } fw_collect_io;
 int fw_collect_policy(const fw_mlp_policy* p, const fw_collect_io* io, void* stream);
+
+/* ABI 12: the deferred final merge on its own (after a collection's last env step): merges the cnt records
+ * (fw_collect_pending's layout), applies update_from_moments to rms [2d + 4] and writes the merged record
+ * (merged may be NULL) -- the same bits as the merging fw_collect_policy launch and as the env step's own
+ * final node. */
+int fw_vecnorm_pending_update(const double* pend, int64_t stride, int32_t cnt, int32_t d, int32_t has_ret,
+                              double* rms, double* merged, void* stream);
 
 #ifdef __cplusplus
 }

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define FWSIM_ABI_VERSION 11
+#define FWSIM_ABI_VERSION 12
 
 /* ---- error codes ---------------------------------------------------------- */
 #define FW_OK 0
@@ -272,6 +272,12 @@ typedef struct fw_env_config {
   double target_slope_low[3], target_slope_high[3];
   double target_amp_low[3], target_amp_high[3];
   double target_period_low[3], target_period_high[3];
+  /* ABI 12: np_random draws sample_simulator_parameters makes at every reset for "simulator" attributes
+   * PyFly never reads (fixed_wing.py:802-813; one each: uniform, or choice with probabilities), which the
+   * env-draw tape holds before sample_target's: fw_reset / the auto-reset skip that many tape draws.  They
+   * leave the episode unchanged, so nothing else reads them.                                         */
+  int32_t tape_skip;
+  int32_t pad12_;
 } fw_env_config;
 
 /* Episode-metric record written for every done env (SoA [FW_NMETRIC][N] so the stores
@@ -461,6 +467,11 @@ int fw_set_metrics_output(fw_handle* h, void* metrics_dev);
  *            RunningMeanStd.update_from_moments (running_mean_std.py:26-40) with the merged record, the
  *            same arithmetic as fw_rms_update of that one record.  A collect step under one VecNormalize is
  *            then policy + env step, two launches.  NULL: update later (sharded: after the exchange).
+ *   defer    (ABI 12; needs merged) 1: the tree stops one level short -- the launch leaves the final node's
+ *            records (at most 64, fw_collect_pending) in place and writes neither merged nor rms; the next
+ *            fw_collect_policy (fwrollout.h, io->pend) merges them in its prologue and applies the update, or
+ *            fw_vecnorm_pending_update does.  Same bits as the in-launch final node (the same sums in the same
+ *            order); takes the final node's hand-off chain off the env step's tail.
  * Applies to fw_env_step only (not fw_env_rollout); NULL (or all fields NULL) turns it off. */
 typedef struct fw_collect_epilogue {
   double* ret;
@@ -469,8 +480,22 @@ typedef struct fw_collect_epilogue {
   int32_t* row_ctrl;
   double* merged;
   double* rms;
+  int32_t defer;
+  int32_t pad;
 } fw_collect_epilogue;
 int fw_set_collect_epilogue(fw_handle* h, const fw_collect_epilogue* epi);
+/* ABI 12: where the deferred final level of the next fw_env_step lives (with the current epilogue and lanes
+ * setting): count records of 1 + 2D fp64 fields, field f of record k at records[f * stride + k]; rms_prev =
+ * the launch's copy of rms [2d + 4] as it found it, which the merging fw_collect_policy launch reads (its
+ * block 0 rewrites rms while other blocks may still be starting). */
+typedef struct fw_collect_pend {
+  const double* records;
+  int64_t stride;
+  int32_t count;
+  int32_t D;
+  const double* rms_prev;
+} fw_collect_pend;
+int fw_collect_pending(const fw_handle* h, fw_collect_pend* out);
 /* Records the next fw_env_step writes (its block count: depends on N and fw_get_lanes) and the most any
  * lanes setting can write (size the buffer with that). */
 int fw_collect_records(const fw_handle* h, int64_t* n_records, int64_t* max_records);

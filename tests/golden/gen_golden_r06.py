@@ -64,6 +64,16 @@ class TapeRNG:
         assert size is None and loc == 0 and scale == 0
         return self.rs.normal(loc, scale)
 
+    def choice(self, a, size=None, replace=True, p=None):
+        # numpy RandomState.choice with p: cdf = p.cumsum() / its last entry, one random_sample(), searchsorted
+        # right (mtrand.pyx); without p it draws an integer (randint), which a tape of doubles cannot hold
+        assert size is None and p is not None
+        cdf = np.cumsum(np.asarray(p, dtype=np.float64))
+        cdf /= cdf[-1]
+        u = float(self.rs.random_sample())
+        self.tape.append(u)
+        return a[int(cdf.searchsorted(u, side="right"))]
+
     def __getattr__(self, name):
         raise AttributeError("TapeRNG: np_random.%s is not on the tape" % name)
 
@@ -111,6 +121,20 @@ def _success(cfg):
     cfg["action"]["scale_space"] = False  # the PID commands the actuators directly
 
 
+def _simattr(cfg):
+    # "simulator" attributes PyFly never reads (sample_simulator_parameters, fixed_wing.py:802-813): drawn at
+    # every reset before sample_target, set on the simulator, no effect on the flight; linear targets so the
+    # tape's order matters
+    _linear(cfg)
+    cfg["simulator"]["inert_gain"] = {"low": 0.5, "high": 2.0}
+    cfg["simulator"]["inert_mode"] = {"values": [0, 1, 2], "probabilities": [0.2, 0.5, 0.3]}
+
+
+CASES_B = {
+    # round 6, second batch (env_r06b.npz)
+    "simattr": (_simattr, "rand", 400, 3, 300, None),
+}
+
 CASES = {
     # name -> (config modifier, policy, steps_max, episodes, steps per episode, explicit targets at reset)
     "linear": (_linear, "rand", 400, 3, 300, None),
@@ -153,10 +177,10 @@ def episode(env, rng, pol, n_steps, target=None):
                                         for k in ("roll", "pitch", "Va")]))
 
 
-def gen_env_r06():
+def gen_env_r06(cases=CASES, fname="env_r06.npz", seed=606):
     out = {}
-    rng = np.random.RandomState(606)
-    for name, (mod, pol, smax, eps, n, target) in CASES.items():
+    rng = np.random.RandomState(seed)
+    for name, (mod, pol, smax, eps, n, target) in cases.items():
         cfg, path = _cfg(mod)
         out[name + "__config_json"] = np.array(json.dumps(cfg))
         out[name + "__steps_max"] = np.array(smax)
@@ -171,7 +195,7 @@ def gen_env_r06():
             print("r06 %s ep%d: %d steps, %d draws, last term=%r, rew sum %.3f" % (
                 name, ep, len(res["rew"]), len(res["tape"]), res["term"][-1], res["rew"].sum()))
         out[name + "__episodes"] = np.array(eps)
-    np.savez_compressed(os.path.join(OUT, "env_r06.npz"), **out)
+    np.savez_compressed(os.path.join(OUT, fname), **out)
 
 
 STREAK_CASES = {
@@ -199,5 +223,10 @@ def gen_env_streak():
 
 
 if __name__ == "__main__":
-    gen_env_r06()
-    gen_env_streak()
+    which = sys.argv[1:] or ["r06", "streak", "r06b"]
+    if "r06" in which:
+        gen_env_r06()
+    if "streak" in which:
+        gen_env_streak()
+    if "r06b" in which:
+        gen_env_r06(CASES_B, "env_r06b.npz", 616)

@@ -17,11 +17,12 @@ import _fixtures as F
 from tum_adlr_deep_reinforcement_learning_amd import config as C
 
 R06 = ["linear", "linear_fix", "sinus", "resample", "success"]
+R06B = ["simattr"]  # env_r06b.npz (round 6, second batch)
 
 
 def r06_spec(name, tmpdir):
-    """EnvSpec of an env_r06.npz case (writes the stored reference config file to tmpdir)."""
-    d = F.load("env_r06.npz")
+    """EnvSpec of an env_r06.npz / env_r06b.npz case (writes the stored reference config file to tmpdir)."""
+    d = F.load("env_r06b.npz" if name in R06B else "env_r06.npz")
     path = os.path.join(str(tmpdir), name + ".json")
     with open(path, "w") as f:
         f.write(str(d[name + "__config_json"]))
@@ -39,7 +40,7 @@ def draws_per_sample(spec):
     return n
 
 
-@pytest.mark.parametrize("name", R06)
+@pytest.mark.parametrize("name", R06 + R06B)
 def test_r06_config_struct(name, tmpdir):
     spec, d = r06_spec(name, tmpdir)
     cfg = json.loads(str(d[name + "__config_json"]))
@@ -72,17 +73,20 @@ def test_r06_config_struct(name, tmpdir):
             assert F_.randomize == 1 and (F_.scaling, F_.scaling_hi) == tuple(f["scaling"])
 
 
-@pytest.mark.parametrize("name", R06)
+@pytest.mark.parametrize("name", R06 + R06B)
 def test_r06_tapes(name, tmpdir):
     """The recorded draws are numpy random_sample() values, as many per episode as the reference's calls:
-    one sample_target at the reset, one per resample, plus one per randomised reward factor at the reset."""
+    one per inert simulator attribute and one sample_target at the reset, one per resample, plus one per
+    randomised reward factor at the reset."""
     spec, d = r06_spec(name, tmpdir)
     per = draws_per_sample(spec)
     n_rsc = sum(1 for f in spec.cfg["reward"]["factors"] if isinstance(f["scaling"], list))
+    skip = spec.struct().tape_skip
+    assert skip == len(spec.sim_attrs) == (2 if name == "simattr" else 0)
     for ep in range(int(d[name + "__episodes"])):
         tape = d["%s__ep%d__tape" % (name, ep)]
         assert np.all((tape >= 0) & (tape < 1))
-        resamples = (len(tape) - per - n_rsc) / per
+        resamples = (len(tape) - skip - per - n_rsc) / per
         assert resamples == int(resamples) and resamples >= 0, (ep, len(tape), per)
         if name == "resample":
             assert int(resamples) == len(d["%s__ep%d__rew" % (name, ep)]) // 60  # every 60 steps
@@ -100,3 +104,33 @@ def test_attitude_angular_refused(tmpdir):
         json.dump(cfg, f)
     with pytest.raises(NotImplementedError):
         C.EnvSpec(config_path=path, sim_config_kw={"turbulence": False}).struct()
+
+
+def _sim_block_spec(tmpdir, extra):
+    _, d = r06_spec("linear", tmpdir)
+    cfg = json.loads(str(d["linear__config_json"]))
+    cfg["simulator"].update(extra)
+    path = os.path.join(str(tmpdir), "sa.json")
+    with open(path, "w") as f:
+        json.dump(cfg, f)
+    return lambda: C.EnvSpec(config_path=path, sim_config_kw={"turbulence": False})
+
+
+def test_simulator_attributes():
+    """The "simulator" block's other keys (sample_simulator_parameters, fixed_wing.py:802-813): attributes PyFly
+    never reads are accepted (their reset draws are skipped on a tape, nothing else changes); dt / cur_sim_step
+    (read by PyFly.step) are refused loudly; a PyFly object replaced by a number is invalid, as the
+    reference's next step would fail on it; neither values nor low / high: KeyError, as there."""
+    import tempfile
+    tmp = tempfile.mkdtemp()
+    spec = _sim_block_spec(tmp, {"foo": {"low": 0, "high": 2}, "bar": {"values": [1, 2], "probabilities": [0.3, 0.7]},
+                                 "baz": {"values": ["x", "y"]}})()
+    assert spec.sim_attrs == {"foo": ("uniform", 0, 2), "bar": ("choice", [1, 2], [0.3, 0.7]),
+                              "baz": ("choice", ["x", "y"], None)}
+    assert spec.struct().tape_skip == 3
+    for key, exc in (("dt", NotImplementedError), ("cur_sim_step", NotImplementedError), ("wind", ValueError),
+                     ("state", ValueError)):
+        with pytest.raises(exc):
+            _sim_block_spec(tmp, {key: {"low": 0.005, "high": 0.02}})()
+    with pytest.raises(KeyError):
+        _sim_block_spec(tmp, {"foo": {"lo": 0}})()

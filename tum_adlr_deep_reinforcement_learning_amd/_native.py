@@ -22,7 +22,7 @@ SOURCES = UNITS + [os.path.join(CSRC, "fw_device.hpp"), os.path.join(CSRC, "fw_q
 ARCH = os.environ.get("FWSIM_ARCH", "gfx950")
 
 _lib = None
-ABI_VERSION = 11  # include/fwsim.h FWSIM_ABI_VERSION
+ABI_VERSION = 12  # include/fwsim.h FWSIM_ABI_VERSION
 
 
 class FwError(RuntimeError):
@@ -140,6 +140,7 @@ SIGNATURES = {
     "fw_set_metrics_output": (_c.c_int, [_vp, _vp]),
     "fw_set_collect_epilogue": (_c.c_int, [_vp, _vp]),
     "fw_collect_records": (_c.c_int, [_vp, _c.POINTER(_i64), _c.POINTER(_i64)]),
+    "fw_collect_pending": (_c.c_int, [_vp, _vp]),
     # include/fwrollout.h
     "fw_gae": (_c.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _c.c_double, _c.c_double, _vp, _vp, _vp]),
     "fw_moments_workspace_bytes": (_c.c_size_t, [_i64, _i32]),
@@ -153,6 +154,7 @@ SIGNATURES = {
     "fw_moments_merge": (_c.c_int, [_vp, _i32, _i32, _vp, _vp]),
     "fw_vecnorm_merge_update": (_c.c_int, [_vp, _i32, _i32, _i32, _vp, _vp, _vp]),
     "fw_collect_policy": (_c.c_int, [_vp, _vp, _vp]),
+    "fw_vecnorm_pending_update": (_c.c_int, [_vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp]),
 }
 
 
@@ -172,7 +174,11 @@ class FwMlpPolicy(ctypes.Structure):  # include/fwrollout.h fw_mlp_policy
 
 class FwCollectEpilogue(ctypes.Structure):  # include/fwsim.h fw_collect_epilogue
     _fields_ = [("ret", _vp), ("gamma", _c.c_double), ("records", _vp), ("row_ctrl", _vp), ("merged", _vp),
-                ("rms", _vp)]
+                ("rms", _vp), ("defer", _i32), ("pad", _i32)]
+
+
+class FwCollectPend(ctypes.Structure):  # include/fwsim.h fw_collect_pend (ABI 12)
+    _fields_ = [("records", _vp), ("stride", _i64), ("count", _i32), ("D", _i32), ("rms_prev", _vp)]
 
 
 class FwCollectIO(ctypes.Structure):  # include/fwrollout.h fw_collect_io
@@ -180,7 +186,8 @@ class FwCollectIO(ctypes.Structure):  # include/fwrollout.h fw_collect_io
                 ("clip_obs", _c.c_double), ("clip_reward", _c.c_double), ("norm_obs", _i32), ("norm_reward", _i32),
                 ("noise", _vp), ("low", _vp), ("high", _vp), ("clipped", _vp), ("ctrl", _vp), ("obs_rows", _vp),
                 ("act_rows", _vp), ("val_rows", _vp), ("logp_rows", _vp), ("rew_rows", _vp), ("start_rows", _vp),
-                ("n", _i64)]
+                ("n", _i64), ("pend", _vp), ("pend_stride", _i64), ("pend_cnt", _i32), ("has_ret", _i32),
+                ("merged", _vp), ("rms_prev", _vp)]
 
 
 def load(path=None):

@@ -162,7 +162,8 @@ class FwEnvConfig(ctypes.Structure):
                 ("target_radians", ctypes.c_int32 * 3), ("pad11_", ctypes.c_int32),
                 ("target_slope_low", ctypes.c_double * 3), ("target_slope_high", ctypes.c_double * 3),
                 ("target_amp_low", ctypes.c_double * 3), ("target_amp_high", ctypes.c_double * 3),
-                ("target_period_low", ctypes.c_double * 3), ("target_period_high", ctypes.c_double * 3)]
+                ("target_period_low", ctypes.c_double * 3), ("target_period_high", ctypes.c_double * 3),
+                ("tape_skip", ctypes.c_int32), ("pad12_", ctypes.c_int32)]
 
 
 # ---------------------------------------------------------------------------
@@ -566,9 +567,7 @@ class EnvSpec:
             raise NotImplementedError("reward.form %r" % cfg["reward"].get("form"))
         if cfg["target"].get("on_success", "none") not in FW_ON_SUCCESS:
             raise ValueError("Unexpected goal action {}".format(cfg["target"].get("on_success")))  # fixed_wing.py:553-559
-        sim_keys = set(cfg.get("simulator", {}).keys()) - {"states", "model"}
-        if sim_keys:  # setattr(simulator, key, sample) of arbitrary simulator attributes (fixed_wing.py:802-813)
-            raise NotImplementedError("randomised simulator attributes %s (only 'model' parameters)" % sorted(sim_keys))
+        self.sim_attrs = self._parse_sim_attrs(cfg.get("simulator", {}))
         self.rand_params = self._parse_model(cfg.get("simulator", {}).get("model"))
         self.scale_actions = bool(cfg["action"].get("scale_space", False))
         self.metrics_enabled = True  # track cfg["metrics"] on the device (False: skip that state traffic)
@@ -577,6 +576,41 @@ class EnvSpec:
         # applies those states in set_curriculum_level afterwards (:300)
         self._build_spaces()
         self.set_curriculum_level(curriculum_level)
+
+    # PyFly attributes PyFly.step / reset read (pyfly.py:1251-1482): the numbers among them change the dynamics
+    # (dt: the RK45 interval, cur_sim_step: the turbulence sample index), the objects the next step would fail on
+    _SIM_STEP_NUMBERS = ("dt", "cur_sim_step")
+    _SIM_STEP_OBJECTS = ("actuation", "cfg", "energy_states", "model_inputs", "params", "plots", "rec", "state",
+                         "viewer", "wind")
+
+    @classmethod
+    def _parse_sim_attrs(cls, sim):
+        """The other keys of the "simulator" block (sample_simulator_parameters, fixed_wing.py:802-813): at every
+        reset np_random.choice(values, p=probabilities) or np_random.uniform(low, high) (bool if low is a bool)
+        is set as an attribute of the PyFly object.  PyFly's step and reset never read an attribute of any other
+        name, so for those the draw leaves the episode unchanged: they are accepted (validated as the reference
+        reads them) and have no device-side effect -- the device draws nothing for them (its draws are keyed
+        per purpose, so no other draw moves).  Randomised dt / cur_sim_step change the integration interval or
+        the turbulence index per episode: refused.  An object attribute replaced by a number makes the
+        reference's next step fail: refused as invalid."""
+        out = {}
+        for key, value in sim.items():
+            if key in ("states", "model"):
+                continue
+            if key in cls._SIM_STEP_NUMBERS:
+                raise NotImplementedError("randomised simulator attribute %r (a per-episode %s on the device)" % (
+                    key, "integration interval" if key == "dt" else "turbulence sample index"))
+            if key in cls._SIM_STEP_OBJECTS:
+                raise ValueError("simulator attribute %r is a PyFly object; a sampled number in its place breaks "
+                                 "PyFly.step" % key)
+            if "values" in value:
+                probs = value.get("probabilities")
+                if probs is not None and len(probs) != len(value["values"]):
+                    raise ValueError("simulator attribute %r: probabilities and values differ in length" % key)
+                out[key] = ("choice", list(value["values"]), probs)
+            else:
+                out[key] = ("uniform", value["low"], value["high"])  # (KeyError without low / high, as there)
+        return out
 
     def _parse_model(self, m):
         """The "simulator": {"model": ...} block -> fw_rand_param entries (sample_simulator_parameters,
@@ -822,6 +856,7 @@ class EnvSpec:
                 e.target_amp_low[i], e.target_amp_high[i] = float(p["amplitude_low"]), float(p["amplitude_high"])
                 e.target_period_low[i] = float(p.get("period_low", 250))
                 e.target_period_high[i] = float(p.get("period_high", 500))
+        e.tape_skip = len(self.sim_attrs)  # (inert simulator attributes: their reset draws, skipped on a tape)
         t = cfg["target"]
         names = [m["name"] for m in cfg.get("metrics", [])]
         unknown = set(names) - set(METRIC_LAYOUT)

@@ -150,6 +150,7 @@ struct DevCfg {
   int has_delta[3], has_bound[3];
   // linear / sinusoidal target classes (fw_env_config ABI 11): draw bounds, np.radians factor (1 or pi/180)
   int tprops;                          // some target is linear or sinusoidal: State::tpr rows are kept
+  int tape_skip;                       // env-draw tape entries before sample_target's at a reset (inert attributes)
   T tgt_rad[3], tgt_slo[3], tgt_shi[3], tgt_alo[3], tgt_ahi[3], tgt_plo[3], tgt_phi[3];
   int goal_flag;                       // a success reward factor: State::gflag keeps goal_achieved
   // goal-status history ring (fw_kernels.hip GB_*): 8 x gring_words entries (a power of two >= 128 and >=

@@ -151,6 +151,8 @@ struct State {
   double* col_rms;    // RunningMeanStd buffer update_from_moments is applied to (with col_merged), or null
   double* col_lvl;    // merge-tree records above level 0 (handle workspace, fw_stats::merge_tree_size)
   uint32_t* col_cnt;  // merge-tree arrival counters (handle workspace, zero between launches)
+  int32_t col_defer;  // 1: the tree stops one level short (the next fw_collect_policy merges the last level)
+  double* col_shadow; // (col_defer) copy of col_rms as the launch found it, what the merging policy launch reads
 };
 
 // streaming episode-metric state (fixed_wing.py:1644-1736 restated over running sums), packed (round 5):
@@ -1039,6 +1041,9 @@ __device__ __forceinline__ void reset_lane(const DevCfg<T>& c, const State<T>& s
     // sample_target (fixed_wing.py:654-746): Philox stream 0 after the state draws, or the env-draw tape
     const T vals[3] = {der[0], der[1], der[3]};
     EnvRng<T> rng(s, i, D);
+    // sample_simulator_parameters' draws for simulator attributes PyFly never reads come first (:802-813);
+    // they change nothing, so a tape replay only steps over them
+    if (s.tape) rng.cur += (uint32_t)c.tape_skip;
     sample_target(c, s, i, rng, vals, 0, tin, ld, tgt);
     if (s.tape && s.rsc)  // reward.randomize_scaling from the tape, after the targets (fixed_wing.py:473-479)
       for (int r = 0; r < c.n_rew; r++)
@@ -1749,12 +1754,15 @@ __device__ __forceinline__ void merge_node(const double* src, int64_t stride, in
 // each node's counter is reset by its last arriver, for the next launch.  The merged record equals the one
 // merge over all block records (fw_moments_merge) to rounding, not bit for bit (another summation tree).
 __device__ __forceinline__ void collect_merge(const double* rec0, double* lvl, uint32_t* cnt, double* merged, double* rms,
-                                           int D, int d, bool has_ret, double* st) {
+                                           int D, int d, bool has_ret, double* st, bool defer) {
   const int l = (int)(threadIdx.x & 63);
   int64_t nodes = gridDim.x, idx = blockIdx.x, stride = gridDim.x;
   const double* src = rec0;
   while (true) {
     const bool fin = nodes <= fw_stats::MERGE_FANIN;
+    // deferred (fw_collect_epilogue.defer, round 6): the final node's records stay where they are published;
+    // the next fw_collect_policy launch merges them in its prologue (fw_collect_pending), off this launch's tail
+    if (fin && defer) return;
     const int64_t g = fin ? 0 : idx / fw_stats::MERGE_FANIN;
     const int gs = fin ? (int)nodes : (int)std::min<int64_t>(fw_stats::MERGE_FANIN, nodes - g * fw_stats::MERGE_FANIN);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's published words have left the CU
@@ -1827,6 +1835,8 @@ __device__ __forceinline__ void collect_epilogue(const State<T>& s, int64_t i, b
     ret = g + (double)(float)rew_out[i];
     s.col_ret[i] = done_out[i] ? 0.0 : ret;
   }
+  if (s.col_defer && blockIdx.x == 0)  // the statistics the next policy launch updates (its blocks read this copy,
+    for (int e = lane; e < 2 * ow + 4; e += 64) s.col_shadow[e] = s.col_rms[e];  // while its block 0 rewrites col_rms)
   if (s.col_rec) {
     const int D = ow + (has_ret ? 1 : 0);
     const bool tree = s.col_merged != nullptr;
@@ -1882,7 +1892,7 @@ __device__ __forceinline__ void collect_epilogue(const State<T>& s, int64_t i, b
     }
     if (tree) {
       __syncthreads();  // (the staging area is reused by the merge)
-      collect_merge(s.col_rec, s.col_lvl, s.col_cnt, s.col_merged, s.col_rms, D, ow, has_ret, mst);
+      collect_merge(s.col_rec, s.col_lvl, s.col_cnt, s.col_merged, s.col_rms, D, ow, has_ret, mst, s.col_defer != 0);
     }
   }
   if (s.col_ctrl && blockIdx.x == 0 && lane == 0) s.col_ctrl[0] += 1;  // the stream's next launch sees it
@@ -2048,6 +2058,7 @@ struct fw_handle {
   fw_collect_epilogue col{};  // fw_set_collect_epilogue (all null: off)
   size_t o_colws = 0, o_colcnt = 0;  // in-launch merge tree workspace (records above level 0, counters)
   size_t colcnt_bytes = 0;           // bytes of the tree's arrival counters (zeroed again by clear_tree)
+  size_t o_colshadow = 0;            // the statistics as a deferring env step found them (fw_collect_pending)
   bool tree_dirty = false;           // an env step with the tree failed: counters may hold stale arrivals
   uint32_t gring_mask = 127u;        // goal-history ring entries - 1 (a power of two >= 128, >= success_streak_req)
   int goal_rows = 18;                // GB_* rows (18 + ring words beyond 16 + a second count word when wide)
@@ -2237,6 +2248,7 @@ void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
       d.tgt_phi[k] = (T)e.target_period_high[k];
     }
     d.tprops = d.tprops && h->o_tpr;
+    d.tape_skip = e.tape_skip > 0 ? e.tape_skip : 0;
     d.goal_flag = h->o_gflag != 0;
     d.streak_frac = (T)e.streak_frac;
     d.step_fail_value = (T)e.step_fail_value;
@@ -2489,6 +2501,8 @@ State<T> state_of(const fw_handle* h) {
   s.col_rms = h->col.rms;
   s.col_lvl = h->o_colws ? (double*)(b + h->o_colws) : nullptr;
   s.col_cnt = h->o_colws ? (uint32_t*)(b + h->o_colcnt) : nullptr;
+  s.col_defer = h->col.defer;
+  s.col_shadow = h->o_colshadow ? (double*)(b + h->o_colshadow) : nullptr;
   return s;
 }
 
@@ -2672,6 +2686,8 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
     h->o_colws = off; off += align_up((size_t)mr * (1 + 2 * COL_MAXD) * sizeof(double), 256);
     h->o_colcnt = off; off += align_up((size_t)mc * sizeof(uint32_t), 256);  // zeroed below, reset by the tree
     h->colcnt_bytes = (size_t)mc * sizeof(uint32_t);
+    // the statistics a deferring launch found (fw_collect_pending.rms_prev)
+    h->o_colshadow = off; off += align_up((size_t)(2 * COL_MAXD + 4) * sizeof(double), 256);
   }
   // rows are ld elements apart: the padding above is folded into ld for simplicity
   h->base_bytes = off;
@@ -2931,6 +2947,8 @@ int fw_set_collect_epilogue(fw_handle* h, const fw_collect_epilogue* epi) {
   if (epi->merged && !epi->records)
     return set_err(FW_E_INVALID, "fw_set_collect_epilogue: merged needs the records buffer (the tree's level 0)");
   if (epi->rms && !epi->merged) return set_err(FW_E_INVALID, "fw_set_collect_epilogue: rms needs merged");
+  if (epi->defer && !epi->rms)
+    return set_err(FW_E_INVALID, "fw_set_collect_epilogue: defer needs rms (the statistics the deferred merge updates)");
   h->col = *epi;
   if (epi->merged && h->tree_dirty) {  // no arrival left over from a failed launch
     FW_HIP(hipSetDevice(h->device));
@@ -2938,6 +2956,39 @@ int fw_set_collect_epilogue(fw_handle* h, const fw_collect_epilogue* epi) {
     FW_HIP(hipMemset((char*)h->base + h->o_colcnt, 0, h->colcnt_bytes));
     h->tree_dirty = false;
   }
+  return FW_OK;
+}
+
+int fw_collect_pending(const fw_handle* h, fw_collect_pend* p) {
+  if (!h || !p) return set_err(FW_E_INVALID, "fw_collect_pending: NULL argument");
+  if (!h->has_env || !h->o_colws) return set_err(FW_E_INVALID, "fw_collect_pending: handle has no env");
+  if (!h->col.records || !h->col.merged || !h->col.defer)
+    return set_err(FW_E_INVALID, "fw_collect_pending: no deferred merge tree (fw_set_collect_epilogue with defer)");
+  // the level the tree stops at (collect_merge): level 0 = the caller's records when the launch has at most
+  // MERGE_FANIN blocks, else the first level of the handle's workspace with at most MERGE_FANIN nodes
+  const int64_t blocks = (h->n * lanes_of(h) + BLOCK - 1) / BLOCK;
+  char* const b = (char*)h->base;
+  if (blocks <= fw_stats::MERGE_FANIN) {
+    p->records = h->col.records;
+    p->stride = blocks;
+    p->count = (int32_t)blocks;
+  } else {
+    double* lvl = (double*)(b + h->o_colws);
+    int64_t nodes = blocks;
+    while (true) {
+      const int64_t up = fw_stats::merge_ceil(nodes, fw_stats::MERGE_FANIN);
+      if (up <= fw_stats::MERGE_FANIN) {
+        p->records = lvl;
+        p->stride = up;
+        p->count = (int32_t)up;
+        break;
+      }
+      lvl += up * (1 + 2 * COL_MAXD);
+      nodes = up;
+    }
+  }
+  p->D = h->env.n_obs * std::max(h->env.obs_length, 1) + (h->col.ret ? 1 : 0);
+  p->rms_prev = (const double*)(b + h->o_colshadow);
   return FW_OK;
 }
 

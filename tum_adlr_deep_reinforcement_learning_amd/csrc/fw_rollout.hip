@@ -403,6 +403,35 @@ __global__ __launch_bounds__(MERGE16_THREADS) void k_merge_update16(const double
   rms_update(rec, 1, d, has_ret, rms, 1, 1, old_count);
 }
 
+// The env step's deferred final merge (fw_collect_epilogue.defer) on its own: one wave, lane j < D owns column
+// j; the same functions (fw_stats::merge_col / update_col) as k_policy_mfma's prologue and the same bits as the
+// in-launch final node + rms_update.
+__global__ __launch_bounds__(64) void k_pending_update(const double* __restrict__ pend, int64_t stride, int cnt, int d,
+                                                       int has_ret, double* __restrict__ rms, double* __restrict__ merged) {
+  const int j = threadIdx.x, D = d + has_ret;
+  const double c_obs = rms[2 * d], c_ret = rms[2 * d + 3];
+  const bool is_ret = has_ret && j == d;
+  double N = 0.0, mu = 0.0, m2 = 0.0, mean = 0.0, var = 0.0;
+  if (j < D) {
+    fw_stats::merge_col(pend, pend + (1 + j) * stride, pend + (1 + D + j) * stride, cnt, N, mu, m2);
+    mean = rms[is_ret ? 2 * d + 1 : j];
+    var = rms[is_ret ? 2 * d + 2 : d + j];
+    fw_stats::update_col(mu, m2 / N, N, is_ret ? c_ret : c_obs, mean, var);
+  }
+  __syncthreads();  // (every lane read the counts before lane 0 / the return lane rewrites them)
+  if (j < D) {
+    rms[is_ret ? 2 * d + 1 : j] = mean;
+    rms[is_ret ? 2 * d + 2 : d + j] = var;
+    if (j == 0) rms[2 * d] = N + c_obs;
+    if (is_ret) rms[2 * d + 3] = N + c_ret;
+    if (merged) {
+      if (j == 0) merged[0] = N;
+      merged[1 + j] = mu;
+      merged[1 + D + j] = m2;
+    }
+  }
+}
+
 // k_moments_merge + k_rms_update of the single merged record in one launch (the unsharded statistics
 // update of a collect step): the same device functions, so the same bits as the two launches.
 __global__ __launch_bounds__(MERGE_THREADS) void k_merge_update(const double* __restrict__ part, int parts, int d,
@@ -521,6 +550,8 @@ __global__ void k_row_advance(int32_t* ctrl) { ctrl[0] += 1; }
 // wave with packed input pairs 94; two envs per lane 100 (register-bound).
 // ---------------------------------------------------------------------------
 constexpr int POL_MAXD = 32, POL_MAXH = 64, POL_MAXA = 8;
+// fields x records of a deferred final merge a k_policy_mfma block stages in LDS (fw_collect_io.pend)
+constexpr int PEND_MAX = 2048;
 constexpr int POL_BLOCK = 256;  // 128 envs per tile
 constexpr int POL_BLOCKS_PER_CU = 2;
 #ifndef FW_POL_ROWPF
@@ -722,6 +753,13 @@ struct PolArgs {
   float *obs_rows, *act, *val, *logp, *rew_rows;
   uint8_t* start_rows;
   int64_t n;
+  // the env step's deferred final merge (fw_collect_io.pend, ABI 12), or pend null
+  const double* pend;
+  int64_t pend_stride;
+  int pend_cnt, has_ret;
+  double* rms_w;     // = rms, written by block 0
+  double* merged;    // [1 + 2D] or null
+  const double* rms_prev;  // the statistics before the update (the env step's copy)
 };
 
 #ifndef FW_POL_VHEADS
@@ -768,7 +806,11 @@ __device__ __forceinline__ float norm_obs_val(float o, double mean, double den, 
 template <int S>
 struct PolLds {
   static constexpr int L1 = 0, L0 = L1 + 2 * 4 * 4 * 64 * 4, HD = L0 + 2 * 4 * 64 * S, B = HD + 2 * 4 * 64 * 4,
-                       BH = B + 2 * 2 * 4 * 16, NRM = BH + 16, HV = NRM + 2 * 2 * 4 * S, FLOATS = HV + 4 * 5 * 16;
+                       BH = B + 2 * 2 * 4 * 16, NRM = BH + 16, HV = NRM + 2 * 2 * 4 * S, RV = HV + 4 * 5 * 16,
+                       PO = RV + 2, FLOATS = PO + 2 * (2 * POL_MAXD + 4 + 1 + 2 * (POL_MAXD + 1));
+  // RV: the return variance (double) and PO: the updated statistics [2d + 4] then the merged record [1 + 2D]
+  // (doubles) of the deferred final merge (PolArgs.pend); its records are staged past FLOATS (dynamic LDS)
+  static_assert(RV % 2 == 0 && FLOATS % 2 == 0, "RV / PO hold doubles");
   // HV: the heads for the VALU form (FW_POL_VHEADS): [g][row][16] with rows 0..3 = actor rows (0 past act_dim),
   // row 4 = the critic; entry 4 T + v of lane group g = hidden unit 16 T + 4 g + v (the layer-1 B-operand slot)
   // NRM: the VecNormalize mean and sqrt(var + eps) of features 0 .. 4 S - 1 as doubles (8-wave blocks read
@@ -905,7 +947,30 @@ __global__ __launch_bounds__(64 * PM_WAVES, PM_WAVES / 2) void k_policy_mfma(Pol
       }
     }
   }
-  const double rden = nrew ? sqrt(rvar + G.eps) : 1.0;
+  // the env step's deferred final merge (fw_collect_epilogue.defer): from row 1 on, the statistics this launch
+  // normalises with are the ones the previous env step's records update (stream order: they are complete)
+  const bool pend = G.pend != nullptr && G.ctrl != nullptr && row >= 1;
+  double* const PD = reinterpret_cast<double*>(Wl + L::FLOATS);
+  // staged: the records (field f of record k at PD[f * cnt + k]), then the statistics before the update
+  const int pcnt = pend ? (1 + 2 * (d + G.has_ret)) * G.pend_cnt : 0, ptot = pend ? pcnt + 2 * d + 4 : 0;
+  auto pend_at = [&](int e) {
+    return e < pcnt ? G.pend[(int64_t)(e / G.pend_cnt) * G.pend_stride + e % G.pend_cnt] : G.rms_prev[e - pcnt];
+  };
+  // 8-wave blocks: the upper half of the block (idle in the weight fill) stages them, two loads in flight per
+  // lane, before its (empty) part of the fill; 4-wave blocks: one element per thread in flight under the fill
+  constexpr int NT = 64 * PM_WAVES;
+  double sv = 0.0;
+  if constexpr (NT > 256) {
+    if (pend && threadIdx.x >= 256) {
+      for (int e = (int)threadIdx.x - 256; e < ptot; e += 512) {
+        const double a = pend_at(e), b = e + 256 < ptot ? pend_at(e + 256) : 0.0;
+        PD[e] = a;
+        if (e + 256 < ptot) PD[e + 256] = b;
+      }
+    }
+  } else {
+    if (pend) sv = pend_at((int)threadIdx.x < ptot ? (int)threadIdx.x : 0);  // (in flight under the weight fill)
+  }
   float* obs_rows = G.obs_rows ? G.obs_rows + row * n * d : nullptr;
   float* act = G.act + row * n * A;
   float* val = G.val + row * n;
@@ -984,6 +1049,69 @@ __global__ __launch_bounds__(64 * PM_WAVES, PM_WAVES / 2) void k_policy_mfma(Pol
   for (int p = 0; p < PT; p++) fetch(wid * PT + p, nxt[p]);
   // the block's weight image after the first tiles' loads are issued (their latency hides under the fill)
   if (FW_POL_DIAG != 3) pol_fill_lds<S, PM_WAVES>(G.P, Wl);
+  if (pend) {
+    if constexpr (NT <= 256) {
+      if ((int)threadIdx.x < ptot) PD[threadIdx.x] = sv;
+      for (int e = (int)threadIdx.x + NT; e < ptot; e += NT) PD[e] = pend_at(e);
+      __syncthreads();
+    }  // (8-wave blocks: staged before the fill's closing barrier)
+    double* const po = reinterpret_cast<double*>(Wl + L::PO);
+    double* const nl = reinterpret_cast<double*>(Wl + L::NRM);
+    double* const rv = reinterpret_cast<double*>(Wl + L::RV);
+    if (threadIdx.x < 64) {
+      // every block computes the same bits; block 0 writes them back (the other blocks read the env step's copy
+      // of the old statistics, so the write cannot race their reads; a ticket on one counter from 512 blocks
+      // serialised on its address: +5 us per launch, profiles/r06_collect_ab.log)
+      const int j = lane, D = d + G.has_ret, nr = 2 * d + 4, cnt = G.pend_cnt;
+      const double* ro = PD + pcnt;  // the statistics before the update
+      for (int e = j; e < nr; e += 64) po[e] = ro[e];  // (what the update leaves alone: no return column)
+      const double c_obs = ro[2 * d], r_m = ro[2 * d + 1], r_v = ro[2 * d + 2], c_ret = ro[2 * d + 3];
+      const double o_m = ro[j < d ? j : 0], o_v = ro[d + (j < d ? j : 0)];
+      double rvar_new = r_v;
+      if (j < D) {
+        double N, mu, m2;
+        fw_stats::merge_col(PD, PD + (1 + j) * cnt, PD + (1 + D + j) * cnt, cnt, N, mu, m2);
+        const bool is_ret = G.has_ret && j == d;
+        double mean = is_ret ? r_m : o_m, var = is_ret ? r_v : o_v;
+        fw_stats::update_col(mu, m2 / N, N, is_ret ? c_ret : c_obs, mean, var);
+        po[is_ret ? 2 * d + 1 : j] = mean;
+        po[is_ret ? 2 * d + 2 : d + j] = var;
+        if (j == 0) po[2 * d] = N + c_obs;
+        if (is_ret) po[2 * d + 3] = N + c_ret;
+        double* mg = po + nr;
+        if (j == 0) mg[0] = N;
+        mg[1 + j] = mu;
+        mg[1 + D + j] = m2;
+        if (j < 4 * S) {
+          const bool on = nobs && j < d;
+          nl[j] = on ? mean : 0.0;
+          nl[4 * S + j] = on ? sqrt(var + G.eps) : 1.0;
+        }
+        if (is_ret) rvar_new = var;
+      } else if (j < 4 * S) {
+        nl[j] = 0.0;
+        nl[4 * S + j] = 1.0;
+      }
+      if (j == (G.has_ret ? d : 0)) rv[0] = rvar_new;
+      if (blockIdx.x == 0) {
+        asm volatile("" ::: "memory");  // (po's stores above are this wave's own: LDS completes them in order)
+        const int nm = 1 + 2 * D;
+        for (int e = lane; e < nr; e += 64) G.rms_w[e] = po[e];
+        if (G.merged)
+          for (int e = lane; e < nm; e += 64) G.merged[e] = po[nr + e];
+      }
+    }
+    __syncthreads();
+    if constexpr (!NRM_LDS) {
+#pragma unroll
+      for (int s = 0; s < S; s++) {
+        mean[s] = nl[4 * s + g];
+        den[s] = nl[4 * S + 4 * s + g];
+      }
+    }
+    rvar = rv[0];
+  }
+  const double rden = nrew ? sqrt(rvar + G.eps) : 1.0;
 #if FW_POL_STAGGER
   // A/B (tools/r05_pol.sh): the CU's second block starts FW_POL_STAGGER x 64 cycles late, so its waves' tanh
   // phases meet their SIMD partners' MFMA phases instead of running in lockstep with them
@@ -1270,13 +1398,16 @@ int launch_mfma(const PolArgs& G, hipStream_t s) {
   const int64_t groups = (tiles + FW_POL_TILES - 1) / FW_POL_TILES;
   const unsigned grid = (unsigned)std::max<int64_t>(
       1, std::min<int64_t>((groups + waves - 1) / waves, (int64_t)cus * std::max(per_cu, 1)));
+  // (+ the deferred merge's records and the statistics before the update, staged per block)
+  const size_t pst =
+      G.pend ? ((size_t)(1 + 2 * (G.P.d + G.has_ret)) * G.pend_cnt + 2 * G.P.d + 4) * sizeof(double) : 0;
   if (small)
     hipLaunchKernelGGL((k_policy_mfma<4, 4, FW_POL_WAVES>), dim3(grid), dim3(64 * FW_POL_WAVES),
-                       PolLds<4>::FLOATS * sizeof(float), s, G);
+                       PolLds<4>::FLOATS * sizeof(float) + pst, s, G);
   else if (G.P.d <= 16)
-    hipLaunchKernelGGL((k_policy_mfma<4, POL_MAXA, 4>), dim3(grid), dim3(256), PolLds<4>::FLOATS * sizeof(float), s, G);
+    hipLaunchKernelGGL((k_policy_mfma<4, POL_MAXA, 4>), dim3(grid), dim3(256), PolLds<4>::FLOATS * sizeof(float) + pst, s, G);
   else
-    hipLaunchKernelGGL((k_policy_mfma<8, POL_MAXA, 4>), dim3(grid), dim3(256), PolLds<8>::FLOATS * sizeof(float), s, G);
+    hipLaunchKernelGGL((k_policy_mfma<8, POL_MAXA, 4>), dim3(grid), dim3(256), PolLds<8>::FLOATS * sizeof(float) + pst, s, G);
   FW_HIP(hipGetLastError());
   return FW_OK;
 }
@@ -1508,7 +1639,32 @@ int fw_collect_policy(const fw_mlp_policy* p, const fw_collect_io* io, void* str
   G.rew_rows = io->rew_rows;
   G.start_rows = io->start_rows;
   G.n = io->n;
+  if (io->pend) {
+    const int D = p->d + (io->has_ret ? 1 : 0);
+    if (!io->rms || !io->rms_prev || io->pend_cnt < 1 || io->pend_cnt > 64 || io->pend_stride < io->pend_cnt ||
+        (1 + 2 * D) * io->pend_cnt > PEND_MAX)
+      return fw::set_error(FW_E_INVALID, "fw_collect_policy: pend needs rms, rms_prev and 1..64 records of at most "
+                                         "PEND_MAX fields in all");
+    G.pend = io->pend;
+    G.pend_stride = io->pend_stride;
+    G.pend_cnt = io->pend_cnt;
+    G.has_ret = io->has_ret ? 1 : 0;
+    G.rms_w = const_cast<double*>(io->rms);
+    G.merged = io->merged;
+    G.rms_prev = io->rms_prev;
+  }
   return launch_mfma(G, (hipStream_t)stream);
+}
+
+int fw_vecnorm_pending_update(const double* pend, int64_t stride, int32_t cnt, int32_t d, int32_t has_ret,
+                              double* rms, double* merged, void* stream) {
+  if (!pend || !rms || cnt < 1 || cnt > 64 || stride < cnt || d < 0 || d + (has_ret ? 1 : 0) < 1 ||
+      d + (has_ret ? 1 : 0) > 64)
+    return fw::set_error(FW_E_INVALID, "fw_vecnorm_pending_update: bad arguments");
+  hipLaunchKernelGGL(k_pending_update, dim3(1), dim3(64), 0, (hipStream_t)stream, pend, stride, (int)cnt, (int)d,
+                     (int)(has_ret != 0), rms, merged);
+  FW_HIP(hipGetLastError());
+  return FW_OK;
 }
 
 }  // extern "C"

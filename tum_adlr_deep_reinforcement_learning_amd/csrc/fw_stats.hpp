@@ -29,6 +29,76 @@ __device__ __forceinline__ Mom chan(Mom a, Mom b) {
   return r;
 }
 
+// update_from_moments of one column (running_mean_std.py:26-40, same operation order): the batch's mean, var
+// and count folded into (mean, var) that held `count` samples.  Shared by rms_update and the deferred final
+// merge (fw_rollout.hip k_policy_mfma / k_pending_update), so every path produces the same bits.
+__device__ __forceinline__ void update_col(double bmean, double bvar, double bc, double count, double& mean,
+                                           double& var) {
+#pragma clang fp contract(off)
+  const double delta = bmean - mean;
+  const double tot = count + bc;
+  const double new_mean = mean + delta * bc / tot;
+  const double m_a = var * count;
+  const double m_b = bvar * bc;
+  const double m_2 = m_a + m_b + delta * delta * count * bc / (count + bc);
+  mean = new_mean;
+  var = m_2 / (count + bc);
+}
+
+// The final node of the in-launch merge tree for one column, computed by one lane from the node's cnt records
+// (record k's n / mean_j / M2_j at nrow[k] / mrow[k] / qrow[k]): N = sum n_k, mean = (sum n_k mean_k) / N,
+// M2 = sum (M2_k + n_k (mean_k - mean)^2), every sum in record order -- the arithmetic of fw_kernels.hip
+// merge_node, whose 64-slot row sums add +0.0 for absent records (which leaves these sums unchanged), so the
+// bits are the same.
+__device__ __forceinline__ void merge_col(const double* nrow, const double* mrow, const double* qrow, int cnt,
+                                          double& N, double& mean, double& m2) {
+#pragma clang fp contract(off)
+  // (reads in batches of 8, issued together; the sums stay in record order)
+  constexpr int B = 8;
+  double a = 0.0, s = 0.0;
+  int k = 0;
+  for (; k + B <= cnt; k += B) {
+    double nv[B], mv[B];
+#pragma unroll
+    for (int u = 0; u < B; u++) {
+      nv[u] = nrow[k + u];
+      mv[u] = mrow[k + u];
+    }
+#pragma unroll
+    for (int u = 0; u < B; u++) {
+      a += nv[u];
+      s += nv[u] * mv[u];
+    }
+  }
+  for (; k < cnt; k++) {
+    a += nrow[k];
+    s += nrow[k] * mrow[k];
+  }
+  N = a;
+  mean = s / a;
+  double q = 0.0;
+  k = 0;
+  for (; k + B <= cnt; k += B) {
+    double nv[B], mv[B], qv[B];
+#pragma unroll
+    for (int u = 0; u < B; u++) {
+      nv[u] = nrow[k + u];
+      mv[u] = mrow[k + u];
+      qv[u] = qrow[k + u];
+    }
+#pragma unroll
+    for (int u = 0; u < B; u++) {
+      const double dm = mv[u] - mean;
+      q += qv[u] + nv[u] * (dm * dm);
+    }
+  }
+  for (; k < cnt; k++) {
+    const double dm = mrow[k] - mean;
+    q += qrow[k] + nrow[k] * (dm * dm);
+  }
+  m2 = q;
+}
+
 // RunningMeanStd.update_from_moments (running_mean_std.py:26-40, same operation order) over n_parts records
 // (contiguous, 1 + 2D each: n, mean[D], M2[D]; D = d + has_ret) merged in order; rms = [mean d | var d |
 // count | ret mean | ret var | ret count].  Thread j < D owns column j.  Every thread of the block calls
@@ -54,15 +124,10 @@ __device__ __forceinline__ void rms_update(const double* __restrict__ parts, int
       double* mean_p = is_ret ? rms + 2 * d + 1 : rms + j;
       double* var_p = is_ret ? rms + 2 * d + 2 : rms + d + j;
       const double count = old_count[is_ret ? 1 : 0];
-      const double mean = *mean_p, var = *var_p;
-      const double delta = bmean - mean;
-      const double tot = count + bc;
-      const double new_mean = mean + delta * bc / tot;
-      const double m_a = var * count;
-      const double m_b = bvar * bc;
-      const double m_2 = m_a + m_b + delta * delta * count * bc / (count + bc);
-      *mean_p = new_mean;
-      *var_p = m_2 / (count + bc);
+      double mean = *mean_p, var = *var_p;
+      update_col(bmean, bvar, bc, count, mean, var);
+      *mean_p = mean;
+      *var_p = var;
       if (j == (is_ret ? d : 0)) {
         if (is_ret)
           rms[2 * d + 3] = bc + count;

@@ -274,14 +274,17 @@ class Engine:
         _native.check(self.lib.fw_observe(self.h, _ptr(self.obs), self.stream()), "fw_observe")
         return self.obs
 
-    def set_collect_epilogue(self, ret=None, gamma=0.0, records=None, row_ctrl=None, merged=None, rms=None):
+    def set_collect_epilogue(self, ret=None, gamma=0.0, records=None, row_ctrl=None, merged=None, rms=None,
+                             defer=False):
         """fw_set_collect_epilogue: every following ``env_step`` also updates VecNormalize's discounted return
         ``ret`` (fp64 [n]: ret*gamma + reward, then 0 where done) and writes one moment record per launch block
         of (observation, ret) into ``records`` (fp64, ``collect_records()[1]`` x (1 + 2 D) rows); ``row_ctrl``
         (int32 device tensor) gets ``[0] += 1`` per launch.  ``merged`` (fp64 [1 + 2 D]): the launch merges its
         block records itself (in-launch tree) into that record; ``rms`` (the fw_rms_update buffer, with
-        ``merged``): it also applies update_from_moments.  All None turns it off.  A captured step keeps the
-        setting it was captured with."""
+        ``merged``): it also applies update_from_moments.  ``defer`` (ABI 12, with ``merged``): the launch stops
+        the tree one level short and leaves that level (``collect_pending()``) to the next fw_collect_policy or
+        to fw_vecnorm_pending_update.  All None turns it off.  A captured step keeps the setting it was
+        captured with."""
         if ret is None and records is None and row_ctrl is None:
             _native.check(self.lib.fw_set_collect_epilogue(self.h, None), "fw_set_collect_epilogue")
             self._collect = None
@@ -301,9 +304,17 @@ class Engine:
         if rms is not None and rms.numel() < 2 * self.n_obs_values + 4:
             raise ValueError("set_collect_epilogue: rms must hold 2 d + 4 values")
         ptr = (lambda t: t.data_ptr() if t is not None else None)
-        e = _native.FwCollectEpilogue(ptr(ret), float(gamma), ptr(records), ptr(row_ctrl), ptr(merged), ptr(rms))
+        e = _native.FwCollectEpilogue(ptr(ret), float(gamma), ptr(records), ptr(row_ctrl), ptr(merged), ptr(rms),
+                                      int(bool(defer)), 0)
         _native.check(self.lib.fw_set_collect_epilogue(self.h, ctypes.byref(e)), "fw_set_collect_epilogue")
         self._collect = (ret, records, row_ctrl, merged, rms)  # keep the buffers alive while the handle writes them
+
+    def collect_pending(self):
+        """fw_collect_pending: where the next env_step leaves its deferred final merge level --
+        (records pointer, stride, count, D, the statistics' copy the next policy launch reads)."""
+        p = _native.FwCollectPend()
+        _native.check(self.lib.fw_collect_pending(self.h, ctypes.byref(p)), "fw_collect_pending")
+        return p.records, p.stride, p.count, p.D, p.rms_prev
 
     def collect_records(self):
         """(records the next env_step writes, the most any lanes setting writes)."""

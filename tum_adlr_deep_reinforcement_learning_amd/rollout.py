@@ -18,6 +18,7 @@ episode starts live outside the slab (inputs of the scan, not of the update).
 """
 import collections
 import ctypes
+import os
 import warnings
 
 import numpy as np
@@ -270,6 +271,10 @@ class MlpActorCritic(nn.Module):
 class RolloutCollector:
     capture_collective = True  # a sharded fused step captures its RCCL exchange inside the one graph
     steps_per_graph = 16       # the fused step is also captured K times in one graph (one replay per K steps)
+    # round 6: the env step leaves its VecNormalize merge's final level to the next step's policy launch (every
+    # policy block merges it under its weight fill; fwsim.h fw_collect_epilogue.defer), off the env step's tail;
+    # the collection's last level is applied by fw_vecnorm_pending_update.  Same bits either way.
+    defer_final_merge = os.environ.get("FW_DEFER_FINAL_MERGE", "1") != "0"  # (A/B: tools/r06_collect_ab.sh)
 
     """OnPolicyAlgorithm.collect_rollouts (on_policy_algorithm.py:126-190) with everything on the device.
 
@@ -376,7 +381,7 @@ class RolloutCollector:
         pol_key = (id(pol), bool(getattr(pol, "deterministic_rollout", False)),
                    tuple(p.data_ptr() for p in pol.parameters()) if isinstance(pol, nn.Module) else None)
         return (env_key, self._split(), self.buffer.slab.data_ptr(), self.buffer.buffer_size, pol_key,
-                self.capture_collective, self.steps_per_graph)
+                self.capture_collective, self.steps_per_graph, self.defer_final_merge)
 
     def _capture(self):
         """Capture one collect step on static tensors: s_obs (the observation the policy acts on, then
@@ -613,8 +618,18 @@ class RolloutCollector:
             if self._graphK is not None:
                 self._graphK.instantiate()
 
+        self._deferred = None  # the deferred level's fields (fw_collect_pending) when the step defers
         if vn is not None:
-            vn.set_epilogue(row_ctrl=self._ctrl)
+            vn.set_epilogue(row_ctrl=self._ctrl, defer=self.defer_final_merge and not grouped)
+            pf = vn.pending_fields()
+            if pf is not None and (1 + 2 * (buf.obs_dim + 1)) * pf[2] > vn.PEND_MAX:  # too big to stage: no deferral
+                vn.set_epilogue(row_ctrl=self._ctrl)
+                pf = None
+            if pf is not None:
+                io.pend, io.pend_stride, io.pend_cnt, io.has_ret, io.merged, io.rms_prev = pf
+                self._deferred = vn._pend
+            else:
+                io.pend = None
         else:
             eng.set_collect_epilogue(row_ctrl=self._ctrl)
         self.capture_error = None
@@ -698,6 +713,8 @@ class RolloutCollector:
         # the last step's reward row and the VecNormalize outputs of the last step (its obs_out is the
         # policy input of the next collection)
         if vn is not None:
+            if self._deferred is not None:  # the last env step's final merge level (no policy launch follows it)
+                vn.pending_update(self._deferred)
             vn._apply(eng.obs, eng.reward, None)
             vn.old_obs, vn.old_reward = eng.obs, eng.reward
             buf.rewards[n - 1].copy_(vn.rew_out)

@@ -259,17 +259,38 @@ class VecNormalize:
     # update) as a separate launch after the env step (fw_vecnorm_merge_update / fw_moments_merge)
     merge_in_launch = True
 
-    def set_epilogue(self, row_ctrl=None):
+    def set_epilogue(self, row_ctrl=None, defer=False):
         """Point the engine's collect epilogue at this wrapper's return and record buffers (and, for a
         captured collect step, the rollout row counter).  With ``merge_in_launch`` the launch also writes the
-        merged record into ``_rec`` and, without an exchange, applies it to ``rms``."""
+        merged record into ``_rec`` and, without an exchange, applies it to ``rms``.  ``defer`` (unsharded,
+        with ``merge_in_launch``): the launch stops the merge one level short; the fused collect's next policy
+        launch finishes it (``pending_fields``), or ``pending_update`` does."""
         eng = self.venv.engine
         self._ensure_parts()
         merged = self._rec if self.merge_in_launch else None
         rms = self.rms if (self.merge_in_launch and not self.exchanged()) else None
+        defer = bool(defer and rms is not None)
         eng.set_collect_epilogue(ret=self.ret, gamma=self.gamma, records=self._records, row_ctrl=row_ctrl,
-                                 merged=merged, rms=rms)
+                                 merged=merged, rms=rms, defer=defer)
         self._n_rec = eng.collect_records()[0]
+        self._pend = eng.collect_pending() if defer else None
+
+    # the deferred final level fits one policy block's LDS staging (fw_rollout.hip PEND_MAX fields x records)
+    PEND_MAX = 2048
+
+    def pending_fields(self):
+        """(pend, stride, count, has_ret, merged, rms_prev) for fw_collect_io, or None when the epilogue set by
+        ``set_epilogue`` does not defer."""
+        if getattr(self, "_pend", None) is None:
+            return None
+        rec, stride, cnt, D, rms_prev = self._pend
+        return rec, stride, cnt, 1, self._rec.data_ptr(), rms_prev
+
+    def pending_update(self, pend=None):
+        """fw_vecnorm_pending_update: apply a deferred final merge (after a collection's last env step)."""
+        rec, stride, cnt, D, _ = pend if pend is not None else self._pend
+        _native.check(self.lib.fw_vecnorm_pending_update(rec, stride, cnt, self.obs_dim, 1, _p(self.rms),
+                                                         _p(self._rec), self._s()), "fw_vecnorm_pending_update")
 
     def merge_records(self, out):
         """fw_moments_merge of the env step's block records into one (obs + return) record."""
