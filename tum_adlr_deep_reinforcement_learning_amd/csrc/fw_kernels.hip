@@ -150,9 +150,10 @@ struct State {
   double* col_merged; // [1 + 2 D] the launch's merged record (in-launch merge tree), or null: merged later
   double* col_rms;    // RunningMeanStd buffer update_from_moments is applied to (with col_merged), or null
   double* col_lvl;    // merge-tree records above level 0 (handle workspace, fw_stats::merge_tree_size)
-  uint32_t* col_cnt;  // merge-tree arrival counters (handle workspace, zero between launches)
-  int32_t col_defer;  // 1: the tree stops one level short (the next fw_collect_policy merges the last level)
-  double* col_shadow; // (col_defer) copy of col_rms as the launch found it, what the merging policy launch reads
+  // merge-tree arrival counters (handle workspace, zero between launches); bit 0 of the address set: the tree
+  // stops one level short (fw_collect_epilogue.defer; a flag bit, not a field: a larger State costs the quad
+  // instances 64 B of scratch)
+  uint32_t* col_cnt;
 };
 
 // streaming episode-metric state (fixed_wing.py:1644-1736 restated over running sums), packed (round 5):
@@ -1673,6 +1674,9 @@ constexpr int MN_COLS = 16;  // columns staged per LDS pass of merge_node
 constexpr int MN_LD = 66;    // staging row stride (doubles): lane j reads row j with 16-B loads, 4 banks apart
 // LDS staging of merge_node: MN_COLS + 1 rows x 64 records, the column means, update_from_moments' counts
 constexpr size_t MN_BYTES = ((MN_COLS + 1) * MN_LD + COL_MAXD + 2) * sizeof(double);
+// the handle's copy of the statistics a deferring env step found (fw_collect_pending.rms_prev): right below the
+// merge tree's level records (State::col_lvl)
+constexpr size_t COL_SHADOW_BYTES = ((2 * COL_MAXD + 4) * sizeof(double) + 255) / 256 * 256;
 
 // sum of row[0 .. 64) in index order (row 16-B aligned): all loads issued first.  The slots of absent
 // records hold +0.0, and adding +0.0 leaves any partial sum that can occur here unchanged (it starts at
@@ -1835,8 +1839,11 @@ __device__ __forceinline__ void collect_epilogue(const State<T>& s, int64_t i, b
     ret = g + (double)(float)rew_out[i];
     s.col_ret[i] = done_out[i] ? 0.0 : ret;
   }
-  if (s.col_defer && blockIdx.x == 0)  // the statistics the next policy launch updates (its blocks read this copy,
-    for (int e = lane; e < 2 * ow + 4; e += 64) s.col_shadow[e] = s.col_rms[e];  // while its block 0 rewrites col_rms)
+  const bool defer = ((uintptr_t)s.col_cnt & 1u) != 0;  // (fw_collect_epilogue.defer)
+  if (defer && blockIdx.x == 0) {  // the statistics the next policy launch updates (its blocks read this copy
+    double* shadow = (double*)((char*)s.col_lvl - COL_SHADOW_BYTES);  // while its block 0 rewrites col_rms)
+    for (int e = lane; e < 2 * ow + 4; e += 64) shadow[e] = s.col_rms[e];
+  }
   if (s.col_rec) {
     const int D = ow + (has_ret ? 1 : 0);
     const bool tree = s.col_merged != nullptr;
@@ -1892,7 +1899,8 @@ __device__ __forceinline__ void collect_epilogue(const State<T>& s, int64_t i, b
     }
     if (tree) {
       __syncthreads();  // (the staging area is reused by the merge)
-      collect_merge(s.col_rec, s.col_lvl, s.col_cnt, s.col_merged, s.col_rms, D, ow, has_ret, mst, s.col_defer != 0);
+      collect_merge(s.col_rec, s.col_lvl, (uint32_t*)((uintptr_t)s.col_cnt & ~(uintptr_t)1), s.col_merged, s.col_rms, D,
+                    ow, has_ret, mst, defer);
     }
   }
   if (s.col_ctrl && blockIdx.x == 0 && lane == 0) s.col_ctrl[0] += 1;  // the stream's next launch sees it
@@ -2500,9 +2508,7 @@ State<T> state_of(const fw_handle* h) {
   s.col_merged = h->col.merged;
   s.col_rms = h->col.rms;
   s.col_lvl = h->o_colws ? (double*)(b + h->o_colws) : nullptr;
-  s.col_cnt = h->o_colws ? (uint32_t*)(b + h->o_colcnt) : nullptr;
-  s.col_defer = h->col.defer;
-  s.col_shadow = h->o_colshadow ? (double*)(b + h->o_colshadow) : nullptr;
+  s.col_cnt = h->o_colws ? (uint32_t*)(b + h->o_colcnt + (h->col.defer ? 1 : 0)) : nullptr;
   return s;
 }
 
@@ -2683,11 +2689,11 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
   if (env) {  // the collect epilogue's in-launch merge tree (fw_collect_epilogue.merged), sized for 4 lanes
     int64_t mr = 0, mc = 0;
     fw_stats::merge_tree_size((h->n * 4 + BLOCK - 1) / BLOCK, &mr, &mc);
+    // the statistics a deferring launch found (fw_collect_pending.rms_prev), right below the tree's records
+    h->o_colshadow = off; off += COL_SHADOW_BYTES;
     h->o_colws = off; off += align_up((size_t)mr * (1 + 2 * COL_MAXD) * sizeof(double), 256);
     h->o_colcnt = off; off += align_up((size_t)mc * sizeof(uint32_t), 256);  // zeroed below, reset by the tree
     h->colcnt_bytes = (size_t)mc * sizeof(uint32_t);
-    // the statistics a deferring launch found (fw_collect_pending.rms_prev)
-    h->o_colshadow = off; off += align_up((size_t)(2 * COL_MAXD + 4) * sizeof(double), 256);
   }
   // rows are ld elements apart: the padding above is folded into ld for simplicity
   h->base_bytes = off;
