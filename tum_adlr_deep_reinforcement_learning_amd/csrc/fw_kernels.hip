@@ -355,6 +355,12 @@ __device__ __forceinline__ void turbulence_at(const DevCfg<T>& c, const State<T>
   dryden(c, k, un1, u0, tl, ta);
 }
 
+// a[k] for a runtime k by selects: a register array indexed at run time would be placed in scratch
+template <typename T>
+__device__ __forceinline__ T pick3(const T* a, int k) {
+  return k == 0 ? a[0] : (k == 1 ? a[1] : a[2]);
+}
+
 // value of an observed / rewarded state variable from the stored state
 template <typename T>
 __device__ __forceinline__ T state_value(int var, const T* y, const T* der) {
@@ -386,10 +392,10 @@ __device__ __forceinline__ T obs_raw(const DevCfg<T>& c, const fw_obs_entry& E, 
     if (E.kind == FW_OBS_STATE) {
       val = state_value(E.var, y, der);
     } else if (E.kind == FW_OBS_TARGET_ABS) {
-      val = tgt[E.var];
+      val = pick3(tgt, E.var);
     } else if (E.kind == FW_OBS_TARGET_REL) {
-      const int tv[3] = {FW_V_ROLL, FW_V_PITCH, FW_V_VA};
-      val = target_error(c, E.var, tgt[E.var], state_value(tv[E.var], y, der));
+      const int tv = E.var == 0 ? FW_V_ROLL : (E.var == 1 ? FW_V_PITCH : FW_V_VA);
+      val = target_error(c, E.var, pick3(tgt, E.var), state_value(tv, y, der));
     } else if (E.kind == FW_OBS_TARGET_INT) {
       val = T(0);  // (written afterwards from the window sums: iw_obs)
     } else {  // action window
@@ -426,11 +432,6 @@ __device__ __forceinline__ T obs_norm(const fw_obs_entry& E, T val) {
 
 // integration_window (State::iws): rows of the window sums
 constexpr int IW_Q = 0, IW_QP = 3, IW_E0 = 6;
-// a[k] for a runtime k by selects: a register array indexed at run time would be placed in scratch
-template <typename T>
-__device__ __forceinline__ T pick3(const T* a, int k) {
-  return k == 0 ? a[0] : (k == 1 ? a[1] : a[2]);
-}
 // the sum plus the padding of an integrator value: s + (W - x) e0 when x < W (fixed_wing.py:1009-1012, 1177-1181)
 template <typename T>
 __device__ __forceinline__ T iw_value(const DevCfg<T>& c, T sum, int x, T e0) {
@@ -657,9 +658,9 @@ __device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* 
         for (int k = 0; k < 3; k++)  // value / len(self.target) per bounded target within its bound
           val += ((gb >> k) & 1u) ? (T)F.value / T(3) : T(0);
       }
-    } else {
-      const int tvv[3] = {FW_V_ROLL, FW_V_PITCH, FW_V_VA};
-      val = target_error(c, F.var, tgt[F.var], state_value(tvv[F.var], y, der));
+    } else {  // (by selects: the factor loop is not unrolled at FW_MAX_REW 12, and tgt[F.var] went to scratch)
+      const int tv_ = F.var == 0 ? FW_V_ROLL : (F.var == 1 ? FW_V_PITCH : FW_V_VA);
+      val = target_error(c, F.var, pick3(tgt, F.var), state_value(tv_, y, der));
     }
     if (F.fun == FW_FUN_LINEAR) {
       val = fabs(val) / scl;
@@ -888,32 +889,30 @@ struct Draws {
       philox(k0, k1, cid, ep, stream, blk++, r);
       used = 0;
     }
-    return u01<T>(r[used++]);
+    // r[used] by selects: where the draw count depends on the configuration (sample_target's class draws) the
+    // index is not a compile-time constant, and an indexed register array is placed in scratch (round 6: 60 B
+    // and ~15 scratch instructions per wave on every step of the fp32 instances)
+    const uint32_t v = used == 0 ? r[0] : (used == 1 ? r[1] : (used == 2 ? r[2] : r[3]));
+    used++;
+    return u01<T>(v);
   }
   __device__ __forceinline__ T uniform(T lo, T hi) { return lo + (hi - lo) * next(); }  // numpy uniform
 };
 
 // The env's own np_random (FixedWingAircraft.np_random, fixed_wing.py:324-332): the caller's tape
-// (fw_set_env_draws: aircraft i's column, from its cursor State::dcur) or a Philox source.
+// (fw_set_env_draws: aircraft i's column, from its cursor `cur`, State::dcur) or the Philox source D.  Free
+// functions on the caller's locals: an object holding references to them placed the Draws (48 B) in scratch.
 template <typename T>
-struct EnvRng {
-  const State<T>& s;
-  int64_t i;
-  Draws<T>& ph;
-  uint32_t cur;
-  __device__ __forceinline__ EnvRng(const State<T>& s_, int64_t i_, Draws<T>& ph_)
-      : s(s_), i(i_), ph(ph_), cur(s_.tape ? s_.dcur[i_] : 0u) {}
-  __device__ __forceinline__ T next() {
-    if (!s.tape) return ph.next();
-    const T u = cur < (uint32_t)s.tape_len ? s.tape[(int64_t)cur * s.n + i] : T(NAN);
-    cur++;
-    return u;
-  }
-  __device__ __forceinline__ T uniform(T lo, T hi) { return lo + (hi - lo) * next(); }  // numpy uniform
-  __device__ __forceinline__ void done() const {
-    if (s.tape) s.dcur[i] = cur;
-  }
-};
+__device__ __forceinline__ T env_draw(const State<T>& s, int64_t i, Draws<T>& D, uint32_t& cur) {
+  if (!s.tape) return D.next();
+  const T u = cur < (uint32_t)s.tape_len ? s.tape[(int64_t)cur * s.n + i] : T(NAN);
+  cur++;
+  return u;
+}
+template <typename T>
+__device__ __forceinline__ T env_uniform(const State<T>& s, int64_t i, Draws<T>& D, uint32_t& cur, T lo, T hi) {
+  return lo + (hi - lo) * env_draw(s, i, D, cur);  // numpy uniform
+}
 
 // sample_target (fixed_wing.py:654-746) of one aircraft: per target (roll, pitch, Va) the initial value
 // U(low, high) narrowed to the current value -+ delta, then the class's draws -- linear: the slope
@@ -923,7 +922,7 @@ struct EnvRng {
 // explicit targets (NaN = sample); such a target is drawn all the same and then flies as "constant" for the
 // episode (reset, :436-448): slope 0, or amplitude 0 and bias = the given value.
 template <typename T>
-__device__ __forceinline__ void sample_target(const DevCfg<T>& c, const State<T>& s, int64_t i, EnvRng<T>& rng,
+__device__ __forceinline__ void sample_target(const DevCfg<T>& c, const State<T>& s, int64_t i, Draws<T>& D, uint32_t& cur,
                                               const T* vals, int steps, const T* tin, int64_t tin_ld, T* tgt) {
   const T two_pi = T(2.0 * PI_D);
 #pragma unroll
@@ -933,19 +932,19 @@ __device__ __forceinline__ void sample_target(const DevCfg<T>& c, const State<T>
       lo = fmax(lo, vals[k] - c.target_delta[k]);
       hi = fmax(fmin(hi, vals[k] + c.target_delta[k]), lo);
     }
-    const T init = rng.uniform(lo, hi);
+    const T init = env_uniform(s, i, D, cur, lo, hi);
     const T given = tin ? tin[k * tin_ld + i] : T(NAN);
     const bool fixed = !isnan(given);
     if (c.tprops && s.tpr) {
       T* tp = s.tpr + (int64_t)(4 * k) * s.ld + i;
       if (c.target_class[k] == FW_TGT_LINEAR) {
-        T slope = rng.uniform(c.tgt_slo[k], c.tgt_shi[k]);
-        if (rng.next() < T(0.5)) slope = -slope;
+        T slope = env_uniform(s, i, D, cur, c.tgt_slo[k], c.tgt_shi[k]);
+        if (env_draw(s, i, D, cur) < T(0.5)) slope = -slope;
         tp[0] = fixed ? T(0) : slope * c.tgt_rad[k];
       } else if (c.target_class[k] == FW_TGT_SINUSOIDAL) {
-        const T amp = rng.uniform(c.tgt_alo[k], c.tgt_ahi[k]) * c.tgt_rad[k];
-        const T per = rng.uniform(c.tgt_plo[k], c.tgt_phi[k]);
-        const T ph = rng.uniform(T(0), two_pi) / (two_pi / per);
+        const T amp = env_uniform(s, i, D, cur, c.tgt_alo[k], c.tgt_ahi[k]) * c.tgt_rad[k];
+        const T per = env_uniform(s, i, D, cur, c.tgt_plo[k], c.tgt_phi[k]);
+        const T ph = env_uniform(s, i, D, cur, T(0), two_pi) / (two_pi / per);
         tp[0] = fixed ? T(0) : amp;
         tp[s.ld] = per;
         tp[2 * s.ld] = ph;
@@ -1041,15 +1040,16 @@ __device__ __forceinline__ void reset_lane(const DevCfg<T>& c, const State<T>& s
   if (c.has_env) {
     // sample_target (fixed_wing.py:654-746): Philox stream 0 after the state draws, or the env-draw tape
     const T vals[3] = {der[0], der[1], der[3]};
-    EnvRng<T> rng(s, i, D);
+    uint32_t cur = s.tape ? s.dcur[i] : 0u;
     // sample_simulator_parameters' draws for simulator attributes PyFly never reads come first (:802-813);
     // they change nothing, so a tape replay only steps over them
-    if (s.tape) rng.cur += (uint32_t)c.tape_skip;
-    sample_target(c, s, i, rng, vals, 0, tin, ld, tgt);
+    if (s.tape) cur += (uint32_t)c.tape_skip;
+    sample_target(c, s, i, D, cur, vals, 0, tin, ld, tgt);
     if (s.tape && s.rsc)  // reward.randomize_scaling from the tape, after the targets (fixed_wing.py:473-479)
       for (int r = 0; r < c.n_rew; r++)
-        if (c.rew[r].randomize) st_(s.rsc, r, s.ld, i, rng.uniform((T)c.rew[r].scaling, (T)c.rew[r].scaling_hi));
-    rng.done();
+        if (c.rew[r].randomize)
+          st_(s.rsc, r, s.ld, i, env_uniform(s, i, D, cur, (T)c.rew[r].scaling, (T)c.rew[r].scaling_hi));
+    if (s.tape) s.dcur[i] = cur;
   }
 }
 
@@ -1059,9 +1059,9 @@ template <typename T>
 __device__ __forceinline__ void resample_targets(const DevCfg<T>& c, const State<T>& s, int64_t i, int steps,
                                                  const T* vals, T* tgt) {
   Draws<T> D{s.key0, s.key1, s.env_offset + (uint32_t)i, s.episode[i], (uint32_t)steps << 4, {0, 0, 0, 0}, 4, 6u};
-  EnvRng<T> rng(s, i, D);
-  sample_target(c, s, i, rng, vals, steps, (const T*)nullptr, 0, tgt);
-  rng.done();
+  uint32_t cur = s.tape ? s.dcur[i] : 0u;
+  sample_target(c, s, i, D, cur, vals, steps, (const T*)nullptr, 0, tgt);
+  if (s.tape) s.dcur[i] = cur;
 }
 
 template <typename T>
