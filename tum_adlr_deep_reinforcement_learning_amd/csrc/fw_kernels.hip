@@ -377,7 +377,24 @@ __device__ __forceinline__ T state_value(int var, const T* y, const T* der) {
     case FW_V_ACT0: return y[13];
     case FW_V_ACT1: return y[14];
     case FW_V_ACT2: return y[15];
-    default: return y[4 + (var - FW_V_OMEGA_P)];
+    default: {  // omega p q r, position n e d, velocity u v w = y[4 .. 12]
+      const int k = var - FW_V_OMEGA_P;
+      if constexpr (sizeof(T) == 4) {
+        return y[4 + k];  // (fp32: the 19-float state stays a register vector at a runtime index)
+      } else {
+        // fp64: y at a runtime index (the factor / entry loops are not unrolled) put the 19-double state in
+        // scratch, and plain selects were folded back into a select of addresses: each candidate passes an
+        // opaque register copy, so the pick is a select of values
+        T v = y[12];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          T yj = y[4 + j];
+          asm volatile("" : "+v"(yj));
+          v = k == j ? yj : v;
+        }
+        return v;
+      }
+    }
   }
 }
 
