@@ -200,6 +200,11 @@ typedef struct fw_rew_factor {
  * (fixed_wing.py:444-448)                                                                              */
 #define FW_TGT_LINEAR 2         /* target += slope * dt; slope = +-U(slope_low, slope_high) */
 #define FW_TGT_SINUSOIDAL 3     /* amplitude sin(2 pi / period (steps_count + phase)) + bias */
+/* ABI 12: class "attitude_angular" (fixed_wing.py:671-675, 741-746, 1455-1460, 1558-1642): omega_p / q / r become
+ * three further targets (fw_env_config.ang_targets), set at every reset from the roll / pitch errors and
+ * low-pass filtered at every step; observation entries (FW_OBS_TARGET_ABS / _REL) and reward factors
+ * (FW_REW_STATE_ERROR) address them as target FW_TGT_OMEGA_P + 0 / 1 / 2 (omega_p / q / r)                */
+#define FW_TGT_OMEGA_P 3
 
 /* simulator parameter randomisation (FixedWingAircraft.sample_simulator_parameters,
  * fixed_wing.py:748-813: the env config's "simulator": {"model": {...}} block), one entry per
@@ -277,7 +282,11 @@ typedef struct fw_env_config {
    * env-draw tape holds before sample_target's: fw_reset / the auto-reset skip that many tape draws.  They
    * leave the episode unchanged, so nothing else reads them.                                         */
   int32_t tape_skip;
-  int32_t pad12_;
+  /* ABI 12: 1 = omega_p / q / r targets of class attitude_angular (all three; no bound, so they stay out of
+   * the goal status; no metrics, observation history or observation noise with them), each with its max_vel
+   * (rad/s, default pi); they live in rows 12..14 of FW_BLK_TARGET_PROPS */
+  int32_t ang_targets;
+  double ang_max_vel[3];
 } fw_env_config;
 
 /* Episode-metric record written for every done env (SoA [FW_NMETRIC][N] so the stores
@@ -320,7 +329,8 @@ enum fw_init_field {
                                coalesce) and the two calls translate */
 #define FW_BLK_CMD_RING 8   /* window*3 rows, T: constrained commands, same layout (unscaled action windows) */
 #define FW_BLK_TARGET_PROPS 10 /* 12 rows, T (ABI 11; linear / sinusoidal target classes only): per target (roll, pitch,
-                                * Va) 4 rows: slope (linear) or amplitude, period, phase, bias (sinusoidal) */
+                                * Va) 4 rows: slope (linear) or amplitude, period, phase, bias (sinusoidal); ABI 12:
+                                * 15 rows with attitude_angular targets, rows 12..14 = the omega_p / q / r targets */
 #define FW_BLK_GOAL 9       /* 4 rows, uint32: the last 128 goal-status bits ("all"), bit 0 of row 0 newest (0 before
                              * the episode's first entry).  Env handles only.  Setting it takes the episode's
                              * history length from FW_BLK_STEPS (steps_count + 1 entries): set FW_BLK_STEPS first */

@@ -130,9 +130,29 @@ def _simattr(cfg):
     cfg["simulator"]["inert_mode"] = {"values": [0, 1, 2], "probabilities": [0.2, 0.5, 0.3]}
 
 
+def _attang(cfg):
+    # target class attitude_angular (fixed_wing.py:671-675, 741-746, 1455-1460, 1558-1642): omega_p / q / r targets
+    # low-pass filtered from the roll / pitch errors; observed (relative and absolute), rewarded (an error factor),
+    # and a per_state goal reward whose value is divided by len(self.target) = 6; no bound on them (the goal
+    # status stays roll / pitch / Va) and no metrics (get_metric would cover every target)
+    for name in ("omega_p", "omega_q", "omega_r"):
+        cfg["target"]["states"].append({"name": name, "class": "attitude_angular"})
+    cfg["target"]["states"][-1]["max_vel"] = 2.5
+    cfg["metrics"] = []
+    obs = cfg["observation"]["states"]
+    obs.append({"name": "omega_p", "type": "target", "value": "relative"})
+    obs.append({"name": "omega_q", "type": "target", "value": "relative"})
+    obs.append({"name": "omega_r", "type": "target", "value": "absolute"})
+    cfg["reward"]["factors"].append({"name": "omega_q", "class": "state", "type": "error", "function_class": "linear",
+                                     "scaling": 2.0, "max": 0.5, "shaping": False, "sign": -1})
+    cfg["reward"]["factors"].append({"name": "goal_ps", "class": "goal", "type": "per_state", "value": 0.3,
+                                     "function_class": "linear", "scaling": 1.0, "shaping": False, "sign": 1})
+
+
 CASES_B = {
     # round 6, second batch (env_r06b.npz)
     "simattr": (_simattr, "rand", 400, 3, 300, None),
+    "attang": (_attang, "rand", 400, 3, 300, None),
 }
 
 CASES = {
@@ -153,7 +173,10 @@ def episode(env, rng, pol, n_steps, target=None):
     obs0 = env.reset(state=dict(st), target=dict(target) if target else None)
     init = np.array([st[k] for k in G.ENV_STATE_KEYS] + [0.0, 0.0, 0.0] + list(st["wind"]))
     tg = lambda: np.array([env.target["roll"], env.target["pitch"], env.target["Va"]])  # noqa: E731
+    ang = "omega_p" in env.target
+    tga = lambda: np.array([float(env.target[k]) for k in ("omega_p", "omega_q", "omega_r")])  # noqa: E731
     obs, rew, done, term, acts, tgt = [obs0], [], [], [], [], [tg()]
+    tang = [tga()] if ang else []
     pid = {"dt": 0.01, "va": env.target["Va"], "phi": env.target["roll"], "theta": env.target["pitch"],
            "iv": 0.0, "ir": 0.0, "ip": 0.0}
     for _ in range(n_steps):
@@ -168,11 +191,14 @@ def episode(env, rng, pol, n_steps, target=None):
         done.append(d)
         term.append(info.get("termination", ""))
         tgt.append(tg())
+        if ang:
+            tang.append(tga())
         pid["phi"], pid["theta"], pid["va"] = info["target"]["roll"], info["target"]["pitch"], info["target"]["Va"]
         if d:
             break
+    extra = {"target_ang": np.array(tang)} if ang else {}
     return dict(init=init, tape=np.array(tape.tape[n0:]), obs=np.array(obs), act=np.array(acts), rew=np.array(rew),
-                done=np.array(done), term=np.array(term), target=np.array(tgt),
+                done=np.array(done), term=np.array(term), target=np.array(tgt), **extra,
                 target0_given=np.array([np.nan if not target or k not in target else target[k]
                                         for k in ("roll", "pitch", "Va")]))
 

@@ -17,7 +17,7 @@ import _fixtures as F
 from tum_adlr_deep_reinforcement_learning_amd import config as C
 
 R06 = ["linear", "linear_fix", "sinus", "resample", "success"]
-R06B = ["simattr"]  # env_r06b.npz (round 6, second batch)
+R06B = ["simattr", "attang"]  # env_r06b.npz (round 6, second batch)
 
 
 def r06_spec(name, tmpdir):
@@ -45,7 +45,8 @@ def test_r06_config_struct(name, tmpdir):
     spec, d = r06_spec(name, tmpdir)
     cfg = json.loads(str(d[name + "__config_json"]))
     e = spec.struct()
-    for i, st in enumerate(cfg["target"]["states"]):
+    assert e.ang_targets == int(name == "attang")
+    for i, st in enumerate(cfg["target"]["states"][:3]):
         cls = st.get("class", "constant")
         assert e.target_class[i] == C.FW_TGT[cls]
         assert e.target_radians[i] == int(bool(st.get("convert_to_radians", False)))
@@ -94,16 +95,43 @@ def test_r06_tapes(name, tmpdir):
             assert resamples >= 2  # several successes: the success reward fires on the first one only
 
 
-def test_attitude_angular_refused(tmpdir):
-    """attitude_angular turns omega_p / q / r into targets (fixed_wing.py:671-675, 1558-1642): not built."""
-    _, d = r06_spec("linear", tmpdir)
-    cfg = json.loads(str(d["linear__config_json"]))
-    cfg["target"]["states"][0]["class"] = "attitude_angular"
+def _attang_spec(tmpdir, mod):
+    _, d = r06_spec("attang", tmpdir)
+    cfg = json.loads(str(d["attang__config_json"]))
+    mod(cfg)
     path = os.path.join(str(tmpdir), "aa.json")
     with open(path, "w") as f:
         json.dump(cfg, f)
-    with pytest.raises(NotImplementedError):
-        C.EnvSpec(config_path=path, sim_config_kw={"turbulence": False}).struct()
+    return lambda: C.EnvSpec(config_path=path, sim_config_kw={"turbulence": False}).struct()
+
+
+def test_attitude_angular_config(tmpdir):
+    """attitude_angular (fixed_wing.py:671-675, 741-746, 1455-1460, 1558-1642): omega_p / q / r become targets
+    FW_TGT_OMEGA_P + k for observation entries and error factors, with max_vel (default pi); the class on
+    roll / pitch / Va is the reference's ValueError; what the device does not carry is refused loudly: a bound
+    on an omega target (the goal status), metrics, observation history / noise, a partial omega set."""
+    e = _attang_spec(tmpdir, lambda cfg: None)()
+    assert e.ang_targets == 1 and list(e.ang_max_vel) == [np.pi, np.pi, 2.5]
+    ang_obs = [e.obs[o].var for o in range(e.n_obs) if e.obs[o].kind in (C.FW_OBS_TARGET_ABS, C.FW_OBS_TARGET_REL)]
+    assert ang_obs[-3:] == [3, 4, 5]
+    assert e.rew[e.n_rew - 2].kind == C.FW_REW_STATE_ERROR and e.rew[e.n_rew - 2].var == 4
+
+    def roll_class(cfg):
+        cfg["target"]["states"][0]["class"] = "attitude_angular"
+    with pytest.raises(ValueError):
+        _attang_spec(tmpdir, roll_class)()
+
+    def bound(cfg):
+        cfg["target"]["states"][4]["bound"] = 0.1
+    def metrics(cfg):
+        cfg["metrics"] = [{"name": "total_error"}]
+    def partial(cfg):
+        cfg["target"]["states"].pop()
+    def history(cfg):
+        cfg["observation"]["length"] = 3
+    for mod in (bound, metrics, partial, history):
+        with pytest.raises(NotImplementedError):
+            _attang_spec(tmpdir, mod)()
 
 
 def _sim_block_spec(tmpdir, extra):

@@ -182,3 +182,40 @@ def test_deferred_final_merge_bitwise(n, cnt):
     assert cb.graph_nodes()[0].count(0) == 2
     for v, _, _, _ in setups:
         v.close()
+
+
+@pytest.mark.parametrize("precision", ["float64", "float32"])
+def test_attitude_angular_targets_follow_the_reference(precision, tmpdir):
+    """The omega_p / q / r targets of class attitude_angular (env_r06b.npz "attang": set from the roll / pitch
+    errors at the reset, low-pass filtered every step, fixed_wing.py:741-746, 1455-1460, 1558-1642) as the device
+    keeps them (FW_BLK_TARGET_PROPS rows 12..14) against the reference's env.target after every step: fp64 within
+    1e-6 + 1e-6 / step, fp32 within 2e-3 (1 + |ref|).  The observations (omega target entries included) and
+    rewards (an omega error factor, a per_state goal factor over len(target) = 6) are compared by
+    test_env_draw_tape_replays_reference_episodes."""
+    from tum_adlr_deep_reinforcement_learning_amd.engine import Engine
+    spec, d = r06_spec("attang", tmpdir)
+    name = "attang"
+    eps = int(d[name + "__episodes"])
+    g = lambda ep, k: d["%s__ep%d__%s" % (name, ep, k)]  # noqa: E731
+    eng = Engine(spec.sim, spec, eps, device=DEV, precision=precision)
+    L = max(len(g(ep, "tape")) for ep in range(eps))
+    tape = np.full((L + 1, eps), np.nan)
+    for ep in range(eps):
+        tape[:len(g(ep, "tape")), ep] = g(ep, "tape")
+    eng.set_env_draws(tape)
+    init = np.stack([F.env_init(g(ep, "init")) for ep in range(eps)], axis=1)
+    eng.reset(init=init)
+    f64 = precision == "float64"
+    n = max(len(g(ep, "rew")) for ep in range(eps))
+    for s in range(n + 1):
+        if s > 0:
+            acts = np.stack([g(ep, "act")[min(s - 1, len(g(ep, "act")) - 1)] for ep in range(eps)])
+            eng.env_step(torch.tensor(acts, dtype=eng.dtype, device=DEV), auto_reset=False)
+        ot = eng.get_block(C.FW_BLK_TARGET_PROPS).double().cpu().numpy()[12:15]
+        for ep in range(eps):
+            if s >= len(g(ep, "target_ang")):
+                continue
+            ref = g(ep, "target_ang")[s]
+            tol = (1e-6 + 1e-6 * s) if f64 else 2e-3 * (1 + np.abs(ref))
+            assert np.all(np.abs(ot[:, ep] - ref) <= tol), (ep, s, ot[:, ep], ref)
+    eng.close()

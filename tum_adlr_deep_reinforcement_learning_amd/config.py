@@ -163,7 +163,7 @@ class FwEnvConfig(ctypes.Structure):
                 ("target_slope_low", ctypes.c_double * 3), ("target_slope_high", ctypes.c_double * 3),
                 ("target_amp_low", ctypes.c_double * 3), ("target_amp_high", ctypes.c_double * 3),
                 ("target_period_low", ctypes.c_double * 3), ("target_period_high", ctypes.c_double * 3),
-                ("tape_skip", ctypes.c_int32), ("pad12_", ctypes.c_int32)]
+                ("tape_skip", ctypes.c_int32), ("ang_targets", ctypes.c_int32), ("ang_max_vel", ctypes.c_double * 3)]
 
 
 # ---------------------------------------------------------------------------
@@ -531,6 +531,9 @@ def build_sim(config_path=None, parameter_path=None, config_kw=None):
 # Env config
 # ---------------------------------------------------------------------------
 TARGET_INDEX = {"roll": 0, "pitch": 1, "Va": 2}
+# attitude_angular targets (fixed_wing.py:671-675, 1558-1642): include/fwsim.h FW_TGT_OMEGA_P + k
+ANG_TARGETS = ["omega_p", "omega_q", "omega_r"]
+ANG_INDEX = {n: 3 + k for k, n in enumerate(ANG_TARGETS)}
 ACTION_INDEX = {"elevator": 0, "aileron": 1, "throttle": 2}
 
 
@@ -576,6 +579,31 @@ class EnvSpec:
         # applies those states in set_curriculum_level afterwards (:300)
         self._build_spaces()
         self.set_curriculum_level(curriculum_level)
+        self.ang_targets = self._check_targets()
+
+    def _check_targets(self):
+        """[roll, pitch, Va], optionally followed by omega_p / q / r of class attitude_angular (all three: the
+        reference computes all three rates, fixed_wing.py:741-746, reading each one's props).  Returns whether
+        the attitude_angular targets are present."""
+        cfg = self.cfg
+        states = cfg["target"]["states"]
+        tnames = [s["name"] for s in states]
+        if tnames[:3] != ["roll", "pitch", "Va"] or sorted(tnames[3:]) not in ([], sorted(ANG_TARGETS)):
+            raise NotImplementedError("targets must be [roll, pitch, Va] (+ omega_p / q / r of class attitude_angular)")
+        if len(tnames) == 3:
+            return False
+        for st in states[3:]:
+            if st.get("class", "constant") != "attitude_angular":
+                raise NotImplementedError("target %s of class %r" % (st["name"], st.get("class", "constant")))
+            if st.get("bound") is not None:
+                # the goal status would count an omega target (fixed_wing.py:1346-1361): the device's goal history
+                # holds roll / pitch / Va
+                raise NotImplementedError("a bound on attitude_angular target %s" % st["name"])
+        if cfg.get("metrics"):
+            raise NotImplementedError("episode metrics with attitude_angular targets (get_metric covers every target)")
+        if self.obs_length > 1 or self.obs_noise is not None:
+            raise NotImplementedError("observation history / noise with attitude_angular targets")
+        return True
 
     # PyFly attributes PyFly.step / reset read (pyfly.py:1251-1482): the numbers among them change the dynamics
     # (dt: the RK45 interval, cur_sim_step: the turbulence sample index), the objects the next step would fail on
@@ -793,7 +821,12 @@ class EnvSpec:
                     E.kind = FW_OBS_TARGET_INT
                 else:
                     raise NotImplementedError("target observation value %r" % val)
-                E.var = TARGET_INDEX[o["name"]]
+                if o["name"] in ANG_INDEX and self.ang_targets:
+                    if val == "integrator":
+                        raise NotImplementedError("integrator observation of an attitude_angular target")
+                    E.var = ANG_INDEX[o["name"]]
+                else:
+                    E.var = TARGET_INDEX[o["name"]]
             elif t == "action":
                 E.kind, E.var = FW_OBS_ACTION_WINDOW, ACTION_INDEX[o["name"]]
                 E.window = int(o.get("window_size", 1))
@@ -822,15 +855,15 @@ class EnvSpec:
             e.act_low[i] = float(self.action_scale_to_low[i])
             e.act_high[i] = float(self.action_scale_to_high[i])
         tnames = [s["name"] for s in cfg["target"]["states"]]
-        if tnames != ["roll", "pitch", "Va"]:
-            raise NotImplementedError("targets must be [roll, pitch, Va]")
-        for i, name in enumerate(tnames):
+        for k, name in enumerate(ANG_TARGETS):  # fixed_wing.py:671-675, 741-746, 1558-1642
+            if self.ang_targets:
+                e.ang_max_vel[k] = float(self.target_props[name].get("max_vel", np.radians(180)))
+        e.ang_targets = int(self.ang_targets)
+        for i, name in enumerate(tnames[:3]):
             p = self.target_props[name]
             cls = p.get("class", "constant")
-            if cls == "attitude_angular":
-                # targets omega_p / q / r derived from the roll / pitch errors (fixed_wing.py:671-675, 1455-1460,
-                # 1558-1642): a target set beyond (roll, pitch, Va) -- not built
-                raise NotImplementedError("target class %r" % cls)
+            if cls == "attitude_angular":  # _get_next_target (:1455-1459)
+                raise ValueError("Invalid state for class attitude_angular {}".format(name))
             if cls not in FW_TGT:
                 raise ValueError("Unexpected target class {}".format(cls))
             if cls == "compensate" and name != "Va":
@@ -911,7 +944,9 @@ class EnvSpec:
                     raise ValueError("Unexpected type {} for reward class action".format(typ))
             elif cls == "state":
                 if typ == "error":
-                    F.kind, F.var = FW_REW_STATE_ERROR, TARGET_INDEX[f["name"]]
+                    F.kind = FW_REW_STATE_ERROR
+                    F.var = ANG_INDEX[f["name"]] if (self.ang_targets and f["name"] in ANG_INDEX) else \
+                        TARGET_INDEX[f["name"]]
                 elif typ == "value":
                     F.kind, F.var = FW_REW_STATE_VALUE, STATE_VAR_IDS[f["name"]]
                 elif typ == "int_error":  # fixed_wing.py:1001-1012

@@ -151,6 +151,9 @@ struct DevCfg {
   // linear / sinusoidal target classes (fw_env_config ABI 11): draw bounds, np.radians factor (1 or pi/180)
   int tprops;                          // some target is linear or sinusoidal: State::tpr rows are kept
   int tape_skip;                       // env-draw tape entries before sample_target's at a reset (inert attributes)
+  int ang;                             // omega_p / q / r targets of class attitude_angular (State::tpr rows 12..14)
+  T ang_max_vel[3];
+  T n_targets;                         // len(self.target): 3, or 6 with the attitude_angular targets
   T tgt_rad[3], tgt_slo[3], tgt_shi[3], tgt_alo[3], tgt_ahi[3], tgt_plo[3], tgt_phi[3];
   int goal_flag;                       // a success reward factor: State::gflag keeps goal_achieved
   // goal-status history ring (fw_kernels.hip GB_*): 8 x gring_words entries (a power of two >= 128 and >=
@@ -188,6 +191,7 @@ struct SpecCfg : DevCfg<T> {
   static constexpr uint32_t cmask = CM, clipmask = CLM, wrapmask = WM, dotmask = DM;
   static constexpr int elevon = ELEVON, trig_alpha = TA, trig_beta = TB, euler_exact = EE;
   static constexpr int obs_general = 0;  // specialisations serve plain length-1, noise-free observations
+  static constexpr int ang = 0;          // ... and the three targets roll / pitch / Va
   static constexpr int const_limits = 0;  // limit values compile-time constants too (see GymX8Cfg)
   static constexpr int const_params = 0;  // airframe constants compile-time too
   static constexpr int rand_params = 0;  // ... with one parameter set for all aircraft
@@ -1625,6 +1629,43 @@ FW_HD void next_target(const DevCfg<T>& c, int steps_tgt, int steps, TP tp, T* t
   tgt[0] = res[0];
   tgt[1] = res[1];
   tgt[2] = res[2];
+}
+
+// _attitude_to_angular_rates (fixed_wing.py:1558-1642) of target omega_p / q / r (k = 0 / 1 / 2): from the errors
+// of the roll / pitch targets `tgt` against the attitude (roll, pitch) and the current omega targets `ot`.  As
+// numpy evaluates it: np.clip keeps a NaN, np.sign(0) = 0, a zero sin(roll) divides to +-inf; the damping's
+// `<= radians(0.1)` branch is overwritten on the next line there, so it is absent here.
+template <typename T>
+FW_HD T np_clip(T x, T lo, T hi) {
+  return x < lo ? lo : (x > hi ? hi : x);
+}
+template <typename T>
+FW_HD T np_sign(T x) {
+  return x > T(0) ? T(1) : (x < T(0) ? T(-1) : x);
+}
+template <typename T>
+FW_HD T att_ang_rate(const DevCfg<T>& c, int k, const T* tgt, const T* ot, T roll, T pitch) {
+  const T mv = c.ang_max_vel[k], dt = c.dt, half_pi = T(0.5 * PI_D);
+  const T roll_err = target_error(c, 0, tgt[0], roll);
+  const T pitch_err = target_error(c, 1, tgt[1], pitch);
+  const T qw = cos(roll), rw = sin(roll);
+  const T mpc = mv * dt * (qw + rw);
+  T res, damp;
+  if (k == 0) {
+    damp = fabs(roll_err / half_pi);
+    const T q_roll = sin(roll) * tan(pitch) * ot[1] * dt;
+    const T r_roll = cos(roll) * tan(pitch) * ot[2] * dt;
+    res = np_clip(-(roll_err - q_roll - r_roll) / dt, -mv, mv);
+  } else if (k == 1) {
+    damp = fabs(pitch_err / half_pi);
+    res = mpc > fabs(pitch_err) ? -pitch_err / (T(2) * qw) : np_sign(qw) * mv * np_sign(pitch_err);
+  } else {
+    damp = fabs(pitch_err / half_pi);
+    res = mpc > fabs(pitch_err) ? pitch_err / rw : -np_sign(rw) * mv * np_sign(pitch_err);
+  }
+  damp = isnan(damp) ? T(0.05) : (damp < T(1) ? damp : T(1));  // min(1, damping)
+  const T t = ot[k];
+  return np_clip(t + (res * damp - t) * T(1) / T(20), -mv, mv);
 }
 
 // linear_action_scaling (fixed_wing.py:630-652)

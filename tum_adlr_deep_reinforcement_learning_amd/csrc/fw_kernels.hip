@@ -361,6 +361,14 @@ __device__ __forceinline__ T pick3(const T* a, int k) {
   return k == 0 ? a[0] : (k == 1 ? a[1] : a[2]);
 }
 
+// the same from three values that pass an opaque register copy first: a select of three ELEMENTS of a register
+// array (y) is folded into a select of their addresses, which puts the array in scratch
+template <typename T>
+__device__ __forceinline__ T pick3v(T a0, T a1, T a2, int k) {
+  asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2));
+  return k == 0 ? a0 : (k == 1 ? a1 : a2);
+}
+
 // value of an observed / rewarded state variable from the stored state
 template <typename T>
 __device__ __forceinline__ T state_value(int var, const T* y, const T* der) {
@@ -408,6 +416,8 @@ __device__ __forceinline__ T obs_raw(const DevCfg<T>& c, const fw_obs_entry& E, 
     T val;
     if (E.kind == FW_OBS_STATE) {
       val = state_value(E.var, y, der);
+    } else if ((E.kind == FW_OBS_TARGET_ABS || E.kind == FW_OBS_TARGET_REL) && E.var >= FW_TGT_OMEGA_P) {
+      val = T(0);  // (an attitude_angular target: written afterwards, ang_obs)
     } else if (E.kind == FW_OBS_TARGET_ABS) {
       val = pick3(tgt, E.var);
     } else if (E.kind == FW_OBS_TARGET_REL) {
@@ -474,6 +484,27 @@ __device__ __forceinline__ void iw_obs(const DevCfg<T>& c, const T* v3, T* out, 
 template <typename T>
 __device__ __forceinline__ void iw_obs_all_rows(const DevCfg<T>& c, const T* v3, T* out) {
   for (int r = 0; r < c.obs_len; r++) iw_obs(c, v3, out, r);
+}
+// the attitude_angular target entries of an observation (obs_raw wrote 0 in their place; plain length-1,
+// noise-free observations only, config.py): the omega target (absolute) or its error target - omega (relative,
+// _get_error: omega does not wrap), normalised (fixed_wing.py:1133-1247)
+template <typename T>
+__device__ __forceinline__ void ang_obs(const DevCfg<T>& c, const T* ot, const T* y, T* out) {
+  if (!out) return;
+  for (int o = 0; o < c.n_obs; o++) {
+    const fw_obs_entry E = c.obs[o];
+    if ((E.kind == FW_OBS_TARGET_ABS || E.kind == FW_OBS_TARGET_REL) && E.var >= FW_TGT_OMEGA_P) {
+      const int k = E.var - FW_TGT_OMEGA_P;
+      const T t = pick3(ot, k);
+      out[o] = obs_norm(E, E.kind == FW_OBS_TARGET_ABS ? t : t - pick3v(y[4], y[5], y[6], k));
+    }
+  }
+}
+// the attitude_angular targets as stored (State::tpr rows 12..14)
+template <typename T>
+__device__ __forceinline__ void ang_load(const State<T>& s, int64_t i, T* ot) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) ot[k] = s.tpr[(int64_t)(12 + k) * s.ld + i];
 }
 // observation history (observation.length > 1): the raw row kept for later lags holds the integrator
 // entries' lag-1 values, so a lagged row reads slice [-W-i:-i] as the reference does (its padding condition
@@ -628,9 +659,10 @@ template <typename T>
 // (shp / iwq are register arrays taken by reference with a flag: a pointer that may be null would take their
 // address and place them in scratch)
 // succ: goal_achieved_on_step (fixed_wing.py:546, 565): the first success of the env's lifetime, this step
+// ot: the attitude_angular targets omega_p / q / r (c.ang; factors with var FW_TGT_OMEGA_P + k)
 __device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* der, const T* tgt, int steps,
                                        const T (*seqA)[3], T (&shp)[3], bool pot, const T* rsc, int64_t ld,
-                                       const T (&iwq)[6], bool iw, bool succ = false) {
+                                       const T (&iwq)[6], bool iw, bool succ, const T (&ot)[3]) {
   T tv[3] = {T(0), T(0), T(0)}, ts[3] = {T(0), T(0), T(0)};
   for (int f = 0; f < c.n_rew; f++) {
     const fw_rew_factor F = c.rew[f];
@@ -673,8 +705,11 @@ __device__ __forceinline__ T reward_of(const DevCfg<T>& c, const T* y, const T* 
       } else {
 #pragma unroll
         for (int k = 0; k < 3; k++)  // value / len(self.target) per bounded target within its bound
-          val += ((gb >> k) & 1u) ? (T)F.value / T(3) : T(0);
+          val += ((gb >> k) & 1u) ? (T)F.value / c.n_targets : T(0);  // (len(self.target): 6 with omega)
       }
+    } else if (F.var >= FW_TGT_OMEGA_P) {  // an attitude_angular target's error (no wrap): target - omega
+      const int k = F.var - FW_TGT_OMEGA_P;
+      val = pick3(ot, k) - pick3v(y[4], y[5], y[6], k);
     } else {  // (by selects: the factor loop is not unrolled at FW_MAX_REW 12, and tgt[F.var] went to scratch)
       const int tv_ = F.var == 0 ? FW_V_ROLL : (F.var == 1 ? FW_V_PITCH : FW_V_VA);
       val = target_error(c, F.var, pick3(tgt, F.var), state_value(tv_, y, der));
@@ -942,6 +977,7 @@ template <typename T>
 __device__ __forceinline__ void sample_target(const DevCfg<T>& c, const State<T>& s, int64_t i, Draws<T>& D, uint32_t& cur,
                                               const T* vals, int steps, const T* tin, int64_t tin_ld, T* tgt) {
   const T two_pi = T(2.0 * PI_D);
+  T drawn[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     T lo = c.target_low[k], hi = c.target_high[k];
@@ -969,6 +1005,14 @@ __device__ __forceinline__ void sample_target(const DevCfg<T>& c, const State<T>
       }
     }
     tgt[k] = fixed ? given : init;
+    drawn[k] = init;
+  }
+  if (c.ang && s.tpr) {
+    // the omega targets (:662-675, 741-746): 0, then all three rates from those zeros and the DRAWN roll / pitch
+    // targets (an explicit target replaces its draw only afterwards, in reset, :444-448)
+    const T z[3] = {T(0), T(0), T(0)};
+#pragma unroll
+    for (int k = 0; k < 3; k++) s.tpr[(int64_t)(12 + k) * s.ld + i] = att_ang_rate(c, k, drawn, z, vals[0], vals[1]);
   }
 }
 
@@ -1184,6 +1228,11 @@ __global__ __launch_bounds__(BLOCK) void k_reset(const DevCfg<T>* __restrict__ c
       for (int a = 0; a < 3; a++) seq[j][a] = T(0);
     observe_env(c, s, i, s.episode[i], OBS_RESET, y, der, tgt, 0, seq, seq,
                 obs ? obs + i * (int64_t)c.n_obs * c.obs_len : nullptr, s.life[i]);
+    if (c.ang && obs) {
+      T ot[3];
+      ang_load(s, i, ot);
+      ang_obs(c, ot, y, obs + i * (int64_t)c.n_obs * c.obs_len);
+    }
     if (s.iws) {
       iw_obs_all_rows(c, rv, obs ? obs + i * (int64_t)c.n_obs * c.obs_len : nullptr);
       iw_hist_init(c, s, i, tgt, der);
@@ -1224,6 +1273,11 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const DevCfg<T>* __restrict__
   }
   observe_env(c, s, i, s.episode[i], OBS_PEEK, y, der, tgt, steps, seqA, seqC, obs + i * (int64_t)c.n_obs * c.obs_len,
               life - (uint32_t)steps);
+  if (c.ang) {
+    T ot[3];
+    ang_load(s, i, ot);
+    ang_obs(c, ot, y, obs + i * (int64_t)c.n_obs * c.obs_len);
+  }
   if (s.iws) {  // get_observation with the current history: the sum before the newest entry + padding
     T v[3];
 #pragma unroll
@@ -1487,6 +1541,10 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
 #pragma unroll
   for (int q = 0; q < 3; q++) st_(s.cmd, q, ld, i, cmd[q]);
   const T tgt_in[3] = {tgt[0], tgt[1], tgt[2]};  // a target row is stored only where some lane changed it
+  T ot[3] = {T(0), T(0), T(0)};  // attitude_angular targets omega_p / q / r (c.ang; a constant 0 in the specialisations)
+  if (c.ang)
+#pragma unroll
+    for (int k = 0; k < 3; k++) ot[k] = s.tpr[(int64_t)(12 + k) * ld + i];
   if (sterm == 0) {
     const T vals[3] = {der[0], der[1], der[3]};
     uint32_t gb = 0;
@@ -1526,18 +1584,26 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
     if (goal_on || c.metrics || s.iws) st_(s.goal, GB_N, ld, i, b + 1u);
     if (s.shp || s.rsc || s.iws) {
       reward = reward_of(c, y, der, tgt, steps, seqA, shp, s.shp != nullptr, s.rsc ? s.rsc + i : nullptr, ld,
-                         iwq, s.iws != nullptr, succ_first);
+                         iwq, s.iws != nullptr, succ_first, ot);
       if (s.shp)
 #pragma unroll
         for (int k = 0; k < 3; k++) st_(s.shp, k, ld, i, shp[k]);
     } else {
-      reward = reward_of(c, y, der, tgt, steps, seqA, shp, false, (const T*)nullptr, 0, iwq, false, succ_first);
+      reward = reward_of(c, y, der, tgt, steps, seqA, shp, false, (const T*)nullptr, 0, iwq, false, succ_first, ot);
     }
     if (resample || (c.resample_every > 0 && steps_tgt >= c.resample_every)) {
       // on_success "new" or target.resample_every (fixed_wing.py:566-574): sample_target (:654-746) from the
       // state after the step, then _get_next_target with the target step count restarted
       resample_targets(c, s, i, steps, vals, tgt);
       steps_tgt = 0;
+      if (c.ang) ang_load(s, i, ot);  // (sample_target's omega targets, from zero)
+    }
+    if (c.ang) {  // _get_next_target's attitude_angular part (:1455-1460), from the targets before the update
+      const T o0[3] = {ot[0], ot[1], ot[2]};
+#pragma unroll
+      for (int k = 0; k < 3; k++) ot[k] = att_ang_rate(c, k, tgt, o0, vals[0], vals[1]);
+#pragma unroll
+      for (int k = 0; k < 3; k++) s.tpr[(int64_t)(12 + k) * ld + i] = ot[k];
     }
     next_target(c, steps_tgt, steps, [&](int r) { return s.tpr[(int64_t)r * ld + i]; }, tgt);
     if (s.iws) {  // history["error"][k].append(self._get_error(k)) (fixed_wing.py:575-579): the window sums move on
@@ -1587,6 +1653,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
     for (int k = 0; k < 3; k++) iwv[k] = iw_value(c, iqp[k], steps - 1, iwq[3 + k]);
   if (done && tobs_out) {
     observe_env(c, s, i, episode, omode, y, der, tgt, steps, seqA, seqC, tobs_out + i * ow, lep);
+    if (c.ang) ang_obs(c, ot, y, tobs_out + i * ow);
     if (s.iws) {
       iw_obs(c, iwv, tobs_out + i * ow);
       if (omode == OBS_FAIL) iw_obs_fail(c, s, i, steps, lep, tobs_out + i * ow);
@@ -1633,6 +1700,11 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
 #endif
       T seq0[RING + 1][3];
       observe_env(c, s, i, s.episode[i], OBS_RESET, yr, dr, tr, 0, seq0, seq0, orow, life0 + 1u);  // (reset_lane's +1)
+      if (c.ang) {
+        T otr[3];
+        ang_load(s, i, otr);
+        ang_obs(c, otr, yr, orow);
+      }
       if (s.iws) {
         // FixedWingAircraft.reset observes BEFORE it replaces the history (fixed_wing.py:452-459): the finished
         // episode's sums, padded as at steps_count 0; then the new episode's entry 0
@@ -1650,6 +1722,7 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   }
 #ifndef FW_SKIP_OBS
   observe_env(c, s, i, episode, omode, y, der, tgt, steps, seqA, seqC, orow, lep);
+  if (c.ang) ang_obs(c, ot, y, orow);
   if (s.iws) {
     iw_obs(c, iwv, orow);
     if (omode == OBS_FAIL) iw_obs_fail(c, s, i, steps, lep, orow);
@@ -2274,6 +2347,9 @@ void fill_devcfg(const fw_handle* h, DevCfg<T>& d) {
     }
     d.tprops = d.tprops && h->o_tpr;
     d.tape_skip = e.tape_skip > 0 ? e.tape_skip : 0;
+    d.ang = e.ang_targets ? 1 : 0;
+    for (int k = 0; k < 3; k++) d.ang_max_vel[k] = (T)e.ang_max_vel[k];
+    d.n_targets = d.ang ? T(6) : T(3);
     d.goal_flag = h->o_gflag != 0;
     d.streak_frac = (T)e.streak_frac;
     d.step_fail_value = (T)e.step_fail_value;
@@ -2344,6 +2420,24 @@ int validate(const fw_sim_config* s, const fw_env_config* e) {
     if (e->target_class[2] == FW_TGT_COMPENSATE && e->target_class[1] == FW_TGT_COMPENSATE)
       return set_err(FW_E_UNSUPPORTED, "compensate Va with a compensate pitch target (fixed_wing.py:1386-1392)");
     if (e->on_success < 0 || e->on_success > 2) return set_err(FW_E_INVALID, "on_success must be 0 (none), 1 (done) or 2 (new)");
+    // attitude_angular targets (ABI 12): entries / factors address them as FW_TGT_OMEGA_P + k only when present;
+    // plain observations only (ang_obs writes row 0); metrics cover roll / pitch / Va
+    for (int o = 0; o < e->n_obs; o++) {
+      const fw_obs_entry& E = e->obs[o];
+      const bool tgt = E.kind == FW_OBS_TARGET_ABS || E.kind == FW_OBS_TARGET_REL || E.kind == FW_OBS_TARGET_INT;
+      if (tgt && (E.var < 0 || E.var > (e->ang_targets && E.kind != FW_OBS_TARGET_INT ? FW_TGT_OMEGA_P + 2 : 2)))
+        return set_err(FW_E_INVALID, "target observation entry: bad target index");
+    }
+    for (int r = 0; r < e->n_rew; r++)
+      if (e->rew[r].kind == FW_REW_STATE_ERROR &&
+          (e->rew[r].var < 0 || e->rew[r].var > (e->ang_targets ? FW_TGT_OMEGA_P + 2 : 2)))
+        return set_err(FW_E_INVALID, "state error reward factor: bad target index");
+    if (e->ang_targets) {
+      if (e->obs_length > 1 || e->obs_noise || e->metrics)
+        return set_err(FW_E_UNSUPPORTED, "attitude_angular targets with observation history / noise or metrics");
+      for (int k = 0; k < 3; k++)
+        if (!(e->ang_max_vel[k] >= 0)) return set_err(FW_E_INVALID, "attitude_angular max_vel < 0");
+    }
   }
   return FW_OK;
 }
@@ -2380,7 +2474,7 @@ bool same_structure(const DevCfg<T>& d) {
   return d.rand_params == S::rand_params && d.cmask == S::cmask && d.clipmask == S::clipmask &&
          d.wrapmask == S::wrapmask && d.dotmask == S::dotmask &&
          d.elevon == S::elevon && d.trig_alpha == S::trig_alpha && d.trig_beta == S::trig_beta &&
-         d.euler_exact == S::euler_exact && d.obs_general == S::obs_general;
+         d.euler_exact == S::euler_exact && d.obs_general == S::obs_general && d.ang == S::ang;
 }
 
 template <typename T>
@@ -2693,7 +2787,7 @@ int fw_create(const fw_sim_config* sim, const fw_env_config* env, int64_t n_envs
     bool tp = false, sf = false;
     for (int k = 0; k < 3; k++) tp = tp || env->target_class[k] == FW_TGT_LINEAR || env->target_class[k] == FW_TGT_SINUSOIDAL;
     for (int r = 0; r < env->n_rew; r++) sf = sf || env->rew[r].kind == FW_REW_SUCCESS;
-    if (tp) { h->o_tpr = off; off += (size_t)12 * row; }
+    if (tp || env->ang_targets) { h->o_tpr = off; off += (size_t)(env->ang_targets ? 15 : 12) * row; }
     if (sf) { h->o_gflag = off; off += align_up((size_t)h->ld * 4, 256); }
     h->o_dcur = off; off += align_up((size_t)h->ld * 4, 256);
   }
@@ -2844,8 +2938,10 @@ int fw_update_config(fw_handle* h, const fw_sim_config* sim, const fw_env_config
     if (env->reward_potential && !h->o_shp)
       return set_err(FW_E_UNSUPPORTED, "reward.form \"potential\" must be set when the handle is created");
     for (int k = 0; k < 3; k++)
-      if ((env->target_class[k] == FW_TGT_LINEAR || env->target_class[k] == FW_TGT_SINUSOIDAL) && !h->o_tpr)
+      if ((env->target_class[k] == FW_TGT_LINEAR || env->target_class[k] == FW_TGT_SINUSOIDAL || env->ang_targets) && !h->o_tpr)
         return set_err(FW_E_UNSUPPORTED, "linear / sinusoidal target classes must be configured when the handle is created");
+    if ((env->ang_targets != 0) != (h->env.ang_targets != 0))
+      return set_err(FW_E_UNSUPPORTED, "attitude_angular targets must be the ones the handle was created with");
     for (int r = 0; r < env->n_rew; r++)
       if (env->rew[r].kind == FW_REW_SUCCESS && !h->o_gflag)
         return set_err(FW_E_UNSUPPORTED, "a success reward factor must be configured when the handle is created");
@@ -3122,8 +3218,8 @@ static int block_info(const fw_handle* h, int32_t block, size_t* off, int* rows,
       if (!h->has_env) return set_err(FW_E_INVALID, "handle has no env (no goal history)");
       *off = h->o_goal; *rows = 4; *esz = 4; return FW_OK;
     case FW_BLK_TARGET_PROPS:
-      if (!h->o_tpr) return set_err(FW_E_INVALID, "handle has no linear / sinusoidal targets");
-      *off = h->o_tpr; *rows = 12; *esz = T_; return FW_OK;
+      if (!h->o_tpr) return set_err(FW_E_INVALID, "handle has no linear / sinusoidal / attitude_angular targets");
+      *off = h->o_tpr; *rows = h->env.ang_targets ? 15 : 12; *esz = T_; return FW_OK;
     default: return set_err(FW_E_INVALID, "unknown state block");
   }
 }
