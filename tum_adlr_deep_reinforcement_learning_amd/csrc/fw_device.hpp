@@ -787,7 +787,7 @@ FW_HD double min_step_at(double t) {
 // still integrating, at the start of a trial step, they continue on lane quads of the same wave
 // (qd::handoff, fw_quad.hpp; ho = the block's handoff slots in LDS) -- the straggler tail at the
 // quad integrator's per-evaluation latency instead of the one-lane one.
-template <typename T, typename C, typename A, bool HO = false>
+template <typename T, typename C, typename A, bool HO = false, bool YF = true>
 FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __restrict__ sy, V2<T>* __restrict__ sf, int stride,
                int& nfev, int& nacc, V2<T>* __restrict__ se = nullptr, void* ho = nullptr) {
   using V = V2<T>;
@@ -799,7 +799,7 @@ FW_HD int rk45(const C& c, const A& a, const StepCtx<T>& X, T* y_io, V2<T>* __re
   // y and f (the accepted state and its derivative) live in LDS slots of this
   // lane (pair p at s[p * stride]); the stage accumulators stay in VGPRs.
   // FW_YF_REGS (fp32): in registers instead (written to the LDS slots before a tail handoff, which reads them there)
-  constexpr bool YFR = FW_YF_REGS && sizeof(T) == 4;  // (fp64: the instances already spill; not measured)
+  constexpr bool YFR = FW_YF_REGS && sizeof(T) == 4 && YF;  // (fp64: the instances already spill; not measured)
   V Yr[YFR ? NP : 1], Fr[YFR ? NP : 1];
   auto Yp = [&](int p) -> V& {
     if constexpr (YFR) return Yr[p];
@@ -1401,7 +1401,7 @@ struct KeepY {  // default: y stays live in registers across the integration
 // Q = 4: the integration runs on the lane quad of the aircraft (fw_quad.hpp; qr = lane in the quad,
 // every lane of the quad returns the same result); Q = 2: on its lane pair (fw_pair.hpp, round 6).
 // HO: the one-lane integration's tail handoff (rk45; ho = the block's qd::HoSlot array in LDS).
-template <int Q = 1, bool HO = false, typename T, typename C, typename A, typename R = KeepY>
+template <int Q = 1, bool HO = false, bool YF = true, typename T, typename C, typename A, typename R = KeepY>
 FW_HD int sim_step_masked(const C& c, const A& a, T* y, T* der, T* cmd, const T* wind, const T* tl, const T* ta, int& nfev,
                           int& nacc, uint32_t& dmask, V2<T>* sy, V2<T>* sf, int stride, R reload = R(), int qr = 0,
                           void* ho = nullptr) {
@@ -1424,7 +1424,7 @@ FW_HD int sim_step_masked(const C& c, const A& a, T* y, T* der, T* cmd, const T*
   for (int i = 0; i < NY; i++) y1[i] = y[i];
   if constexpr (Q == 4) term = qd::rk45_quad(c, a, X, y1, nfev, nacc, qr);
   else if constexpr (Q == 2) term = pr::rk45_pair(c, a, X, y1, nfev, nacc, qr, sy, stride);
-  else term = rk45<T, C, A, HO>(c, a, X, y1, sy, sf, stride, nfev, nacc, FW_ER_LDS ? sf + NP * stride : nullptr, ho);
+  else term = rk45<T, C, A, HO, YF>(c, a, X, y1, sy, sf, stride, nfev, nacc, FW_ER_LDS ? sf + NP * stride : nullptr, ho);
   reload(y);
   if (term < 0) {  // solver failure: y1 = the last accepted sub-step (rk45 wrote Y back), saved as usual
     dmask = DM_SOLVER_FAIL | (term == -2 ? DM_BUDGET : 0u);

@@ -1366,7 +1366,9 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_sim_step(const DevCfg<T>
 // lane 0 alone runs the epilogue.  PREF: the epilogue's loads (rings, goal register, metric state) are
 // issued before the integration, so their latency hides under it instead of following it; that keeps
 // ~90 more values live across the RK loop, which the one-wave quad instances have room for.
-template <typename T, typename C, bool RP = false, int Q = 1, bool PREF = false>
+// YF: the one-lane integrator keeps the accepted y / f in registers (FW_YF_REGS) -- false: in LDS (A/B only; the
+// bits differ, profiles/r06_openloop_yf_ab.log)
+template <typename T, typename C, bool RP = false, int Q = 1, bool PREF = false, bool YF = true>
 __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, const int64_t i, V2<T>* lds,
                                               const T* __restrict__ actions, T* __restrict__ obs_out,
                                               T* __restrict__ rew_out, uint8_t* __restrict__ done_out,
@@ -1485,11 +1487,11 @@ __device__ __forceinline__ void env_step_lane(const C& c, const State<T>& s, con
   int sterm;
   if constexpr (RP) {  // this aircraft's own parameters (simulator parameter randomisation)
     const AeroP<T> ap = aero_from<T>(c, [&](int k) { return s.prm[k * ld + i]; });
-    sterm = sim_step_masked<Q>(c, ap, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
-                               lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i}, qr);
+    sterm = sim_step_masked<Q, false, YF>(c, ap, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
+                                          lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i}, qr);
   } else {
-    sterm = sim_step_masked<Q, HO>(c, c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
-                                   lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i}, qr, ho);
+    sterm = sim_step_masked<Q, HO, YF>(c, c, y, der, cmd, wind, tl, ta, nfev, nacc, dmask, lds + threadIdx.x,
+                                       lds + NP * BLOCK + threadIdx.x, BLOCK, ReloadRow<T>{s.y, ld, i}, qr, ho);
   }
   if (Q > 1 && qr != 0) return;
   if constexpr (!PREF) {
@@ -2052,8 +2054,11 @@ __device__ __forceinline__ void env_step_inl(const C& c, const State<T>& s, cons
                                              const T* actions, T* obs_out, T* rew_out, uint8_t* done_out,
                                              int32_t* term_out, T* tobs_out, T* episode_out, int32_t* stats,
                                              int auto_reset, int qr, void* ho) {
-  env_step_lane<T, C, RP, Q, false>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out, episode_out,
-                                    stats, auto_reset, qr, ho);  // no prefetch: the open loop needs no overlap
+  // no prefetch (the open loop needs no overlap); y / f in registers as in k_env_step, although the open loop alone
+  // runs 7 % faster with them in LDS: the two forms round differently (contraction), and the open loop must equal
+  // K k_env_step launches bit for bit (profiles/r06_openloop_yf_ab.log)
+  env_step_lane<T, C, RP, Q, false, true>(c, s, i, lds, actions, obs_out, rew_out, done_out, term_out, tobs_out,
+                                          episode_out, stats, auto_reset, qr, ho);
 }
 template <typename T, typename C, bool RP, int Q>
 __device__ __noinline__ void env_step_noinl(const C& c, const State<T>& s, const int64_t i, V2<T>* lds,
