@@ -198,6 +198,9 @@ class FixedWingVecEnv(VecEnv):
         # to the host, meant for evaluation with few envs
         self._hists = None
         if record_history:
+            if getattr(self.spec, "ang_targets", False):
+                # history["target"] / ["error"] would carry omega_p / q / r as well (fixed_wing.py:575-580)
+                raise NotImplementedError("record_history with attitude_angular targets")
             from .history import EpisodeHistory
             self._hists = [EpisodeHistory(self.spec) for _ in range(self.num_envs)]
 
