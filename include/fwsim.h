@@ -426,7 +426,8 @@ int fw_env_rollout(fw_handle* h, int32_t n_steps, const void* actions_dev, void*
 
 /* Lanes per aircraft of fw_env_step / fw_sim_step (an execution choice, no reference counterpart):
  * 1 = one lane integrates one aircraft; 4 = a lane quad integrates it (the RHS split by rows,
- * DESIGN.md 3.3): lower latency per aircraft, for shards of few aircraft and the RK45 straggler tail.
+ * DESIGN.md 3.3): lower latency per aircraft, for shards of few aircraft and the RK45 straggler tail;
+ * 2 (round 6) = a lane pair (two virtual quad rows per lane), an option the automatic choice never takes.
  * FW_LANES_AUTO (0, the default) picks by N.  The two agree within rounding, not bit for bit; a config
  * with a wrapped ODE-state variable always runs 1 (fw_set_lanes(h, 4) fails).  fw_get_lanes returns the
  * value the next launch uses; fw_env_rollout runs the same, so it still equals fw_env_step launches.   */

@@ -9,7 +9,7 @@ Its reference parity runs with the other integrators' (``test_gpu_parity.py``: r
   env steps fp32 .................. >= 99 % of the aircraft within 1e-4 per step over 10 steps
   stragglers ...................... stiff sideways states integrate to the same states
   lanes API ....................... fw_set_lanes(2) / FWSIM_LANES=2; refused with a wrapped ODE variable;
-                                    fw_env_rollout runs one lane (no pair instance)
+                                    fw_env_rollout runs the pair too (== K pair env steps bit for bit)
 """
 import numpy as np
 import pytest
@@ -116,18 +116,19 @@ def test_pair_lanes_api():
     w.close()
 
 
-def test_pair_rollout_runs_one_lane():
-    """fw_env_rollout has no pair instance: with lanes 2 it runs the one-lane integrator, equal to one-lane
-    fw_env_step launches bit for bit (fp64, with auto-resets)."""
+@pytest.mark.parametrize("precision", ["float64", "float32"])
+def test_pair_rollout_equals_pair_steps(precision):
+    """fw_env_rollout under lanes 2 runs the pair integrator too (round 6: it had no pair instance and ran one
+    lane, which rounds differently): equal to K pair fw_env_step launches bit for bit, with auto-resets."""
     spec = C.EnvSpec(config_kw={"steps_max": 30}, sim_config_kw={"turbulence": False})
     n, K = 300, 40
-    a, b = _engine(spec, n, "float64", 2), _engine(spec, n, "float64", 1)
+    a, b = _engine(spec, n, precision, 2), _engine(spec, n, precision, 2)
     for e in (a, b):
         e.seed(5)
         e.reset()
     g = torch.Generator(device=DEV)
     g.manual_seed(8)
-    acts = (torch.rand(K, n, 3, generator=g, device=DEV, dtype=torch.float64) * 2.4 - 1.2).contiguous()
+    acts = (torch.rand(K, n, 3, generator=g, device=DEV, dtype=a.dtype) * 2.4 - 1.2).contiguous()
     obs, rew, done, term = a.env_rollout(acts)
     for k in range(K):
         o, r, d, t = b.env_step(acts[k])

@@ -2099,7 +2099,9 @@ __global__ __launch_bounds__(BLOCK, FW_WAVES(Q)) void k_env_rollout(const DevCfg
   const int64_t i = tid / Q;
   const int qr = (int)(tid % Q);
   if (i >= s.n) return;
-  __shared__ V2<T> lds[Q == 1 ? lds_slots<T>() * NP * BLOCK : 1];
+  // (Q = 2: the pair integrator's Y / F / ER, as k_env_step -- fw_set_lanes(2) runs the open loop on pairs too, so
+  // it equals K k_env_step launches bit for bit under every lanes setting)
+  __shared__ V2<T> lds[(Q == 1 ? lds_slots<T>() * NP : Q == 2 ? pr::LDS_PAIRS : 1) * BLOCK];
   __shared__ qd::HoSlot<T> ho[Q == 1 && !RP ? BLOCK : 1];
   const int64_t n = s.n, ow = (int64_t)cfgp->n_obs * cfgp->obs_len;
   for (int k = 0; k < n_steps; k++) {
@@ -2664,7 +2666,7 @@ int env_step(fw_handle* h, hipStream_t st, const void* actions, void* obs, void*
 template <typename T>
 int env_rollout(fw_handle* h, hipStream_t st, int32_t n_steps, const void* actions, void* obs, void* reward,
                 uint8_t* done, int32_t* term, void* tobs, void* episode, int32_t* stats, int32_t auto_reset) {
-  FW_LAUNCH_SPEC_Q(k_env_rollout, false, T, h, st, state_of<T>(h), n_steps, (const T*)actions, (T*)obs, (T*)reward, done,
+  FW_LAUNCH_SPEC_Q(k_env_rollout, true, T, h, st, state_of<T>(h), n_steps, (const T*)actions, (T*)obs, (T*)reward, done,
                    term, (T*)tobs, (T*)episode, stats, auto_reset);
   return check_launch();
 }
