@@ -65,7 +65,7 @@ def algorithmic_bytes_per_env_step(spec, esz=4):
             done flag                                                                   -> u8
     (life: the lifetime step counter the ring slots are indexed by, round 4.)  Not counted: the kernel's
     deliberate re-reads after the RK loop (pre-step state 19, targets 3, actions 3 -- held across the
-    integration they would cost VGPRs), which PMC shows partly served from HBM (profiles/r04_traffic_split.json).
+    integration they would cost VGPRs), which PMC shows partly served from HBM (profiles/r04_traffic_split.json, r06_traffic_split.json).
     """
     act_need = 0
     for o in spec.cfg["observation"]["states"]:
@@ -602,7 +602,7 @@ def main():
                                  "env_steps_per_s_per_gpu": n / (f_early * 1e-3)},
                 "long_window": ({"steps": args.long_window, "kernel_ms": f_long,
                                  "env_steps_per_s": args.envs / (f_long * 1e-3)} if f_long > 0 else None),
-                "isa": "profiles/r05_isa_resources.txt (VGPR / spill counts per kernel instance)"}
+                "isa": "profiles/r06_isa_resources.txt (VGPR / spill counts per kernel instance)"}
 
     esz = 4 if args.precision == "float32" else 8
     rd, wr = algorithmic_bytes_per_env_step(spec, esz)
