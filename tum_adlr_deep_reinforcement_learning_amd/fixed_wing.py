@@ -62,7 +62,14 @@ class FixedWingAircraft:
     @property
     def target(self):
         t = self.engine.get_block(C.FW_BLK_TARGET)[:, 0].double().cpu().numpy()
-        return {"roll": float(t[0]), "pitch": float(t[1]), "Va": float(t[2])}
+        return self._with_ang({"roll": float(t[0]), "pitch": float(t[1]), "Va": float(t[2])})
+
+    def _with_ang(self, d):
+        """+ the attitude_angular targets omega_p / q / r (rows 12..14 of FW_BLK_TARGET_PROPS) when configured."""
+        if getattr(self.spec, "ang_targets", False):
+            o = self.engine.get_block(C.FW_BLK_TARGET_PROPS)[12:15, 0].double().cpu().numpy()
+            d.update({n: float(v) for n, v in zip(C.ANG_TARGETS, o)})
+        return d
 
     @property
     def steps_count(self):
@@ -102,7 +109,7 @@ class FixedWingAircraft:
             if self.engine.metrics is not None:
                 info.update(metric_info(self.engine.metrics[:, 0].cpu().numpy(),
                                         [m["name"] for m in self.cfg.get("metrics", [])]))
-        info["target"] = {"roll": float(t[0]), "pitch": float(t[1]), "Va": float(t[2])}
+        info["target"] = self._with_ang({"roll": float(t[0]), "pitch": float(t[1]), "Va": float(t[2])})
         return o, float(rew[0].item()), d, info
 
     def render(self, mode="plot", **kw):

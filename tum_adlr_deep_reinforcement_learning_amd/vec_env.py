@@ -348,7 +348,12 @@ class FixedWingVecEnv(VecEnv):
         idx = list(self._get_indices(indices))
         if attr_name == "target":
             t = self.engine.get_block(C.FW_BLK_TARGET).cpu().numpy()
-            return [{"roll": float(t[0, i]), "pitch": float(t[1, i]), "Va": float(t[2, i])} for i in idx]
+            out = [{"roll": float(t[0, i]), "pitch": float(t[1, i]), "Va": float(t[2, i])} for i in idx]
+            if getattr(self.spec, "ang_targets", False):  # + omega_p / q / r (FW_BLK_TARGET_PROPS rows 12..14)
+                o = self.engine.get_block(C.FW_BLK_TARGET_PROPS)[12:15].double().cpu().numpy()
+                for d, i in zip(out, idx):
+                    d.update({n: float(o[k, i]) for k, n in enumerate(C.ANG_TARGETS)})
+            return out
         if attr_name == "simulator":
             from .pyfly import SimulatorView
             return [SimulatorView(self.engine, i) for i in idx]
